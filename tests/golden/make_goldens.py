@@ -1,0 +1,362 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE.
+
+Run ONLY in the build container (the reference is not present on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 PYTHONPATH=/root/reference/src:/root/reference \
+        python tests/golden/make_goldens.py
+
+Every fixture is data only (inputs and the reference's outputs, as .npz with no
+pickles).  Weights of the random-init models are NOT stored: they are rebuilt by
+`torch.manual_seed(seed)` + module construction in the reference's parameter order
+(verified bit-identical by the CPU tests through the stored per-parameter checksums).
+Exceptions: the base_ch=16 U-Net fixture stores its full state (its GroupNorm affine
+parameters are perturbed away from the 1/0 default init so the affine path is pinned),
+and one short-trained base_ch=32 score model is stored (trajectory-level parity needs
+a real score; random weights make the 300-step SDE diverge).
+
+Reference call sites reproduced (file:line in /root/reference):
+  CondUNetTiny.forward                 src/toycrystals/models/sde_score_model.py:243-266
+  predict_eps_cfg                      sde_score_model.py:402-423
+  sample_reverse_sde_euler_maruyama    sde_score_model.py:507-569
+  sample_probability_flow_ode          sde_score_model.py:452-504
+  diffusion_loss_eps                   sde_score_model.py:358-399
+  CondVAE / VAE                        src/toycrystals/models/vae.py:8-134
+  kl_stats + VAE loss                  scripts/train_vae.py:17-36,309-312
+  DiffusionPriorFiLM / ddim_sample     src/toycrystals/models/diffusion_prior.py:57-252
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+from toycrystals.models import sde_score_model as ref_sde  # noqa: E402  (reference)
+from toycrystals.models import vae as ref_vae  # noqa: E402
+from toycrystals.models import diffusion_prior as ref_prior  # noqa: E402
+from toycrystals.data import ToyCrystalsDataset  # noqa: E402
+
+
+def sd_checksums(module: torch.nn.Module) -> dict:
+    out = {}
+    for k, v in module.state_dict().items():
+        vv = v.detach().double()
+        out["ck/" + k] = np.array([vv.sum().item(), vv.abs().sum().item(), float(vv.numel())])
+    return out
+
+
+def sd_arrays(module: torch.nn.Module, prefix: str = "w/") -> dict:
+    return {prefix + k: v.detach().cpu().numpy() for k, v in module.state_dict().items()}
+
+
+def save(name: str, **arrays) -> None:
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print(f"  wrote {name}.npz ({os.path.getsize(path) / 1e3:.1f} kB)")
+
+
+def cond_inputs(B: int, n_types: int = 4, null_last: bool = True, seed: int = 7):
+    g = torch.Generator().manual_seed(seed)
+    y_cat = torch.tensor([i % n_types for i in range(B)], dtype=torch.int64)
+    if null_last:
+        y_cat[-1] = n_types  # CFG null token
+    y_cont = torch.zeros(B, 4)
+    y_cont[:, 1] = torch.rand(B, generator=g) * (math.pi / 3)
+    y_cont[:, 0] = torch.rand(B, generator=g)  # exercises the non-rot-only slots too
+    y_cont[:, 3] = torch.rand(B, generator=g)
+    return y_cat, y_cont
+
+
+def perturb_norms(model: torch.nn.Module, seed: int) -> None:
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, (torch.nn.GroupNorm, torch.nn.LayerNorm)):
+                m.weight.copy_(1.0 + 0.2 * torch.randn(m.weight.shape, generator=g))
+                m.bias.copy_(0.2 * torch.randn(m.bias.shape, generator=g))
+
+
+# ---------------------------------------------------------------- score U-Net
+def gen_unet(base_ch: int, B: int, name: str, store_weights: bool, H: int = 64) -> None:
+    torch.manual_seed(0)
+    model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=base_ch)
+    ck = sd_checksums(model)
+    if store_weights:
+        perturb_norms(model, 11)
+    model.eval()
+    g = torch.Generator().manual_seed(3)
+    x_t = torch.randn(B, 1, H, H, generator=g)
+    t = torch.rand(B, generator=g) * 0.99 + 0.005
+    y_cat, y_cont = cond_inputs(B)
+    with torch.no_grad():
+        eps = model(x_t, t, y_cat, y_cont)
+        # intermediate taps for per-layer debugging
+        maps = model._make_maps(t, y_cat, y_cont, H, H)
+        temb = ref_sde.timestep_embedding(t, 128)
+        cemb = model.cond_emb(y_cat, y_cont)
+    extra = sd_arrays(model) if store_weights else {}
+    save(name, x_t=x_t.numpy(), t=t.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(),
+         eps=eps.numpy(), maps=maps[:, :, 0, 0].numpy(), temb=temb.numpy(), cemb=cemb.numpy(),
+         base_ch=np.int64(base_ch), seed=np.int64(0), **ck, **extra)
+
+
+def gen_cfg(name: str) -> None:
+    torch.manual_seed(0)
+    model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=16).eval()
+    g = torch.Generator().manual_seed(5)
+    B = 3
+    x_t = torch.randn(B, 1, 64, 64, generator=g)
+    t = torch.full((B,), 0.37)
+    y_cat, y_cont = cond_inputs(B, null_last=False)
+    with torch.no_grad():
+        eps = ref_sde.predict_eps_cfg(model, x_t, t, y_cat, y_cont, guidance_scale=1.5)
+        eps0 = ref_sde.predict_eps_cfg(model, x_t, t, y_cat, y_cont, guidance_scale=0.0)
+    save(name, x_t=x_t.numpy(), t=t.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(),
+         eps=eps.numpy(), eps0=eps0.numpy(), base_ch=np.int64(16), guidance=np.float64(1.5))
+
+
+def draw_noise(seed: int, shape, n: int):
+    """The reference's draw order with the global CPU RNG seeded at `seed`:
+    x_T = randn(shape) then one randn_like(x) per step (sde_score_model.py:537,557)."""
+    torch.manual_seed(seed)
+    return [torch.randn(shape) for _ in range(n)]
+
+
+def gen_sampler(name: str, sampler: str, base_ch: int, B: int, steps: int, cfg: float, t_end: float,
+                beta_max: float = 30.0, state_dict=None, store_noise: bool = True) -> None:
+    torch.manual_seed(0)
+    model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=base_ch)
+    if state_dict is not None:
+        model.load_state_dict(state_dict)
+    model.eval()
+    sde = ref_sde.VPSDE(beta_min=0.1, beta_max=beta_max)
+    y_cat = torch.tensor([i % 4 for i in range(B)], dtype=torch.int64)
+    y_cont = torch.zeros(B, 4)
+    y_cont[:, 1] = torch.linspace(0.0, math.pi / 3, B)
+    shape = (B, 1, 64, 64)
+    seed = 1234
+    n_draws = steps + 1 if sampler == "sde" else 1
+    noise = draw_noise(seed, shape, n_draws)
+    torch.manual_seed(seed)  # the reference sampler now consumes the identical stream
+    fn = ref_sde.sample_reverse_sde_euler_maruyama if sampler == "sde" else ref_sde.sample_probability_flow_ode
+    t0 = time.time()
+    with torch.no_grad():
+        out = fn(model=model, sde=sde, y_cat=y_cat, y_cont=y_cont, img_shape=shape,
+                 n_steps=steps, guidance_scale=cfg, t_end=t_end)
+    print(f"  {name}: reference sampler {time.time() - t0:.1f}s")
+    # Also record the unclamped x0_hat (the clamp saturates most pixels for weak models).
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        x0_unclamped = _unclamped(model, sde, y_cat, y_cont, shape, steps, cfg, t_end, sampler)
+    arrays = dict(y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), out=out.numpy(),
+                  x0_unclamped=x0_unclamped.numpy(), steps=np.int64(steps), cfg=np.float64(cfg),
+                  t_end=np.float64(t_end), beta_min=np.float64(0.1), beta_max=np.float64(beta_max),
+                  base_ch=np.int64(base_ch), noise_seed=np.int64(seed), B=np.int64(B))
+    if store_noise:
+        arrays["noise"] = torch.stack(noise).numpy()
+    save(name, **arrays)
+
+
+def _unclamped(model, sde, y_cat, y_cont, shape, steps, cfg, t_end, sampler):
+    """Same arithmetic as the reference samplers (sde_score_model.py:452-569), returning
+    x0_hat before the (x+1)/2 map and the clamp.  Calls the reference's own
+    predict_eps_cfg / _probflow_drift so that only the final two lines differ."""
+    B = shape[0]
+    x = torch.randn(shape)
+    u = torch.linspace(0.0, 1.0, steps + 1)
+    ts = t_end + (1.0 - t_end) * (1.0 - u) ** 2
+    for i in range(steps):
+        t = ts[i].expand(B)
+        t_next = ts[i + 1].expand(B)
+        dt = (t_next - t).view(B, 1, 1, 1)
+        if sampler == "sde":
+            beta_t = sde.beta(t).view(B, 1, 1, 1)
+            sigma_t = sde.sigma(t).view(B, 1, 1, 1)
+            gg = torch.sqrt(beta_t)
+            eps_hat = ref_sde.predict_eps_cfg(model, x, t, y_cat, y_cont, guidance_scale=cfg)
+            score = -eps_hat / sigma_t
+            drift = (-0.5 * beta_t * x) - (beta_t * score)
+            z = torch.randn_like(x)
+            x = x + drift * dt + gg * torch.sqrt(torch.abs(dt)) * z
+        else:
+            drift = ref_sde._probflow_drift(model, sde, x, t, y_cat, y_cont, cfg)
+            x_e = x + drift * dt
+            drift_n = ref_sde._probflow_drift(model, sde, x_e, t_next, y_cat, y_cont, cfg)
+            x = x + 0.5 * (drift + drift_n) * dt
+    t_final = ts[-1].expand(B)
+    a = sde.alpha(t_final).view(B, 1, 1, 1)
+    s = sde.sigma(t_final).view(B, 1, 1, 1)
+    eps_hat = ref_sde.predict_eps_cfg(model, x, t_final, y_cat, y_cont, guidance_scale=cfg)
+    return (x - s * eps_hat) / torch.clamp(a, min=1e-6)
+
+
+def train_fixture_model(n_steps: int = 600, B: int = 32, base_ch: int = 32):
+    """Short-train a base_ch=32 score model with the reference's own loss
+    (sde_score_model.py:358-399) + Adam, on the reference's rot-only renderer."""
+    torch.manual_seed(0)
+    model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=base_ch)
+    sde = ref_sde.VPSDE(beta_min=0.1, beta_max=30.0)
+    ds = ToyCrystalsDataset(n_samples=2048, img_size=64, seed=0, rot_only=True)
+    t0 = time.time()
+    xs, ycs, yvs = zip(*[ds[i] for i in range(len(ds))])
+    X, YC, YV = torch.stack(xs), torch.stack(ycs), torch.stack(yvs)
+    print(f"  rendered {len(ds)} images in {time.time() - t0:.1f}s")
+    opt = torch.optim.Adam(model.parameters(), lr=5e-4)
+    g = torch.Generator().manual_seed(99)
+    t0 = time.time()
+    for step in range(n_steps):
+        idx = torch.randint(0, len(ds), (B,), generator=g)
+        loss = ref_sde.diffusion_loss_eps(model, sde, X[idx], YC[idx], YV[idx], p_uncond=0.1)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        if step % 100 == 0 or step == n_steps - 1:
+            print(f"    step {step} loss {loss.item():.4f} ({time.time() - t0:.0f}s)")
+    return model.state_dict(), X[:8], YC[:8], YV[:8]
+
+
+def gen_loss(name: str) -> None:
+    """diffusion_loss_eps with the global RNG seeded: draws u, eps, drop in the reference's
+    order (sde_score_model.py:380-391).  Stores the drawn tensors so no RNG is needed to check."""
+    torch.manual_seed(0)
+    model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=16)
+    sde = ref_sde.VPSDE(0.1, 30.0)
+    g = torch.Generator().manual_seed(21)
+    B = 4
+    x0 = torch.rand(B, 1, 64, 64, generator=g)
+    y_cat, y_cont = cond_inputs(B, null_last=False)
+    torch.manual_seed(77)
+    u = torch.rand((B,))
+    eps = torch.randn((B, 1, 64, 64))
+    drop_u = torch.rand((B,))
+    torch.manual_seed(77)
+    loss = ref_sde.diffusion_loss_eps(model, sde, x0, y_cat, y_cont, p_uncond=0.5, t_power=1.0)
+    loss.backward()
+    grads = {"g/" + k: p.grad.numpy() for k, p in model.named_parameters()
+             if k in ("out.weight", "out.bias", "down1.net.0.weight", "attn.qkv.bias", "cond_emb.cat_emb.weight")}
+    save(name, x0=x0.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), u=u.numpy(), eps=eps.numpy(),
+         drop_u=drop_u.numpy(), p_uncond=np.float64(0.5), loss=np.float64(loss.item()), base_ch=np.int64(16), **grads)
+
+
+def gen_vpsde(name: str) -> None:
+    sde = ref_sde.VPSDE(beta_min=0.1, beta_max=30.0)
+    steps, t_end = 300, 0.005
+    u = torch.linspace(0.0, 1.0, steps + 1)
+    ts = t_end + (1.0 - t_end) * (1.0 - u) ** 2
+    save(name, ts=ts.numpy(), beta=sde.beta(ts).numpy(), alpha=sde.alpha(ts).numpy(),
+         sigma=sde.sigma(ts).numpy(), int_beta=sde.int_beta(ts).numpy(), steps=np.int64(steps),
+         t_end=np.float64(t_end))
+
+
+# ---------------------------------------------------------------- VAE
+def gen_vae(name: str, cond: bool) -> None:
+    torch.manual_seed(0)
+    model = ref_vae.CondVAE(z_dim=32, n_types=4, y_cont_dim=4, cond_drop=0.0) if cond else ref_vae.VAE(z_dim=32)
+    ck = sd_checksums(model)
+    model.eval()
+    g = torch.Generator().manual_seed(4)
+    B = 4
+    x = torch.rand(B, 1, 64, 64, generator=g)
+    y_cat = torch.tensor([0, 1, 2, 3])
+    y_cont = torch.zeros(B, 4)
+    y_cont[:, 1] = torch.rand(B, generator=g)
+    # forward() draws eps = randn_like(std) inside reparameterise (vae.py:57-60)
+    torch.manual_seed(8)
+    rep_eps = torch.randn(B, 32)
+    torch.manual_seed(8)
+    with torch.no_grad():
+        if cond:
+            x_hat, mu, logvar = model(x, y_cat, y_cont)
+        else:
+            x_hat, mu, logvar = model(x)
+    sys.path.insert(0, "/root/reference")
+    from scripts.train_vae import kl_stats  # reference loss helper
+    recon = torch.mean((x_hat - x) ** 2)
+    kl_used, kl_raw = kl_stats(mu, logvar, free_bits=0.05)
+    beta = 3e-4 * min(1.0, (0 + 1) / 5.0)
+    loss = recon + beta * kl_used
+    save(name, x=x.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), rep_eps=rep_eps.numpy(),
+         x_hat=x_hat.numpy(), mu=mu.numpy(), logvar=logvar.numpy(), recon=np.float64(recon.item()),
+         kl_used=np.float64(kl_used.item()), kl_raw=np.float64(kl_raw.item()), loss=np.float64(loss.item()),
+         beta=np.float64(beta), **ck)
+
+
+# ---------------------------------------------------------------- latent prior
+def gen_prior(name: str, width: int, n_blocks: int, store_weights: bool) -> None:
+    torch.manual_seed(0)
+    model = ref_prior.DiffusionPriorFiLM(z_dim=32, n_types=4, y_cont_dim=4, t_emb_dim=64, width=width,
+                                         n_blocks=n_blocks, y_cat_emb_dim=64)
+    ck = sd_checksums(model)
+    if store_weights:
+        perturb_norms(model, 12)
+    model.eval()
+    g = torch.Generator().manual_seed(6)
+    B = 5
+    z_t = torch.randn(B, 32, generator=g)
+    t = torch.tensor([0, 1, 17, 500, 999])
+    y_cat = torch.tensor([0, 1, 2, 3, 1])
+    y_cont = torch.zeros(B, 4)
+    y_cont[:, 1] = torch.rand(B, generator=g)
+    with torch.no_grad():
+        eps = model(z_t, t, y_cat, y_cont)
+        te = ref_prior.timestep_embedding(t, 64)
+    sched = ref_prior.DiffusionSchedule.linear(T=1000, beta_start=1e-4, beta_end=0.05, device=torch.device("cpu"))
+    torch.manual_seed(31)
+    z_init = torch.randn(B, 32)
+    torch.manual_seed(31)
+    with torch.no_grad():
+        z0 = sched.ddim_sample(model, y_cat=y_cat, y_cont=y_cont, n_steps=4, eta=0.0)
+    eps_q = torch.randn(B, 32, generator=g)
+    zq = sched.q_sample(z_t, t, eps_q)
+    extra = sd_arrays(model) if store_weights else {}
+    save(name, z_t=z_t.numpy(), t=t.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), eps=eps.numpy(),
+         temb=te.numpy(), ddim_z_init=z_init.numpy(), ddim_z0=z0.numpy(), ddim_steps=np.int64(4),
+         alpha_bars=sched.alpha_bars.numpy(), q_eps=eps_q.numpy(), q_out=zq.numpy(),
+         width=np.int64(width), n_blocks=np.int64(n_blocks), **ck, **extra)
+
+
+def main() -> int:
+    torch.set_num_threads(8)
+    which = set(sys.argv[1:])
+
+    def want(k):
+        return not which or k in which
+
+    if want("unet"):
+        gen_unet(16, 3, "unet16_b3", store_weights=True)
+        gen_unet(96, 2, "unet96_b2", store_weights=False)
+        gen_unet(32, 2, "unet32_b2_h32", store_weights=False, H=32)
+    if want("cfg"):
+        gen_cfg("cfg16_b3")
+    if want("vpsde"):
+        gen_vpsde("vpsde_grid300")
+    if want("samplers"):
+        gen_sampler("sde16_3step", "sde", 16, 3, 3, 1.5, 0.005)
+        gen_sampler("ode16_2step", "ode", 16, 3, 2, 1.5, 0.005)
+        gen_sampler("sde96_2step_b2", "sde", 96, 2, 2, 1.5, 0.005)
+    if want("trained"):
+        sd, X, YC, YV = train_fixture_model()
+        np.savez_compressed(os.path.join(HERE, "trained32_state.npz"),
+                            **{k: v.numpy() for k, v in sd.items()})
+        print("  wrote trained32_state.npz")
+        gen_sampler("sde32_trained_300", "sde", 32, 4, 300, 1.5, 0.005, state_dict=sd, store_noise=False)
+        gen_sampler("ode32_trained_20", "ode", 32, 4, 20, 1.5, 0.005, state_dict=sd, store_noise=False)
+    if want("loss"):
+        gen_loss("loss16_b4")
+    if want("vae"):
+        gen_vae("condvae_b4", cond=True)
+        gen_vae("vae_b4", cond=False)
+    if want("prior"):
+        gen_prior("prior_w64_b2", 64, 2, store_weights=True)
+        gen_prior("prior_w1024_b8", 1024, 8, store_weights=False)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,546 @@
+// CondUNetTiny forward + sampler step, natively (/root/reference/src/toycrystals/models/
+// sde_score_model.py:170-266 forward, :402-423 CFG, :507-569 reverse SDE, :452-504 PF-ODE).
+//
+// Per U-Net evaluation the host issues ONE call (tcx_unet_eval); the whole reverse-SDE loop is
+// one call too (tcx_sde_sample), so no Python runs between kernels.  Kernels here:
+//   k_cond   — conditioning MLPs (timestep_embedding :17-32, ConditionEmbedding :35-82,
+//              time_mlp/to_*_map :195-202) and the fold of the 16 spatially-constant map
+//              channels of the first conv into a per-(batch, channel) bias (circular padding
+//              keeps a constant map constant, so its 3x3 contribution is sum_taps(w) * value).
+//   k_head   — GroupNorm+SiLU of up1's last conv fused with the out conv's channel reduction:
+//              r[b][tap][p] = sum_ci silu(gn(h))[b,p,ci] * w_out[ci][tap] (a 9-wide GEMV per pixel).
+//   k_step   — out conv's 9-tap circular gather of r + bias, CFG combine eps_u + s(eps_c - eps_u),
+//              and the sampler update (EM / Heun stage / final x0 projection) in one pass;
+//              noise either host-injected or Philox4x32-10 in-kernel.
+#include "common.hpp"
+
+#include <cmath>
+
+namespace tcx {
+namespace {
+
+constexpr float kLn1e4 = 9.210340371976184f;  // math.log(10000.0)
+constexpr float kTwoPi = 6.283185307179586f;
+
+struct CondArgs {
+    const float *time_w1t, *time_b1, *time_w2t, *time_b2, *ttm_wt, *ttm_b, *tcm_wt, *tcm_b, *cat_emb, *cmlp_w1t,
+        *cmlp_b1, *cmlp_w2t, *cmlp_b2, *cout_wt, *cout_b, *map_wsum, *conv_b;
+    int E, n_types, ycd, time_ch, cond_ch, C0;
+};
+
+// One block per (CFG-doubled) batch row.
+__global__ __launch_bounds__(256) void k_cond(CondArgs a, const float* __restrict__ t, int t_per_sample,
+                                              const int64_t* __restrict__ y_cat, const float* __restrict__ y_cont,
+                                              int B, int cfg, float* __restrict__ bias_b) {
+    __shared__ float te[256], h1[256], te2[256], yv[16], g1[256], u[512], ce[256], maps[64];
+    const int bb = blockIdx.x;
+    const int bs = bb % B;
+    const bool null_c = cfg && bb < B;  // first half of a CFG batch = unconditional
+    const int E = a.E, half = E / 2;
+    const int j = threadIdx.x;
+    const float tv = t_per_sample ? t[bs] : t[0];
+    if (j < E) {
+        // timestep_embedding: freqs = exp(-ln(1e4) * k / max(half-1,1)); args = (2*pi*t) * freqs
+        const int k = j < half ? j : j - half;
+        const float fr = expf((-kLn1e4 * (float)k) / (float)(half > 1 ? half - 1 : 1));
+        const float arg = (kTwoPi * tv) * fr;
+        te[j] = j < half ? cosf(arg) : sinf(arg);
+    }
+    if (j < a.ycd) {
+        // y = y_cont; y[1] = sin(theta); y[2] = cos(y[1]).  NB: the reference takes
+        // theta = y[:, 1] as a VIEW, so its cos reads the already-replaced sin(theta)
+        // (sde_score_model.py:75-78): y[2] = cos(sin(theta)).
+        float v = null_c ? 0.f : y_cont[(size_t)bs * a.ycd + j];
+        const float th = null_c ? 0.f : y_cont[(size_t)bs * a.ycd + 1];
+        if (j == 1) v = sinf(th);
+        if (j == 2) v = cosf(sinf(th));
+        yv[j] = v;
+    }
+    __syncthreads();
+    if (j < E) {
+        float s = a.time_b1[j];
+        for (int k = 0; k < E; ++k) s = fmaf(a.time_w1t[k * E + j], te[k], s);
+        h1[j] = silu_f(s);
+        float g = a.cmlp_b1[j];
+        for (int k = 0; k < a.ycd; ++k) g = fmaf(a.cmlp_w1t[k * E + j], yv[k], g);
+        g1[j] = silu_f(g);
+    }
+    __syncthreads();
+    if (j < E) {
+        float s = a.time_b2[j];
+        for (int k = 0; k < E; ++k) s = fmaf(a.time_w2t[k * E + j], h1[k], s);
+        te2[j] = s;
+        float c = a.cmlp_b2[j];
+        for (int k = 0; k < E; ++k) c = fmaf(a.cmlp_w2t[k * E + j], g1[k], c);
+        long long yc = null_c ? a.n_types : y_cat[bs];
+        yc = yc < 0 ? 0 : (yc > a.n_types ? a.n_types : yc);
+        u[j] = silu_f(a.cat_emb[(size_t)yc * E + j]);
+        u[E + j] = silu_f(c);
+    }
+    __syncthreads();
+    if (j < E) {
+        float s = a.cout_b[j];
+        for (int k = 0; k < 2 * E; ++k) s = fmaf(a.cout_wt[k * E + j], u[k], s);
+        ce[j] = s;
+    }
+    __syncthreads();
+    const int nm = a.time_ch + a.cond_ch;
+    if (j < a.time_ch) {
+        float s = a.ttm_b[j];
+        for (int k = 0; k < E; ++k) s = fmaf(a.ttm_wt[k * a.time_ch + j], te2[k], s);
+        maps[j] = s;
+    } else if (j < nm) {
+        const int c = j - a.time_ch;
+        float s = a.tcm_b[c];
+        for (int k = 0; k < E; ++k) s = fmaf(a.tcm_wt[k * a.cond_ch + c], ce[k], s);
+        maps[j] = s;
+    }
+    __syncthreads();
+    for (int co = j; co < a.C0; co += blockDim.x) {
+        float s = a.conv_b[co];
+        for (int c = 0; c < nm; ++c) s = fmaf(maps[c], a.map_wsum[co * nm + c], s);
+        bias_b[(size_t)bb * a.C0 + co] = s;
+    }
+}
+
+// ---------------------------------------------------------------- GN scale/shift (shared)
+__device__ void gn_fold(const double* __restrict__ part, int b, int nsplit, int C, int groups, int HW,
+                        const float* __restrict__ gamma, const float* __restrict__ beta, float* sc, float* sh,
+                        double* gstat) {
+    const int cpg = C / groups;
+    for (int g = threadIdx.x; g < groups; g += blockDim.x) {
+        double s = 0, q = 0;
+        for (int sp = 0; sp < nsplit; ++sp) {
+            const double* src = part + (((size_t)b * nsplit + sp) * C + g * cpg) * 2;
+            for (int c = 0; c < cpg; ++c) {
+                s += src[2 * c];
+                q += src[2 * c + 1];
+            }
+        }
+        const double n = (double)HW * cpg;
+        const double mean = s / n;
+        double var = q / n - mean * mean;
+        var = var < 0 ? 0 : var;
+        gstat[2 * g] = mean;
+        gstat[2 * g + 1] = 1.0 / sqrt(var + 1e-5);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const int g = c / cpg;
+        const float scl = (float)gstat[2 * g + 1] * gamma[c];
+        sc[c] = scl;
+        sh[c] = beta[c] - (float)gstat[2 * g] * scl;
+    }
+    __syncthreads();
+}
+
+// grid (ceil(HW/256), Bt); one thread per pixel.
+__global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int HW, int C, int groups,
+                                              const double* __restrict__ part, int nsplit,
+                                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                                              const float* __restrict__ w_out, float* __restrict__ r) {
+    extern __shared__ __attribute__((aligned(16))) float hs[];  // sc[C] sh[C] w[C*9] gstat
+    float* sc = hs;
+    float* sh = hs + C;
+    float* w = hs + 2 * C;
+    double* gstat = reinterpret_cast<double*>(hs + ((11 * C + 3) & ~3));
+    const int b = blockIdx.y;
+    for (int i = threadIdx.x; i < 9 * C; i += blockDim.x) w[i] = w_out[i];
+    gn_fold(part, b, nsplit, C, groups, HW, gamma, beta, sc, sh, gstat);
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= HW) return;
+    const float* src = h + ((size_t)b * HW + p) * C;
+    float acc[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[k] = 0.f;
+    for (int c = 0; c < C; c += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src + c);
+        const float e0 = silu_f(fmaf(v.x, sc[c], sh[c]));
+        const float e1 = silu_f(fmaf(v.y, sc[c + 1], sh[c + 1]));
+        const float e2 = silu_f(fmaf(v.z, sc[c + 2], sh[c + 2]));
+        const float e3 = silu_f(fmaf(v.w, sc[c + 3], sh[c + 3]));
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            float a = acc[k];
+            a = fmaf(e0, w[(c + 0) * 9 + k], a);
+            a = fmaf(e1, w[(c + 1) * 9 + k], a);
+            a = fmaf(e2, w[(c + 2) * 9 + k], a);
+            a = fmaf(e3, w[(c + 3) * 9 + k], a);
+            acc[k] = a;
+        }
+    }
+    float* dst = r + (size_t)b * 9 * HW + p;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) dst[(size_t)k * HW] = acc[k];
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[1] = (uint32_t)p1;
+        c[3] = (uint32_t)p0;
+        c[0] = n0;
+        c[2] = n2;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+// N(0,1) for element `idx` of draw stream `sid` (Box-Muller on the first two Philox words).
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t sid, uint64_t idx) {
+    uint32_t c[4] = {(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)sid, (uint32_t)(sid >> 32)};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float u1 = ((float)c[0] + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
+    const float u2 = (float)c[1] * 2.3283064365386963e-10f;
+    return sqrtf(-2.0f * logf(u1)) * cosf(kTwoPi * u2);
+}
+
+__global__ void k_randn(float* out, size_t n, uint64_t seed, uint64_t sid) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = philox_normal(seed, sid, i);
+}
+
+// ---------------------------------------------------------------- fused out-conv gather + update
+struct StepArgs {
+    const float* r;       // [Bt][9][HW]
+    float out_b;
+    int B, H, W, cfg;
+    float guidance;
+    int mode;
+    const float* scal;    // current row of the step table
+    const float* x;       // U-Net input image [B][HW] (x_t, or x_e in Heun stage 2)
+    float* x_inout;       // sampler state
+    float* x2;            // Heun x_e
+    float* eps_out;
+    const float* z;
+    uint64_t seed, step;
+};
+
+__device__ __forceinline__ float gather_eps(const float* __restrict__ rb, int HW, int W, int H, int y, int x,
+                                            float ob) {
+    // out[p] = b + sum_{dy,dx} r[tap=(dy*3+dx)][wrap(y+dy-1), wrap(x+dx-1)]
+    float s = ob;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+        const int yy = wrap_idx(y + dy - 1, H);
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+            const int xx = wrap_idx(x + dx - 1, W);
+            s += rb[(size_t)(dy * 3 + dx) * HW + yy * W + xx];
+        }
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(256) void k_step(StepArgs a) {
+    const int HW = a.H * a.W;
+    const size_t n = (size_t)a.B * HW;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int b = (int)(i / HW);
+        const int p = (int)(i - (size_t)b * HW);
+        const int y = p / a.W, x = p - (p / a.W) * a.W;
+        float eps;
+        if (a.cfg) {
+            const float eu = gather_eps(a.r + (size_t)b * 9 * HW, HW, a.W, a.H, y, x, a.out_b);
+            const float ec = gather_eps(a.r + (size_t)(a.B + b) * 9 * HW, HW, a.W, a.H, y, x, a.out_b);
+            eps = eu + a.guidance * (ec - eu);
+        } else {
+            eps = gather_eps(a.r + (size_t)b * 9 * HW, HW, a.W, a.H, y, x, a.out_b);
+        }
+        if (a.mode == 0) {
+            a.eps_out[i] = eps;
+        } else if (a.mode == 1) {
+            // reverse-SDE EM (sde_score_model.py:548-559)
+            const float dt = a.scal[2], beta = a.scal[3], sigma = a.scal[4], g = a.scal[5], sq = a.scal[6];
+            const float xv = a.x_inout[i];
+            const float score = -eps / sigma;
+            const float drift = ((-0.5f * beta) * xv) - (beta * score);
+            const float z = a.z ? a.z[i] : philox_normal(a.seed, a.step + 1, i);
+            a.x_inout[i] = (xv + drift * dt) + (g * sq) * z;
+        } else if (a.mode == 2) {
+            // final projection (sde_score_model.py:562-569)
+            const float sigma = a.scal[4], alpha = a.scal[7];
+            const float x0 = (a.x[i] - sigma * eps) / fmaxf(alpha, 1e-6f);
+            const float v = (x0 + 1.0f) * 0.5f;
+            a.eps_out[i] = fminf(fmaxf(v, 0.f), 1.f);
+        } else if (a.mode == 3) {
+            // Heun stage 1: d = -0.5 b x - 0.5 b score; x_e = x + d dt (sde_score_model.py:444-449,490-491)
+            const float dt = a.scal[2], beta = a.scal[3], sigma = a.scal[4];
+            const float xv = a.x_inout[i];
+            const float score = -eps / sigma;
+            const float d = ((-0.5f * beta) * xv) - ((0.5f * beta) * score);
+            a.eps_out[i] = d;
+            a.x2[i] = xv + d * dt;
+        } else {
+            // Heun stage 2 at t_next on x_e: x += 0.5 (d + d_next) dt  (sde_score_model.py:492-493)
+            const float dt = a.scal[2];
+            const float beta = a.scal[TCX_SCAL + 3], sigma = a.scal[TCX_SCAL + 4];
+            const float xe = a.x[i];
+            const float score = -eps / sigma;
+            const float dn = ((-0.5f * beta) * xe) - ((0.5f * beta) * score);
+            a.x_inout[i] = a.x_inout[i] + (0.5f * (a.eps_out[i] + dn)) * dt;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- workspace plan
+struct Plan {
+    int Bt, H, W, C, C2, P0, P1, P2;
+    float *bias0, *a64, *b64, *h1, *a32, *b32, *h2, *a16, *b16, *qkv, *r;
+    double* gn;
+    size_t bytes;
+};
+
+Plan make_plan(const tcx_unet* net, int Bt, int H, int W, char* base) {
+    Plan p{};
+    p.Bt = Bt; p.H = H; p.W = W;
+    p.C = net->base_ch; p.C2 = 2 * net->base_ch;
+    p.P0 = H * W; p.P1 = (H / 2) * (W / 2); p.P2 = (H / 4) * (W / 4);
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> char* {
+        char* ptr = base ? base + off : nullptr;
+        off += align_up(bytes, 256);
+        return ptr;
+    };
+    const size_t f = sizeof(float);
+    p.bias0 = (float*)take((size_t)Bt * p.C * f);
+    p.a64 = (float*)take((size_t)Bt * p.P0 * p.C * f);
+    p.b64 = (float*)take((size_t)Bt * p.P0 * p.C * f);
+    p.h1 = (float*)take((size_t)Bt * p.P0 * p.C * f);
+    p.a32 = (float*)take((size_t)Bt * p.P1 * p.C2 * f);
+    p.b32 = (float*)take((size_t)Bt * p.P1 * p.C2 * f);
+    p.h2 = (float*)take((size_t)Bt * p.P1 * p.C2 * f);
+    p.a16 = (float*)take((size_t)Bt * p.P2 * p.C2 * f);
+    p.b16 = (float*)take((size_t)Bt * p.P2 * p.C2 * f);
+    p.qkv = (float*)take((size_t)Bt * p.P2 * 3 * p.C2 * f);
+    p.r = (float*)take((size_t)Bt * 9 * p.P0 * f);
+    const int maxsplit = std::max(1, p.P0 / 128);
+    p.gn = (double*)take((size_t)Bt * maxsplit * std::max(p.C2, 2 * p.C2) * 2 * sizeof(double));
+    p.bytes = off;
+    return p;
+}
+
+struct GnRef {
+    int nsplit;
+};
+
+// conv helper: writes GN partials in the epilogue when the tile geometry allows it, else runs
+// the partials kernel afterwards.  Returns nsplit of the partials in `gn`.
+int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2, int Bt, int bmod, int H, int W,
+            int stride, int pad, int ups, const float* bias_b, const float* resid, float* y, double* gn,
+            int* nsplit, hipStream_t st) {
+    const int Hi = ups ? 2 * H : H, Wi = ups ? 2 * W : W;
+    const int Ho = (Hi + 2 * pad - cv.ks) / stride + 1, Wo = (Wi + 2 * pad - cv.ks) / stride + 1;
+    const int HoWo = Ho * Wo;
+    const bool fused = gn && HoWo % 128 == 0;
+    TCX_TRY(tcx_conv2d(x1, x2, Bt, bmod, H, W, C1, C2, cv.w, cv.b, bias_b, resid, y, cv.cout, cv.cout_pad, cv.kpad,
+                       cv.ks, stride, pad, 1, ups, 0, fused ? gn : nullptr, st));
+    if (gn && !fused) {
+        const int ns = std::max(1, HoWo / 512);
+        TCX_TRY(tcx_gn_partials(y, Bt, HoWo, cv.cout, ns, gn, st));
+        *nsplit = ns;
+    } else if (gn) {
+        *nsplit = HoWo / 128;
+    }
+    return TCX_OK;
+}
+
+int groups_of(int ch) {
+    for (int g : {8, 4, 2})
+        if (ch % g == 0) return g;
+    return 1;
+}
+
+int gn_apply(const tcx_unet* net, int idx, float* y, int Bt, int HW, int C, const double* gn, int ns, int silu,
+             hipStream_t st, const float* src = nullptr) {
+    return tcx_gn_apply(src ? src : y, y, Bt, HW, C, groups_of(C), gn, ns, net->gn_w[idx], net->gn_b[idx], 1e-5f,
+                        silu, st);
+}
+
+// The U-Net body (everything up to and including the head partials r).  Input x [B][H][W] (C=1).
+int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const float* t, int t_per_sample,
+              const int64_t* y_cat, const float* y_cont, int cfg, hipStream_t st) {
+    const int Bt = P.Bt, H = P.H, W = P.W, C = P.C, C2 = P.C2;
+    // conditioning -> per-batch first-conv bias
+    {
+        CondArgs a{};
+        a.time_w1t = net->time_w1t; a.time_b1 = net->time_b1; a.time_w2t = net->time_w2t; a.time_b2 = net->time_b2;
+        a.ttm_wt = net->ttm_wt; a.ttm_b = net->ttm_b; a.tcm_wt = net->tcm_wt; a.tcm_b = net->tcm_b;
+        a.cat_emb = net->cat_emb; a.cmlp_w1t = net->cmlp_w1t; a.cmlp_b1 = net->cmlp_b1;
+        a.cmlp_w2t = net->cmlp_w2t; a.cmlp_b2 = net->cmlp_b2; a.cout_wt = net->cout_wt; a.cout_b = net->cout_b;
+        a.map_wsum = net->map_wsum; a.conv_b = net->down1_0.b;
+        a.E = net->emb_dim; a.n_types = net->n_types; a.ycd = net->y_cont_dim;
+        a.time_ch = net->time_ch; a.cond_ch = net->cond_ch; a.C0 = C;
+        hipLaunchKernelGGL(k_cond, dim3(Bt), dim3(256), 0, st, a, t, t_per_sample, y_cat, y_cont, B, cfg, P.bias0);
+        TCX_TRY(check_launch("k_cond"));
+    }
+    int ns = 1;
+    double* gn = P.gn;
+    // down1 (first conv: x_t channel only, maps folded into bias0; bias already inside bias0)
+    {
+        const tcx_conv& c0 = net->down1_0;
+        TCX_TRY(tcx_conv2d(x, nullptr, Bt, B, H, W, 1, 0, c0.w, nullptr, P.bias0, nullptr, P.a64, c0.cout, c0.cout_pad,
+                           c0.kpad, 3, 1, 1, 1, 0, 0, (H * W) % 128 == 0 ? gn : nullptr, st));
+        if ((H * W) % 128 == 0) ns = H * W / 128;
+        else { ns = std::max(1, H * W / 512); TCX_TRY(tcx_gn_partials(P.a64, Bt, H * W, C, ns, gn, st)); }
+    }
+    TCX_TRY(gn_apply(net, 0, P.a64, Bt, P.P0, C, gn, ns, 1, st));
+    TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, 0, nullptr, nullptr, P.h1, gn, &ns, st));
+    TCX_TRY(gn_apply(net, 1, P.h1, Bt, P.P0, C, gn, ns, 1, st));
+    // ds1: 4x4/s2 circular
+    TCX_TRY(conv_gn(net->ds1, P.h1, nullptr, C, 0, Bt, 0, H, W, 2, 1, 0, nullptr, nullptr, P.a32, nullptr, &ns, st));
+    const int H1 = H / 2, W1 = W / 2, H2 = H / 4, W2 = W / 4;
+    // down2
+    TCX_TRY(conv_gn(net->down2_0, P.a32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, 0, nullptr, nullptr, P.b32, gn, &ns, st));
+    TCX_TRY(gn_apply(net, 2, P.b32, Bt, P.P1, C2, gn, ns, 1, st));
+    TCX_TRY(conv_gn(net->down2_1, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, 0, nullptr, nullptr, P.h2, gn, &ns, st));
+    TCX_TRY(gn_apply(net, 3, P.h2, Bt, P.P1, C2, gn, ns, 1, st));
+    // ds2
+    TCX_TRY(conv_gn(net->ds2, P.h2, nullptr, C2, 0, Bt, 0, H1, W1, 2, 1, 0, nullptr, nullptr, P.a16, nullptr, &ns, st));
+    // mid
+    TCX_TRY(conv_gn(net->mid_0, P.a16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, 0, nullptr, nullptr, P.b16, gn, &ns, st));
+    TCX_TRY(gn_apply(net, 4, P.b16, Bt, P.P2, C2, gn, ns, 1, st));
+    TCX_TRY(conv_gn(net->mid_1, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, 0, nullptr, nullptr, P.a16, gn, &ns, st));
+    TCX_TRY(gn_apply(net, 5, P.a16, Bt, P.P2, C2, gn, ns, 1, st));
+    // attention: x_in = a16; b16 = GN(x_in); qkv = 1x1; b16 = attn; a16 = x_in + proj(b16)
+    {
+        const int ns_a = std::max(1, P.P2 / 256);
+        TCX_TRY(tcx_gn_partials(P.a16, Bt, P.P2, C2, ns_a, gn, st));
+        TCX_TRY(gn_apply(net, 6, P.b16, Bt, P.P2, C2, gn, ns_a, 0, st, P.a16));
+        const tcx_conv& q = net->qkv;
+        TCX_TRY(tcx_conv2d(P.b16, nullptr, Bt, 0, H2, W2, C2, 0, q.w, q.b, nullptr, nullptr, P.qkv, q.cout, q.cout_pad,
+                           q.kpad, 1, 1, 0, 1, 0, 0, nullptr, st));
+        TCX_TRY(tcx_attention(P.qkv, P.b16, Bt, P.P2, C2, net->heads, st));
+        const tcx_conv& pr = net->proj;
+        TCX_TRY(tcx_conv2d(P.b16, nullptr, Bt, 0, H2, W2, C2, 0, pr.w, pr.b, nullptr, P.a16, P.a16, pr.cout,
+                           pr.cout_pad, pr.kpad, 1, 1, 0, 1, 0, 0, nullptr, st));
+    }
+    // us2 (bilinear x2 fused into the conv's A load) -> a32 [C2]
+    TCX_TRY(conv_gn(net->us2, P.a16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, 1, nullptr, nullptr, P.a32, nullptr, &ns, st));
+    // up2 on cat[a32, h2]
+    TCX_TRY(conv_gn(net->up2_0, P.a32, P.h2, C2, C2, Bt, 0, H1, W1, 1, 1, 0, nullptr, nullptr, P.b32, gn, &ns, st));
+    TCX_TRY(gn_apply(net, 7, P.b32, Bt, P.P1, C, gn, ns, 1, st));
+    TCX_TRY(conv_gn(net->up2_1, P.b32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, 0, nullptr, nullptr, P.a32, gn, &ns, st));
+    TCX_TRY(gn_apply(net, 8, P.a32, Bt, P.P1, C, gn, ns, 1, st));
+    // us1 -> a64 [C]
+    TCX_TRY(conv_gn(net->us1, P.a32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, 1, nullptr, nullptr, P.a64, nullptr, &ns, st));
+    // up1 on cat[a64, h1]
+    TCX_TRY(conv_gn(net->up1_0, P.a64, P.h1, C, C, Bt, 0, H, W, 1, 1, 0, nullptr, nullptr, P.b64, gn, &ns, st));
+    TCX_TRY(gn_apply(net, 9, P.b64, Bt, P.P0, C, gn, ns, 1, st));
+    TCX_TRY(conv_gn(net->up1_1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, 0, nullptr, nullptr, P.a64, gn, &ns, st));
+    // head: GN(up1.net.4)+SiLU fused with the out conv's channel reduction
+    {
+        const size_t shm = (size_t)((11 * C + 3) & ~3) * sizeof(float) + 2 * 8 * sizeof(double) + 64;
+        const dim3 grid(cdiv(P.P0, 256), Bt);
+        hipLaunchKernelGGL(k_head, grid, dim3(256), shm, st, P.a64, P.P0, C, groups_of(C), gn, ns, net->gn_w[10],
+                           net->gn_b[10], net->out_w, P.r);
+        TCX_TRY(check_launch("k_head"));
+    }
+    return TCX_OK;
+}
+
+int validate(const tcx_unet* net, int B, int H, int W) {
+    TCX_REQUIRE(net, "tcx_unet: null net");
+    TCX_REQUIRE(B > 0 && H % 4 == 0 && W % 4 == 0 && H >= 8 && W >= 8, "tcx_unet: need B>0 and H,W multiples of 4 (>=8)");
+    TCX_REQUIRE(net->base_ch % 4 == 0 && net->base_ch >= 4, "tcx_unet: base_ch must be a multiple of 4");
+    TCX_REQUIRE(net->emb_dim <= 256 && net->emb_dim % 2 == 0, "tcx_unet: emb_dim must be even and <= 256");
+    TCX_REQUIRE(net->time_ch + net->cond_ch <= 64 && net->y_cont_dim >= 3 && net->y_cont_dim <= 16, "tcx_unet: bad cond dims");
+    TCX_REQUIRE((H / 4) * (W / 4) <= 256, "tcx_unet: bottleneck attention supports N <= 256 tokens");
+    return TCX_OK;
+}
+
+int launch_step(const StepArgs& a, hipStream_t st) {
+    const size_t n = (size_t)a.B * a.H * a.W;
+    const int blocks = (int)std::min<size_t>((n + 255) / 256, 16384);
+    hipLaunchKernelGGL(k_step, dim3(blocks), dim3(256), 0, st, a);
+    return check_launch("k_step");
+}
+
+}  // namespace
+}  // namespace tcx
+
+using namespace tcx;
+
+extern "C" size_t tcx_unet_workspace_size(const tcx_unet* net, int Bt, int H, int W) {
+    if (!net) return 0;
+    return make_plan(net, Bt, H, W, nullptr).bytes + 256;
+}
+
+extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, const float* t, int t_per_sample,
+                             const int64_t* y_cat, const float* y_cont, int B, int H, int W, float guidance, int mode,
+                             const float* scal, const float* z, uint64_t seed, uint64_t step, float* x_inout,
+                             float* eps_out, void* ws, size_t ws_bytes, void* stream) {
+    TCX_TRY(validate(net, B, H, W));
+    TCX_REQUIRE(x && t && y_cat && y_cont && ws, "tcx_unet_eval: null pointer");
+    TCX_REQUIRE(mode >= 0 && mode <= 4, "tcx_unet_eval: bad mode");
+    TCX_REQUIRE(mode == 0 || scal, "tcx_unet_eval: sampler modes need the step table row");
+    TCX_REQUIRE((mode != 0 && mode != 2 && mode != 3 && mode != 4) || eps_out, "tcx_unet_eval: eps_out needed");
+    TCX_REQUIRE((mode != 1 && mode != 3 && mode != 4) || x_inout, "tcx_unet_eval: x_inout needed");
+    TCX_REQUIRE(mode != 3 || x2, "tcx_unet_eval: Heun stage 1 needs x2");
+    const int cfg = guidance > 0.f ? 1 : 0;
+    const int Bt = cfg ? 2 * B : B;
+    char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
+    Plan P = make_plan(net, Bt, H, W, base);
+    TCX_REQUIRE(P.bytes + (base - (char*)ws) <= ws_bytes, "tcx_unet_eval: workspace too small (%zu < %zu)", ws_bytes,
+                P.bytes + 256);
+    hipStream_t st = (hipStream_t)stream;
+    TCX_TRY(unet_body(net, P, x, B, t, t_per_sample, y_cat, y_cont, cfg, st));
+    StepArgs a{};
+    a.r = P.r; a.out_b = net->out_b; a.B = B; a.H = H; a.W = W; a.cfg = cfg; a.guidance = guidance; a.mode = mode;
+    a.scal = scal; a.x = x; a.x_inout = x_inout; a.x2 = x2; a.eps_out = eps_out; a.z = z; a.seed = seed; a.step = step;
+    return launch_step(a, st);
+}
+
+extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
+                              int W, int n_steps, float guidance, const float* scal_table, const float* noise,
+                              uint64_t seed, void* ws, size_t ws_bytes, void* stream) {
+    TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_sde_sample: bad args");
+    const size_t img = (size_t)B * H * W;
+    for (int i = 0; i < n_steps; ++i) {
+        const float* row = scal_table + (size_t)i * TCX_SCAL;
+        TCX_TRY(tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 1, row,
+                              noise ? noise + (size_t)i * img : nullptr, seed, (uint64_t)i, x, nullptr, ws, ws_bytes,
+                              stream));
+    }
+    // final projection -> image written over x
+    const float* row = scal_table + (size_t)n_steps * TCX_SCAL;
+    return tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 2, row, nullptr, seed, 0, nullptr,
+                         x, ws, ws_bytes, stream);
+}
+
+extern "C" int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
+                              int W, int n_steps, float guidance, const float* scal_table, void* ws, size_t ws_bytes,
+                              void* stream) {
+    TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_ode_sample: bad args");
+    // Scratch for d and x_e lives at the end of the workspace.
+    const size_t img = (size_t)B * H * W;
+    const size_t need = tcx_unet_workspace_size(net, guidance > 0.f ? 2 * B : B, H, W);
+    TCX_REQUIRE(ws_bytes >= need + 2 * img * sizeof(float) + 512, "tcx_ode_sample: workspace too small");
+    char* tail = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>((char*)ws + need), 256));
+    float* d = reinterpret_cast<float*>(tail);
+    float* xe = d + align_up(img, 64);
+    for (int i = 0; i < n_steps; ++i) {
+        const float* row = scal_table + (size_t)i * TCX_SCAL;
+        TCX_TRY(tcx_unet_eval(net, x, xe, row, 0, y_cat, y_cont, B, H, W, guidance, 3, row, nullptr, 0, 0, x, d, ws,
+                              need, stream));
+        const float* row_n = row + TCX_SCAL;  // t_{i+1}
+        TCX_TRY(tcx_unet_eval(net, xe, nullptr, row_n, 0, y_cat, y_cont, B, H, W, guidance, 4, row, nullptr, 0, 0, x,
+                              d, ws, need, stream));
+    }
+    const float* row = scal_table + (size_t)n_steps * TCX_SCAL;
+    return tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 2, row, nullptr, 0, 0, nullptr, x,
+                         ws, need, stream);
+}
+
+extern "C" int tcx_randn(float* out, size_t n, uint64_t seed, uint64_t stream_id, void* stream) {
+    TCX_REQUIRE(out, "tcx_randn: null pointer");
+    if (n == 0) return TCX_OK;
+    const int blocks = (int)std::min<size_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_randn, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, n, seed, stream_id);
+    return check_launch("tcx_randn");
+}

@@ -1,0 +1,121 @@
+"""ctypes binding of libtcx.so (the C ABI in include/tcx.h).
+
+The library is built in-tree (`make -C vae-diffusion-toy-crystals_amd/csrc`, or
+`__graft_entry__.build()`).  There is NO fallback: if the library is missing or a call fails,
+the caller gets an exception (the product path never routes through a CPU implementation).
+torch is imported first so that libtcx binds to the HIP runtime torch already loaded
+(same soname, libamdhip64.so.7) and shares its device allocations and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before libtcx: shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtcx.so")
+
+c_fp = ctypes.c_void_p
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_size = ctypes.c_size_t
+c_u64 = ctypes.c_uint64
+
+TCX_SCAL = 8
+
+
+class TcxConv(ctypes.Structure):
+    _fields_ = [("w", c_fp), ("b", c_fp), ("cin", c_int), ("cout", c_int), ("ks", c_int), ("kpad", c_int),
+                ("cout_pad", c_int)]
+
+
+_CONV_NAMES = ["down1_0", "down1_1", "ds1", "down2_0", "down2_1", "ds2", "mid_0", "mid_1", "qkv", "proj", "us2",
+               "up2_0", "up2_1", "us1", "up1_0", "up1_1"]
+
+
+class TcxUnet(ctypes.Structure):
+    _fields_ = ([(n, c_int) for n in ("base_ch", "emb_dim", "cond_ch", "time_ch", "n_types", "y_cont_dim", "heads")]
+                + [(n, c_fp) for n in ("time_w1t", "time_b1", "time_w2t", "time_b2", "ttm_wt", "ttm_b", "tcm_wt",
+                                       "tcm_b", "cat_emb", "cmlp_w1t", "cmlp_b1", "cmlp_w2t", "cmlp_b2", "cout_wt",
+                                       "cout_b", "map_wsum")]
+                + [(n, TcxConv) for n in _CONV_NAMES]
+                + [("out_w", c_fp), ("out_b", c_float), ("gn_w", c_fp * 11), ("gn_b", c_fp * 11)])
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "tcx_last_error": (ctypes.c_char_p, []),
+    "tcx_version": (c_int, []),
+    "tcx_prof_enable": (c_int, [c_int]),
+    "tcx_prof_read": (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
+                              ctypes.POINTER(ctypes.c_double)]),
+    "tcx_conv2d": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp, c_fp, c_int,
+                           c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp]),
+    "tcx_pack_conv_weight": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_pack_convT_weight": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_convT2x": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_gn_partials": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),
+    "tcx_gn_apply": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_int, c_fp, c_fp, c_float, c_int, c_fp]),
+    "tcx_upsample2x": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_attention": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_unet_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int]),
+    "tcx_unet_eval": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_fp, c_fp, c_int, c_int, c_int,
+                              c_float, c_int, c_fp, c_fp, c_u64, c_u64, c_fp, c_fp, c_fp, c_size, c_fp]),
+    "tcx_sde_sample": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_float, c_fp,
+                               c_fp, c_u64, c_fp, c_size, c_fp]),
+    "tcx_ode_sample": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_float, c_fp,
+                               c_fp, c_size, c_fp]),
+    "tcx_randn": (c_int, [c_fp, c_size, c_u64, c_u64, c_fp]),
+    "tcx_linear": (c_int, [c_fp, c_int, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_layernorm_film": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_float, c_fp]),
+}
+
+_lib = None
+
+
+class TcxError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libtcx.so once (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise TcxError(f"libtcx.so not found at {LIB_PATH}: build it with "
+                           f"`make -C vae-diffusion-toy-crystals_amd/csrc` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().tcx_last_error().decode(errors="replace")
+        raise TcxError(f"{what or 'libtcx'} failed (rc={rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu_tensor(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise TcxError(f"{name} must be a GPU tensor (device 'cuda' is the MI355X under ROCm); "
+                       f"got {t.device}. This build has no CPU path.")

@@ -1,0 +1,474 @@
+"""MI355X-native drop-in for toycrystals.models.sde_score_model.
+
+Mirrors /root/reference/src/toycrystals/models/sde_score_model.py: same class and function
+names, constructor signatures, attributes, submodule names (so `state_dict` keys and the seeded
+default initialisation are identical: `torch.manual_seed(s); CondUNetTiny(...)` gives the same
+weights as the reference) and the same error behaviour.  The arithmetic runs in libtcx (HIP,
+gfx950): the nn.Modules here are parameter containers only.  Tensors must live on the GPU
+(`device="cuda"` is the MI355X under PyTorch-ROCm); there is no CPU path.
+
+Reference map:
+  timestep_embedding :17-32, ConditionEmbedding :35-82, _gn_groups/_ConvBlock :89-111,
+  SelfAttention2d :114-167, CondUNetTiny :170-266, VPSDE :273-298, save_sde_samples :301-355,
+  diffusion_loss_eps :358-399, predict_eps_cfg :402-423, _probflow_drift :426-449,
+  sample_probability_flow_ode :452-504, sample_reverse_sde_euler_maruyama :507-569.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import _lib
+from .._lib import TCX_SCAL, TcxConv, TcxUnet, check, lib, ptr, require_gpu_tensor, stream_ptr
+
+
+# =========================
+# Embeddings (host-side helpers with the reference's semantics)
+# =========================
+
+def timestep_embedding(t: torch.Tensor, dim: int) -> torch.Tensor:
+    """Continuous-time sinusoidal embedding [cos, sin] of 2*pi*t (sde_score_model.py:17-32).
+    Kept as a plain tensor function for API parity; the U-Net computes it inside k_cond."""
+    half = dim // 2
+    freqs = torch.exp(-math.log(10_000.0) * torch.arange(half, device=t.device, dtype=torch.float32)
+                      / max(half - 1, 1))
+    args = (2.0 * math.pi) * t.float().unsqueeze(1) * freqs.unsqueeze(0)
+    emb = torch.cat([torch.cos(args), torch.sin(args)], dim=1)
+    if dim % 2 == 1:
+        emb = torch.nn.functional.pad(emb, (0, 1))
+    return emb
+
+
+class ConditionEmbedding(nn.Module):
+    """Parameter container of (y_cat, y_cont) -> emb (sde_score_model.py:35-82).
+    Evaluated by libtcx k_cond (null token = n_types for CFG)."""
+
+    def __init__(self, n_types: int, y_cont_dim: int, emb_dim: int) -> None:
+        super().__init__()
+        self.n_types = int(n_types)
+        self.y_cont_dim = int(y_cont_dim)
+        self.emb_dim = int(emb_dim)
+        if self.y_cont_dim < 3:
+            raise ValueError("theta_sincos requires y_cont_dim >= 3 (needs indices 1 and 2).")
+        self.cat_emb = nn.Embedding(self.n_types + 1, emb_dim)
+        self.cont_mlp = nn.Sequential(nn.Linear(self.y_cont_dim, emb_dim), nn.SiLU(), nn.Linear(emb_dim, emb_dim))
+        self.out = nn.Sequential(nn.SiLU(), nn.Linear(emb_dim * 2, emb_dim))
+
+
+def _gn_groups(ch: int) -> int:
+    for g in (8, 4, 2):
+        if ch % g == 0:
+            return g
+    return 1
+
+
+class _ConvBlock(nn.Module):
+    def __init__(self, in_ch: int, out_ch: int) -> None:
+        super().__init__()
+        g = _gn_groups(out_ch)
+        self.net = nn.Sequential(
+            nn.Conv2d(in_ch, out_ch, kernel_size=3, padding=1, padding_mode="circular"),
+            nn.GroupNorm(num_groups=g, num_channels=out_ch),
+            nn.SiLU(),
+            nn.Conv2d(out_ch, out_ch, kernel_size=3, padding=1, padding_mode="circular"),
+            nn.GroupNorm(num_groups=g, num_channels=out_ch),
+            nn.SiLU(),
+        )
+
+
+class SelfAttention2d(nn.Module):
+    def __init__(self, ch: int, num_heads: int = 4) -> None:
+        super().__init__()
+        if ch % num_heads != 0:
+            raise ValueError(f"ch ({ch}) must be divisible by num_heads ({num_heads})")
+        self.ch = int(ch)
+        self.num_heads = int(num_heads)
+        self.head_dim = self.ch // self.num_heads
+        self.norm = nn.GroupNorm(num_groups=_gn_groups(self.ch), num_channels=self.ch)
+        self.qkv = nn.Conv2d(self.ch, 3 * self.ch, kernel_size=1, padding=0)
+        self.proj = nn.Conv2d(self.ch, self.ch, kernel_size=1, padding=0)
+
+
+def _round_up(v: int, a: int) -> int:
+    return (v + a - 1) // a * a
+
+
+def _cout_pad(cout: int) -> int:
+    return _round_up(cout, 32)
+
+
+class _UNetPack:
+    """Device-resident packed weights + the tcx_unet descriptor for one CondUNetTiny."""
+
+    def __init__(self, model: "CondUNetTiny", device: torch.device) -> None:
+        self.device = device
+        self.keep = []  # tensors referenced by raw pointers in the descriptor
+        L = lib()
+        st = stream_ptr(device)
+        net = TcxUnet()
+        net.base_ch = model.base_ch
+        net.emb_dim = model.cond_emb.emb_dim
+        net.cond_ch = model.cond_ch
+        net.time_ch = model.time_ch
+        net.n_types = model.n_types
+        net.y_cont_dim = model.y_cont_dim
+        net.heads = model.attn.num_heads
+
+        def dev(t: torch.Tensor) -> int:
+            t = t.detach().to(device=device, dtype=torch.float32).contiguous()
+            self.keep.append(t)
+            return t.data_ptr()
+
+        def lin_t(m: nn.Linear):
+            return dev(m.weight.detach().t()), dev(m.bias)
+
+        net.time_w1t, net.time_b1 = lin_t(model.time_mlp[0])
+        net.time_w2t, net.time_b2 = lin_t(model.time_mlp[2])
+        net.ttm_wt, net.ttm_b = lin_t(model.to_time_map)
+        net.tcm_wt, net.tcm_b = lin_t(model.to_cond_map)
+        ce = model.cond_emb
+        net.cat_emb = dev(ce.cat_emb.weight)
+        net.cmlp_w1t, net.cmlp_b1 = lin_t(ce.cont_mlp[0])
+        net.cmlp_w2t, net.cmlp_b2 = lin_t(ce.cont_mlp[2])
+        net.cout_wt, net.cout_b = lin_t(ce.out[1])
+
+        def conv(m: nn.Conv2d, weight: Optional[torch.Tensor] = None) -> TcxConv:
+            w = (m.weight if weight is None else weight).detach().to(device=device, dtype=torch.float32).contiguous()
+            cout, cin, ks, _ = w.shape
+            kpad = _round_up(ks * ks * cin, 32)
+            cpad = _cout_pad(cout)
+            wpk = torch.empty((cpad, kpad), device=device, dtype=torch.float32)
+            check(L.tcx_pack_conv_weight(w.data_ptr(), wpk.data_ptr(), cout, cin, ks, cpad, kpad, st),
+                  "pack conv weight")
+            self.keep.extend([w, wpk])
+            return TcxConv(wpk.data_ptr(), dev(m.bias), cin, cout, ks, kpad, cpad)
+
+        w0 = model.down1.net[0].weight.detach()
+        net.down1_0 = conv(model.down1.net[0], w0[:, :1])
+        net.map_wsum = dev(w0[:, 1:].to(torch.float64).sum(dim=(2, 3)).to(torch.float32))
+        net.down1_1 = conv(model.down1.net[3])
+        net.ds1 = conv(model.ds1)
+        net.down2_0 = conv(model.down2.net[0])
+        net.down2_1 = conv(model.down2.net[3])
+        net.ds2 = conv(model.ds2)
+        net.mid_0 = conv(model.mid.net[0])
+        net.mid_1 = conv(model.mid.net[3])
+        net.qkv = conv(model.attn.qkv)
+        net.proj = conv(model.attn.proj)
+        net.us2 = conv(model.us2_conv)
+        net.up2_0 = conv(model.up2.net[0])
+        net.up2_1 = conv(model.up2.net[3])
+        net.us1 = conv(model.us1_conv)
+        net.up1_0 = conv(model.up1.net[0])
+        net.up1_1 = conv(model.up1.net[3])
+        wo = model.out.weight.detach()
+        net.out_w = dev(wo[0].reshape(wo.shape[1], 9))
+        net.out_b = float(model.out.bias.detach().float().cpu()[0])
+        norms = [model.down1.net[1], model.down1.net[4], model.down2.net[1], model.down2.net[4], model.mid.net[1],
+                 model.mid.net[4], model.attn.norm, model.up2.net[1], model.up2.net[4], model.up1.net[1],
+                 model.up1.net[4]]
+        for i, gnm in enumerate(norms):
+            net.gn_w[i] = dev(gnm.weight)
+            net.gn_b[i] = dev(gnm.bias)
+        self.net = net
+        self.ws = None
+
+    def workspace(self, Bt: int, H: int, W: int, extra: int = 0) -> Tuple[torch.Tensor, int]:
+        need = int(lib().tcx_unet_workspace_size(ctypes.byref(self.net), Bt, H, W)) + extra
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self.ws, self.ws.numel()
+
+
+class _EpsNoGrad(torch.autograd.Function):
+    """Forward through libtcx; the HIP backward (dgrad/wgrad with circular halos) is a later
+    milestone, so differentiating through it raises instead of silently falling back."""
+
+    @staticmethod
+    def forward(ctx, eps, *params):  # noqa: D401
+        return eps
+
+    @staticmethod
+    def backward(ctx, grad):
+        raise NotImplementedError("CondUNetTiny backward on MI355X is not implemented yet (forward/sampling only)")
+
+
+class CondUNetTiny(nn.Module):
+    """Tiny conditional U-Net predicting eps_hat = eps_theta(x_t, t, c) (sde_score_model.py:170-266)."""
+
+    def __init__(self, n_types: int, y_cont_dim: int, base_ch: int = 32, emb_dim: int = 128, cond_ch: int = 8,
+                 time_ch: int = 8) -> None:
+        super().__init__()
+        self.n_types = int(n_types)
+        self.y_cont_dim = int(y_cont_dim)
+        self.base_ch = int(base_ch)
+        self.cond_ch = int(cond_ch)
+        self.time_ch = int(time_ch)
+        self.cond_emb = ConditionEmbedding(n_types=self.n_types, y_cont_dim=self.y_cont_dim, emb_dim=emb_dim)
+        self.time_mlp = nn.Sequential(nn.Linear(emb_dim, emb_dim), nn.SiLU(), nn.Linear(emb_dim, emb_dim))
+        self.to_cond_map = nn.Linear(emb_dim, cond_ch)
+        self.to_time_map = nn.Linear(emb_dim, time_ch)
+        in_ch = 1 + cond_ch + time_ch
+        self.down1 = _ConvBlock(in_ch, base_ch)
+        self.ds1 = nn.Conv2d(base_ch, base_ch, kernel_size=4, stride=2, padding=1, padding_mode="circular")
+        self.down2 = _ConvBlock(base_ch, base_ch * 2)
+        self.ds2 = nn.Conv2d(base_ch * 2, base_ch * 2, kernel_size=4, stride=2, padding=1, padding_mode="circular")
+        self.mid = _ConvBlock(base_ch * 2, base_ch * 2)
+        self.attn = SelfAttention2d(base_ch * 2, num_heads=4)
+        self.us2 = nn.Upsample(scale_factor=2, mode="bilinear", align_corners=False)
+        self.us2_conv = nn.Conv2d(base_ch * 2, base_ch * 2, kernel_size=3, padding=1, padding_mode="circular")
+        self.up2 = _ConvBlock(base_ch * 4, base_ch)
+        self.us1 = nn.Upsample(scale_factor=2, mode="bilinear", align_corners=False)
+        self.us1_conv = nn.Conv2d(base_ch, base_ch, kernel_size=3, padding=1, padding_mode="circular")
+        self.up1 = _ConvBlock(base_ch * 2, base_ch)
+        self.out = nn.Conv2d(base_ch, 1, kernel_size=3, padding=1, padding_mode="circular")
+        self._pack: Optional[_UNetPack] = None
+        self._pack_key = None
+
+    # ---------------------------------------------------------------- packing
+    def _weights_key(self, device):
+        return (device,) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+
+    def tcx_pack(self, device: Optional[torch.device] = None) -> _UNetPack:
+        """(Re)pack the weights for libtcx when they changed (new storage or in-place update)."""
+        device = torch.device(device) if device is not None else next(self.parameters()).device
+        if device.type != "cuda":
+            raise _lib.TcxError("CondUNetTiny runs on the MI355X only: move the model and inputs to 'cuda'")
+        key = self._weights_key(device)
+        if self._pack is None or self._pack_key != key:
+            with torch.no_grad():
+                self._pack = _UNetPack(self, device)
+            self._pack_key = key
+        return self._pack
+
+    # ---------------------------------------------------------------- forward
+    def _check_inputs(self, x_t, t, y_cat, y_cont):
+        require_gpu_tensor(x_t, "x_t")
+        if x_t.dim() != 4 or x_t.shape[1] != 1:
+            raise ValueError(f"x_t must be [B,1,H,W], got {tuple(x_t.shape)}")
+        B = x_t.shape[0]
+        t = torch.as_tensor(t, device=x_t.device).float().expand(B).contiguous()
+        y_cat = y_cat.to(device=x_t.device, dtype=torch.int64).contiguous()
+        y_cont = y_cont.to(device=x_t.device, dtype=torch.float32).contiguous()
+        return x_t.float().contiguous(), t, y_cat, y_cont
+
+    def forward(self, x_t: torch.Tensor, t: torch.Tensor, y_cat: torch.Tensor, y_cont: torch.Tensor) -> torch.Tensor:
+        x, t, y_cat, y_cont = self._check_inputs(x_t, t, y_cat, y_cont)
+        eps = _eval_eps(self, x, t, 1, y_cat, y_cont, 0.0)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            eps = _EpsNoGrad.apply(eps, *[p for p in self.parameters() if p.requires_grad])
+        return eps
+
+
+def _eval_eps(model: CondUNetTiny, x, t, t_per_sample, y_cat, y_cont, guidance: float) -> torch.Tensor:
+    B, _, H, W = x.shape
+    pk = model.tcx_pack(x.device)
+    Bt = 2 * B if guidance > 0.0 else B
+    ws, nbytes = pk.workspace(Bt, H, W)
+    eps = torch.empty_like(x)
+    check(lib().tcx_unet_eval(ctypes.byref(pk.net), ptr(x), None, ptr(t), t_per_sample, ptr(y_cat), ptr(y_cont), B, H,
+                              W, float(guidance), 0, None, None, 0, 0, None, ptr(eps), ptr(ws), nbytes,
+                              stream_ptr(x.device)), "tcx_unet_eval")
+    return eps
+
+
+# =========================
+# OU/VP-SDE + loss + sampler
+# =========================
+
+@dataclass(frozen=True)
+class VPSDE:
+    """VP SDE dx = -0.5 beta(t) x dt + sqrt(beta(t)) dW with linear beta (sde_score_model.py:273-298)."""
+    beta_min: float = 0.1
+    beta_max: float = 20.0
+
+    def beta(self, t: torch.Tensor) -> torch.Tensor:
+        return self.beta_min + t * (self.beta_max - self.beta_min)
+
+    def int_beta(self, t: torch.Tensor) -> torch.Tensor:
+        return self.beta_min * t + 0.5 * (self.beta_max - self.beta_min) * (t ** 2)
+
+    def alpha(self, t: torch.Tensor) -> torch.Tensor:
+        return torch.exp(-0.5 * self.int_beta(t))
+
+    def sigma(self, t: torch.Tensor) -> torch.Tensor:
+        a = self.alpha(t)
+        return torch.sqrt(torch.clamp(1.0 - a * a, min=1e-8))
+
+
+def step_table(sde: VPSDE, n_steps: int, t_end: float) -> torch.Tensor:
+    """Per-step scalars [n_steps+1, 8] = {t, t_next, dt, beta, sigma, sqrt(beta), sqrt|dt|, alpha},
+    computed on the host with the reference's fp32 torch formulas (quadratic grid
+    sde_score_model.py:540-541, per-step scalars :545-550, final projection :562-565), so the
+    device update sees exactly the reference's scalar values."""
+    u = torch.linspace(0.0, 1.0, n_steps + 1)
+    ts = t_end + (1.0 - t_end) * (1.0 - u) ** 2
+    t_next = torch.cat([ts[1:], ts[-1:]])
+    dt = t_next - ts
+    beta = sde.beta(ts)
+    tab = torch.stack([ts, t_next, dt, beta, sde.sigma(ts), torch.sqrt(beta), torch.sqrt(torch.abs(dt)),
+                       sde.alpha(ts)], dim=1).to(torch.float32)
+    assert tab.shape[1] == TCX_SCAL
+    return tab.contiguous()
+
+
+@torch.no_grad()
+def save_sde_samples(model: CondUNetTiny, sde: VPSDE, out_path: str, device: torch.device, n: int = 36,
+                     theta_max: float = math.pi / 3.0, steps: int = 200, cfg: float = 0.0, t_end: float = 1e-3,
+                     sampler: str = "ode") -> None:
+    """Save a 6x6 grid: cycle lattice types, sweep theta in [0, pi/3] (sde_score_model.py:301-355)."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+
+    model.eval()
+    y_cat = torch.tensor([i % model.n_types for i in range(n)], device=device, dtype=torch.int64)
+    thetas = torch.linspace(0.0, theta_max, steps=n, device=device)
+    y_cont = torch.zeros((n, model.y_cont_dim), device=device)
+    y_cont[:, 1] = thetas
+    kw = dict(model=model, sde=sde, y_cat=y_cat, y_cont=y_cont, img_shape=(n, 1, 64, 64), n_steps=steps,
+              guidance_scale=cfg, t_end=t_end)
+    if sampler == "ode":
+        x = sample_probability_flow_ode(**kw)
+    elif sampler == "sde":
+        x = sample_reverse_sde_euler_maruyama(**kw)
+    else:
+        raise ValueError(f"Unknown sampler='{sampler}'. Use 'ode' or 'sde'.")
+    fig, axes = plt.subplots(6, 6, figsize=(6, 6))
+    fig.suptitle(f"{sampler} | steps={steps} | cfg={cfg:.2f} | t_end={t_end:g}", fontsize=10)
+    for i, ax in enumerate(axes.flat):
+        ax.imshow(x[i, 0].cpu(), cmap="gray", vmin=0.0, vmax=1.0)
+        ax.axis("off")
+    fig.tight_layout()
+    fig.savefig(out_path, dpi=200)
+    plt.close(fig)
+
+
+def diffusion_loss_eps(model: CondUNetTiny, sde: VPSDE, x0: torch.Tensor, y_cat: torch.Tensor,
+                       y_cont: torch.Tensor, p_uncond: float = 0.1, t_power: float = 1.0) -> torch.Tensor:
+    """Eps-prediction denoising loss with CFG condition dropout (sde_score_model.py:358-399).
+    Same RNG draw order as the reference (u, eps, drop).  Forward value only this round."""
+    device = x0.device
+    B = x0.shape[0]
+    x0 = x0 * 2.0 - 1.0
+    u = torch.rand((B,), device=device)
+    t = u ** float(t_power)
+    eps = torch.randn_like(x0)
+    a = sde.alpha(t).view(B, 1, 1, 1)
+    s = sde.sigma(t).view(B, 1, 1, 1)
+    x_t = a * x0 + s * eps
+    if p_uncond > 0.0:
+        drop = (torch.rand((B,), device=device) < p_uncond)
+        if drop.any():
+            y_cat = y_cat.clone()
+            y_cont = y_cont.clone()
+            y_cat[drop] = model.n_types
+            y_cont[drop] = 0.0
+    eps_hat = model(x_t, t, y_cat, y_cont)
+    return torch.mean((eps_hat - eps) ** 2)
+
+
+@torch.no_grad()
+def predict_eps_cfg(model: CondUNetTiny, x_t: torch.Tensor, t: torch.Tensor, y_cat: torch.Tensor,
+                    y_cont: torch.Tensor, guidance_scale: float) -> torch.Tensor:
+    """eps = eps_u + s (eps_c - eps_u) (sde_score_model.py:402-423).  Both halves run as ONE
+    2B-batch U-Net evaluation (null token n_types, y_cont = 0 first) combined in the head."""
+    x, t, y_cat, y_cont = model._check_inputs(x_t, t, y_cat, y_cont)
+    return _eval_eps(model, x, t, 1, y_cat, y_cont, float(guidance_scale) if guidance_scale > 0.0 else 0.0)
+
+
+def _probflow_drift(model, sde, x, t, y_cat, y_cont, guidance_scale):
+    """PF-ODE drift -0.5 beta x - 0.5 beta score, score = -eps/sigma (sde_score_model.py:426-449)."""
+    B = x.shape[0]
+    beta_t = sde.beta(t).view(B, 1, 1, 1)
+    sigma_t = sde.sigma(t).view(B, 1, 1, 1)
+    eps_hat = predict_eps_cfg(model, x, t, y_cat, y_cont, guidance_scale=guidance_scale)
+    score = -eps_hat / sigma_t
+    return -0.5 * beta_t * x - 0.5 * beta_t * score
+
+
+def _sampler_prologue(model, y_cat, y_cont, img_shape, t_end):
+    device = y_cat.device
+    B, C, H, W = img_shape
+    assert C == 1
+    t_end = float(t_end)
+    if not (0.0 < t_end < 1.0):
+        raise ValueError(f"t_end must be in (0,1), got {t_end}")
+    require_gpu_tensor(y_cat, "y_cat")
+    return device, B, H, W, t_end, y_cat.to(torch.int64).contiguous(), y_cont.to(torch.float32).contiguous()
+
+
+def host_noise(shape, n_draws: int, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """Noise in the reference's CPU draw order: x_T = randn(shape), then one randn_like per step
+    (sde_score_model.py:537,557).  Parity mode: copy this to the device and pass as `noise`."""
+    return torch.stack([torch.randn(shape, generator=generator) for _ in range(n_draws)])
+
+
+@torch.no_grad()
+def sample_reverse_sde_euler_maruyama(model: CondUNetTiny, sde: VPSDE, y_cat: torch.Tensor, y_cont: torch.Tensor,
+                                      img_shape: Tuple[int, int, int, int], n_steps: int = 200,
+                                      guidance_scale: float = 0.0, t_end: float = 1e-3, *,
+                                      noise: Optional[torch.Tensor] = None,
+                                      seed: Optional[int] = None) -> torch.Tensor:
+    """Reverse-time SDE via Euler-Maruyama, t: 1 -> t_end (sde_score_model.py:507-569).
+
+    The whole loop runs natively (tcx_sde_sample): per step ONE fused CFG-doubled U-Net
+    evaluation whose head applies the EM update in place.
+    Noise: `noise` [n_steps+1, B, 1, H, W] (x_T then one z per step, e.g. host_noise(...)) for
+    bit-reproducible parity runs; otherwise x_T and z come from in-kernel Philox4x32-10 keyed by
+    `seed` (default: drawn from torch's global CPU generator, so torch.manual_seed governs it).
+    """
+    device, B, H, W, t_end, y_cat, y_cont = _sampler_prologue(model, y_cat, y_cont, img_shape, t_end)
+    pk = model.tcx_pack(device)
+    tab = step_table(sde, n_steps, t_end).to(device)
+    L = lib()
+    st = stream_ptr(device)
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    x = torch.empty((B, 1, H, W), device=device, dtype=torch.float32)
+    if noise is not None:
+        noise = noise.to(device=device, dtype=torch.float32).contiguous()
+        if noise.shape[0] != n_steps + 1 or noise[0].numel() != x.numel():
+            raise ValueError(f"noise must be [n_steps+1, B, 1, H, W], got {tuple(noise.shape)}")
+        x.copy_(noise[0].view_as(x))
+        zs = noise[1:]
+    else:
+        check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
+        zs = None
+    g = float(guidance_scale) if guidance_scale > 0.0 else 0.0
+    ws, nbytes = pk.workspace(2 * B if g > 0 else B, H, W)
+    check(L.tcx_sde_sample(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g, ptr(tab),
+                           ptr(zs) if zs is not None else None, seed, ptr(ws), nbytes, st), "tcx_sde_sample")
+    return x
+
+
+@torch.no_grad()
+def sample_probability_flow_ode(model: CondUNetTiny, sde: VPSDE, y_cat: torch.Tensor, y_cont: torch.Tensor,
+                                img_shape: Tuple[int, int, int, int], n_steps: int = 200,
+                                guidance_scale: float = 0.0, t_end: float = 1e-3, *,
+                                x_init: Optional[torch.Tensor] = None,
+                                seed: Optional[int] = None) -> torch.Tensor:
+    """Deterministic probability-flow ODE with Heun steps (sde_score_model.py:452-504)."""
+    device, B, H, W, t_end, y_cat, y_cont = _sampler_prologue(model, y_cat, y_cont, img_shape, t_end)
+    pk = model.tcx_pack(device)
+    tab = step_table(sde, n_steps, t_end).to(device)
+    L = lib()
+    st = stream_ptr(device)
+    x = torch.empty((B, 1, H, W), device=device, dtype=torch.float32)
+    if x_init is not None:
+        x.copy_(x_init.to(device=device, dtype=torch.float32).view_as(x))
+    else:
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
+    g = float(guidance_scale) if guidance_scale > 0.0 else 0.0
+    img_bytes = B * H * W * 4
+    ws, nbytes = pk.workspace(2 * B if g > 0 else B, H, W, extra=2 * img_bytes + 1024)
+    check(L.tcx_ode_sample(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g, ptr(tab),
+                           ptr(ws), nbytes, st), "tcx_ode_sample")
+    return x
