@@ -58,11 +58,18 @@ int tcx_prof_read(double* total_ms, long long* launches, double* flops);
  *   act: epilogue activation 0 none, 1 ReLU, 2 sigmoid, 3 SiLU (vae.py:20-26).
  *   gn_stats: if non-NULL, per-(batch, m-tile, channel) partial sums {sum, sumsq} of the
  *     output (fp64) are written for the following GroupNorm: [Bt][nsplit][Cout][2],
- *     nsplit = ceil(Ho*Wo/128).  */
+ *     nsplit = ceil(Ho*Wo/128).
+ *   pro_scale/shift{1,2}: optional fused GroupNorm+SiLU prologue per source:
+ *     x -> silu(x * scale[b][c] + shift[b][c]) (tables [Bt][C] from tcx_gn_finalize), applied
+ *     once per element as the staged tile is written to LDS — the normalised tensor never
+ *     exists in HBM (sde_score_model.py:103-107 feeding the next conv).  Needs Cin, C1 % 32 == 0,
+ *     circular padding, Ho*Wo % 128 == 0.  */
 int tcx_conv2d(const float* x1, const float* x2, int Bt, int bmod, int H, int W, int C1, int C2,
                const float* wpk, const float* bias, const float* bias_b, const float* resid,
                float* y, int Cout, int cout_pad, int kpad, int ks, int stride, int pad,
-               int circular, int upsample, int act, double* gn_stats, void* stream);
+               int circular, int upsample, int act, double* gn_stats, const float* pro_scale1,
+               const float* pro_shift1, const float* pro_scale2, const float* pro_shift2,
+               void* stream);
 
 /* Pack an nn.Conv2d weight [Cout][Cin][ks][ks] into the implicit-GEMM layout above. */
 int tcx_pack_conv_weight(const float* w, float* wpk, int Cout, int Cin, int ks, int cout_pad,
@@ -87,8 +94,20 @@ int tcx_gn_apply(const float* x, float* y, int Bt, int HW, int C, int groups, co
                  int nsplit, const float* gamma, const float* beta, float eps, int silu,
                  void* stream);
 
-/* Bilinear x2 upsample, align_corners=False (nn.Upsample, sde_score_model.py:217,221). */
-int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, int C, void* stream);
+/* GroupNorm finalize: partials -> per-(batch, channel) scale = rstd*gamma, shift = beta - mean*scale
+ * ([Bt][C] each), consumed by the fused prologues of tcx_conv2d / tcx_upsample2x. */
+int tcx_gn_finalize(const double* part, int Bt, int HW, int C, int groups, int nsplit,
+                    const float* gamma, const float* beta, float eps, float* scale, float* shift,
+                    void* stream);
+
+/* GroupNorm apply from finalize tables: y = x*scale[b][c] + shift[b][c] (+ SiLU); in place OK. */
+int tcx_gn_apply_tab(const float* x, float* y, int Bt, int HW, int C, const float* scale,
+                     const float* shift, int silu, void* stream);
+
+/* Bilinear x2 upsample, align_corners=False (nn.Upsample, sde_score_model.py:217,221); optional
+ * fused GN+SiLU of the source (scale/shift tables as above, or NULL). */
+int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, int C, const float* scale,
+                   const float* shift, void* stream);
 
 /* Multi-head self-attention core of SelfAttention2d (sde_score_model.py:150-160):
  * qkv [Bt,N,3C] (1x1-conv output, channel order [q,k,v], head-major inside each),

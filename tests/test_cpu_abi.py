@@ -43,7 +43,7 @@ def test_validation_errors_without_gpu():
     from toycrystals_amd import _lib
     L = _lib.lib()
     rc = L.tcx_conv2d(None, None, 1, 0, 8, 8, 4, 0, None, None, None, None, None, 4, 32, 64, 3, 1, 1, 1, 0, 0, None,
-                      None)
+                      None, None, None, None, None)
     assert rc == -1
     assert b"null pointer" in L.tcx_last_error()
     rc = L.tcx_attention(None, None, 1, 4096, 192, 4, None)

@@ -53,7 +53,7 @@ def pack(w):
 
 
 def run_conv(x, w, b, stride, pad, circular, x2=None, ups=False, act=0, bias_b=None, resid=None, bmod=0, gn=False,
-             Bt=None):
+             Bt=None, pro1=None, pro2=None):
     """x, x2 NCHW numpy; returns NCHW numpy (and GN partials)."""
     B, C1, H, W = x.shape
     C2 = 0 if x2 is None else x2.shape[1]
@@ -71,11 +71,14 @@ def run_conv(x, w, b, stride, pad, circular, x2=None, ups=False, act=0, bias_b=N
     rd = dev(nhwc(resid)) if resid is not None else None
     nsplit = -(-Ho * Wo // 128)
     gnd = torch.zeros((Bt, nsplit, co, 2), dtype=torch.float64, device="cuda") if gn else None
+    p1 = [dev(a) for a in pro1] if pro1 is not None else [None, None]
+    p2 = [dev(a) for a in pro2] if pro2 is not None else [None, None]
+    pp = [t.data_ptr() if t is not None else None for t in p1 + p2]
     chk(L().tcx_conv2d(xd.data_ptr(), x2d.data_ptr() if x2d is not None else None, Bt, bmod, H, W, C1, C2,
                        wpk.data_ptr(), bd.data_ptr() if bd is not None else None,
                        bbd.data_ptr() if bbd is not None else None, rd.data_ptr() if rd is not None else None,
                        y.data_ptr(), co, cpad, kpad, ks, stride, pad, int(circular), int(ups), act,
-                       gnd.data_ptr() if gnd is not None else None, st()))
+                       gnd.data_ptr() if gnd is not None else None, *pp, st()))
     torch.cuda.synchronize()
     out = nchw(y.cpu().numpy())
     return (out, gnd.cpu().numpy()) if gn else out
@@ -200,8 +203,54 @@ def test_upsample():
     x = rng.standard_normal((2, 24, 16, 16))
     xd = dev(nhwc(x))
     y = torch.empty((2, 32, 32, 24), device="cuda")
-    chk(L().tcx_upsample2x(xd.data_ptr(), y.data_ptr(), 2, 16, 16, 24, st()))
+    chk(L().tcx_upsample2x(xd.data_ptr(), y.data_ptr(), 2, 16, 16, 24, None, None, st()))
     close(nchw(y.cpu().numpy()), nn_np.upsample_bilinear2x(x))
+
+
+def test_upsample_with_gn_silu_prologue():
+    x = rng.standard_normal((2, 24, 16, 16)) * 2 + 0.3
+    sc = rng.standard_normal((2, 24))
+    sh = rng.standard_normal((2, 24))
+    ref = nn_np.upsample_bilinear2x(nn_np.silu(x * sc[:, :, None, None] + sh[:, :, None, None]))
+    xd, scd, shd = dev(nhwc(x)), dev(sc), dev(sh)
+    y = torch.empty((2, 32, 32, 24), device="cuda")
+    chk(L().tcx_upsample2x(xd.data_ptr(), y.data_ptr(), 2, 16, 16, 24, scd.data_ptr(), shd.data_ptr(), st()))
+    close(nchw(y.cpu().numpy()), ref)
+
+
+@pytest.mark.parametrize("C1,C2,Co,H,ks,stride,which", [(96, 0, 96, 64, 3, 1, 1), (192, 192, 96, 32, 3, 1, 2),
+                                                        (96, 96, 96, 64, 3, 1, 3), (96, 0, 96, 64, 4, 2, 1)])
+def test_conv_fused_gn_silu_prologue(C1, C2, Co, H, ks, stride, which):
+    """silu(x*scale[b,c] + shift[b,c]) applied to source 1 and/or 2 while staging (which: bit mask)."""
+    B = 2
+    x1 = rng.standard_normal((B, C1, H, H)) * 1.5 + 0.2
+    x2 = rng.standard_normal((B, C2, H, H)) if C2 else None
+    w = rng.standard_normal((Co, C1 + C2, ks, ks)) / np.sqrt((C1 + C2) * ks * ks)
+    b = rng.standard_normal(Co)
+    t1 = (rng.standard_normal((B, C1)), rng.standard_normal((B, C1))) if which & 1 else None
+    t2 = (rng.standard_normal((B, C2)), rng.standard_normal((B, C2))) if (which & 2 and C2) else None
+    s1 = nn_np.silu(x1 * t1[0][:, :, None, None] + t1[1][:, :, None, None]) if t1 else x1
+    s2 = None if x2 is None else (nn_np.silu(x2 * t2[0][:, :, None, None] + t2[1][:, :, None, None]) if t2 else x2)
+    xin = s1 if s2 is None else np.concatenate([s1, s2], 1)
+    ref = nn_np.conv2d(xin, w, b, stride=stride, padding=1, mode="circular")
+    close(run_conv(x1, w, b, stride, 1, True, x2=x2, pro1=t1, pro2=t2), ref, rel=5e-5)
+
+
+def test_gn_finalize_tables():
+    C, HW, groups = 96, 4096, 8
+    x = rng.standard_normal((3, C, 64, 64)) * 2 + 0.7
+    gm, bt = rng.standard_normal(C), rng.standard_normal(C)
+    xd = dev(nhwc(x))
+    part = torch.empty((3, 8, C, 2), dtype=torch.float64, device="cuda")
+    chk(L().tcx_gn_partials(xd.data_ptr(), 3, HW, C, 8, part.data_ptr(), st()))
+    sc = torch.empty((3, C), device="cuda")
+    sh = torch.empty((3, C), device="cuda")
+    gmd, btd = dev(gm), dev(bt)
+    chk(L().tcx_gn_finalize(part.data_ptr(), 3, HW, C, groups, 8, gmd.data_ptr(), btd.data_ptr(), 1e-5,
+                            sc.data_ptr(), sh.data_ptr(), st()))
+    torch.cuda.synchronize()
+    got = x * sc.cpu().numpy()[:, :, None, None] + sh.cpu().numpy()[:, :, None, None]
+    close(got, nn_np.group_norm(x, groups, gm, bt))
 
 
 @pytest.mark.parametrize("B,C,N,heads", [(2, 192, 256, 4), (3, 32, 256, 4), (2, 64, 64, 4)])

@@ -58,10 +58,67 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 }
 
 __device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
+// SiLU with the hardware exp2 / reciprocal (a few ulp; used in staged prologues)
+__device__ __forceinline__ float silu_fast(float v) { return __fdividef(v, 1.0f + __expf(-v)); }
 
 __device__ __forceinline__ int wrap_idx(int i, int n) {
     i = i < 0 ? i + n : i;
     return i >= n ? i - n : i;
 }
+
+// Per-channel scale/shift of batch b into LDS from the partials [b][nsplit][C][2].
+// Stage 1: one thread per channel sums its nsplit partials (independent, coalesced loads);
+// stage 2: one thread per group sums its cpg channel totals.  (A group-per-thread loop over
+// nsplit*cpg dependent loads was ~80 us of serialised latency per block.)
+__device__ inline void gn_scale_shift(const double* __restrict__ part, int b, int nsplit, int C, int groups, int HW,
+                               const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                               float* sc, float* sh, double* gstat, double* csum) {
+    const int cpg = C / groups;
+    const int tid = threadIdx.x;
+    const double* pb = part + (size_t)b * nsplit * C * 2;
+    for (int c = tid; c < C; c += blockDim.x) {
+        double a = 0, q = 0;
+#pragma unroll 8
+        for (int sp = 0; sp < nsplit; ++sp) {
+            const double2 v = *reinterpret_cast<const double2*>(pb + ((size_t)sp * C + c) * 2);
+            a += v.x;
+            q += v.y;
+        }
+        csum[2 * c] = a;
+        csum[2 * c + 1] = q;
+    }
+    __syncthreads();
+    for (int g = tid; g < groups; g += blockDim.x) {
+        double a = 0, q = 0;
+        for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+            a += csum[2 * c];
+            q += csum[2 * c + 1];
+        }
+        const double n = (double)HW * cpg;
+        const double mean = a / n;
+        double var = q / n - mean * mean;
+        var = var < 0 ? 0 : var;
+        gstat[2 * g] = mean;
+        gstat[2 * g + 1] = 1.0 / sqrt(var + (double)eps);
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += blockDim.x) {
+        const int g = c / cpg;
+        const float rstd = (float)gstat[2 * g + 1];
+        const float mean = (float)gstat[2 * g];
+        const float gm = gamma ? gamma[c] : 1.f;
+        const float bt = beta ? beta[c] : 0.f;
+        const float scl = rstd * gm;
+        sc[c] = scl;
+        sh[c] = bt - mean * scl;
+    }
+    __syncthreads();
+}
+
+inline size_t gn_fold_lds_bytes(int C, int groups) {
+    return (size_t)2 * ((C + 3) & ~3) * sizeof(float) + (size_t)2 * groups * sizeof(double) +
+           (size_t)2 * C * sizeof(double) + 64;
+}
+
 
 }  // namespace tcx

@@ -24,6 +24,10 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// 16 zero bytes: masked-out im2col elements load from here (an address select, not a value
+// select after the load, which hipcc lowers through scratch memory).
+__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
+
 constexpr int BM = 128;
 constexpr int BK = 32;
 constexpr int LDA = 36;  // padded LDS row (floats)
@@ -48,7 +52,12 @@ struct ConvParams {
     double* gn;    // [Bt][nsplit][Cout][2] or null
     int nsplit;
     int n_nblk;
+    // GroupNorm+SiLU prologue of each source: x -> silu(x * scale[b][c] + shift[b][c]) applied
+    // when the staged chunk is written to LDS (tables from tcx_gn_finalize; null = raw source)
+    const float *sc1, *sh1, *sc2, *sh2;
 };
+
+constexpr int PRO_MAXC = 384;  // max channels per source for the fused GN prologue
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
@@ -68,11 +77,18 @@ __device__ __forceinline__ void bilin_axis(int d, int n, int& i0, int& i1, float
     l0 = 1.f - l1;
 }
 
-template <int NT, int MODE>  // MODE 0: float4 loads (Cin%4==0); 1: scalar (any Cin); 2: upsample
+// MODE 0: float4 loads, per-lane (tap, ci) decode (Cin % 4 == 0)
+// MODE 1: scalar loads, any Cin (the Cin = 1 first convs)
+// MODE 2: float4 loads through a bilinear x2 upsample of the source
+// MODE 3: float4 loads, chunk-uniform (SGPR) decode: Cin % 32 == 0 and C1 % 32 == 0, so a
+//         32-deep K chunk is one tap of one source (every 3x3/4x4 layer of the U-Net)
+template <int NT, int MODE, bool CIRC, bool PRO>
 __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     constexpr int BN = 32 * NT;
     __shared__ __attribute__((aligned(16))) float As[2][BM * LDA];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDA];
+    // fused GN prologue tables of this tile's image: [src1 scale, src1 shift, src2 scale, src2 shift]
+    __shared__ __attribute__((aligned(16))) float Tr[PRO ? 4 * PRO_MAXC : 4];
 
     const int nwg = gridDim.x;
     const int tile = xcd_remap(blockIdx.x, nwg);
@@ -106,87 +122,110 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     float4 ra[4];
     float4 rb[NT];
 
-    auto load_chunk = [&](int c) {
-        // ---- A (im2col gather)
-        if constexpr (MODE == 1) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float v[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int k = c * BK + k4 * 4 + e;
-                    const int tap = k / p.Cin;
-                    const int ci = k - tap * p.Cin;
-                    const int dy = tap / p.ks, dx = tap - (tap / p.ks) * p.ks;
-                    int yy = piy[i] + dy, xx = pix[i] + dx;
-                    bool ok = pv[i] && tap < p.ks * p.ks;
-                    if (p.circular) {
-                        yy = wrap_idx(yy, p.Hi);
-                        xx = wrap_idx(xx, p.Wi);
-                    } else {
-                        ok = ok && yy >= 0 && yy < p.Hi && xx >= 0 && xx < p.Wi;
-                    }
-                    v[e] = ok ? p.x1[(size_t)(pbase[i] + yy * p.W + xx) * p.C1 + ci] : 0.f;
-                }
-                ra[i] = make_float4(v[0], v[1], v[2], v[3]);
-            }
+    // ---- per-chunk decode of k -> (tap, source, channel offset)
+    struct Dec {
+        const float* src;
+        int cs, cc, dy, dx;
+        bool kval;
+        int tsel;  // which prologue table (0 = source 1, 2 = source 2)
+        bool tr;   // apply the GN+SiLU prologue to this chunk
+        int cb;    // chunk's first channel within its source (MODE 3)
+    };
+    auto decode = [&](int c) -> Dec {
+        Dec d;
+        if constexpr (MODE == 3) {
+            const int kc = c * BK;                 // uniform: SGPR arithmetic
+            int tap = kc / p.Cin;
+            const int ci0 = kc - tap * p.Cin;
+            d.kval = tap < p.ks * p.ks;
+            tap = d.kval ? tap : 0;
+            d.dy = tap / p.ks;
+            d.dx = tap - d.dy * p.ks;
+            const bool s1 = ci0 < p.C1;
+            d.src = s1 ? p.x1 : p.x2;
+            d.cs = s1 ? p.C1 : p.C2;
+            d.cc = (s1 ? ci0 : ci0 - p.C1) + k4 * 4;
+            d.tsel = s1 ? 0 : 2;
+            d.tr = s1 ? p.sc1 != nullptr : p.sc2 != nullptr;
+            d.cb = s1 ? ci0 : ci0 - p.C1;
         } else {
             const int k = c * BK + k4 * 4;
-            const int tap = k / p.Cin;
+            int tap = k / p.Cin;
             const int ci = k - tap * p.Cin;
-            const bool kval = tap < p.ks * p.ks;
-            const int dy = tap / p.ks, dx = tap - (tap / p.ks) * p.ks;
-            const float* src;
-            int cs, cc;
-            if (ci < p.C1) {
-                src = p.x1; cs = p.C1; cc = ci;
-            } else {
-                src = p.x2; cs = p.C2; cc = ci - p.C1;
-            }
+            d.kval = tap < p.ks * p.ks;
+            tap = d.kval ? tap : 0;
+            d.dy = tap / p.ks;
+            d.dx = tap - d.dy * p.ks;
+            const bool s1 = ci < p.C1;
+            d.src = s1 ? p.x1 : p.x2;
+            d.cs = s1 ? p.C1 : p.C2;
+            d.cc = s1 ? ci : ci - p.C1;
+            d.tsel = 0;
+            d.tr = false;
+            d.cb = 0;
+        }
+        return d;
+    };
+
+    // A gather for pixel row i (all loads unconditional: masked elements read g_zero4; a
+    // `cond ? load : 0` value select makes hipcc branch/wait per element or go through scratch).
+    auto load_a = [&](const Dec& d, int c, int i) {
+        constexpr bool circ = CIRC;
+        if constexpr (MODE == 1) {
+            float v[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                int yy = piy[i] + dy, xx = pix[i] + dx;
-                bool ok = pv[i] && kval;
-                if (p.circular) {
-                    yy = wrap_idx(yy, p.Hi);
-                    xx = wrap_idx(xx, p.Wi);
-                } else {
-                    ok = ok && yy >= 0 && yy < p.Hi && xx >= 0 && xx < p.Wi;
-                }
-                if constexpr (MODE == 0) {
-                    ra[i] = ok ? ld4(src + (size_t)(pbase[i] + yy * p.W + xx) * cs + cc)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-                } else {  // MODE 2: read through the bilinear x2 upsample of a HxW source
-                    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (ok) {
-                        int y0, y1, x0, x1;
-                        float ly0, ly1, lx0, lx1;
-                        bilin_axis(yy, p.H, y0, y1, ly0, ly1);
-                        bilin_axis(xx, p.W, x0, x1, lx0, lx1);
-                        const float* b0 = src + (size_t)pbase[i] * cs + cc;
-                        const float4 a00 = ld4(b0 + (size_t)(y0 * p.W + x0) * cs);
-                        const float4 a01 = ld4(b0 + (size_t)(y0 * p.W + x1) * cs);
-                        const float4 a10 = ld4(b0 + (size_t)(y1 * p.W + x0) * cs);
-                        const float4 a11 = ld4(b0 + (size_t)(y1 * p.W + x1) * cs);
-                        float4 r0 = make_float4(lx0 * a00.x, lx0 * a00.y, lx0 * a00.z, lx0 * a00.w);
-                        r0 = f4_fma(lx1, a01, r0);
-                        float4 r1 = make_float4(lx0 * a10.x, lx0 * a10.y, lx0 * a10.z, lx0 * a10.w);
-                        r1 = f4_fma(lx1, a11, r1);
-                        acc = make_float4(ly0 * r0.x, ly0 * r0.y, ly0 * r0.z, ly0 * r0.w);
-                        acc = f4_fma(ly1, r1, acc);
-                    }
-                    ra[i] = acc;
-                }
+            for (int e = 0; e < 4; ++e) {
+                const int k = c * BK + k4 * 4 + e;
+                int tap = k / p.Cin;
+                const int ci = k - tap * p.Cin;
+                const bool kval = tap < p.ks * p.ks;
+                tap = kval ? tap : 0;
+                const int dy = tap / p.ks, dx = tap - (tap / p.ks) * p.ks;
+                const int yr = piy[i] + dy, xr = pix[i] + dx;
+                const bool inb = yr >= 0 && yr < p.Hi && xr >= 0 && xr < p.Wi;
+                const int yy = circ ? wrap_idx(yr, p.Hi) : min(max(yr, 0), p.Hi - 1);
+                const int xx = circ ? wrap_idx(xr, p.Wi) : min(max(xr, 0), p.Wi - 1);
+                const bool ok = pv[i] && kval && (circ || inb);
+                const float* a = p.x1 + (size_t)(pbase[i] + yy * p.W + xx) * p.C1 + ci;
+                v[e] = *(ok ? a : g_zero4);
+            }
+            ra[i] = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+            const int yr = piy[i] + d.dy, xr = pix[i] + d.dx;
+            const bool inb = yr >= 0 && yr < p.Hi && xr >= 0 && xr < p.Wi;
+            const int yy = circ ? wrap_idx(yr, p.Hi) : min(max(yr, 0), p.Hi - 1);
+            const int xx = circ ? wrap_idx(xr, p.Wi) : min(max(xr, 0), p.Wi - 1);
+            const bool ok = pv[i] && d.kval && (circ || inb);
+            if constexpr (MODE != 2) {
+                const float* a = d.src + (size_t)(pbase[i] + yy * p.W + xx) * d.cs + d.cc;
+                ra[i] = ld4(ok ? a : g_zero4);
+            } else {
+                int y0, y1, x0, x1;
+                float ly0, ly1, lx0, lx1;
+                bilin_axis(yy, p.H, y0, y1, ly0, ly1);
+                bilin_axis(xx, p.W, x0, x1, lx0, lx1);
+                const float* b0 = d.src + (size_t)pbase[i] * d.cs + d.cc;
+                const float4 a00 = ld4(b0 + (size_t)(y0 * p.W + x0) * d.cs);
+                const float4 a01 = ld4(b0 + (size_t)(y0 * p.W + x1) * d.cs);
+                const float4 a10 = ld4(b0 + (size_t)(y1 * p.W + x0) * d.cs);
+                const float4 a11 = ld4(b0 + (size_t)(y1 * p.W + x1) * d.cs);
+                float4 r0 = make_float4(lx0 * a00.x, lx0 * a00.y, lx0 * a00.z, lx0 * a00.w);
+                r0 = f4_fma(lx1, a01, r0);
+                float4 r1 = make_float4(lx0 * a10.x, lx0 * a10.y, lx0 * a10.z, lx0 * a10.w);
+                r1 = f4_fma(lx1, a11, r1);
+                float4 acc = make_float4(ly0 * r0.x, ly0 * r0.y, ly0 * r0.z, ly0 * r0.w);
+                acc = f4_fma(ly1, r1, acc);
+                ra[i] = make_float4(ok ? acc.x : 0.f, ok ? acc.y : 0.f, ok ? acc.z : 0.f, ok ? acc.w : 0.f);
             }
         }
-        // ---- B (packed weights, zero padded to kpad x cout_pad)
+    };
+    auto load_b = [&](int c) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
             const int co = n0 + prow + 32 * j;
             rb[j] = ld4(p.w + (size_t)co * p.kpad + c * BK + k4 * 4);
         }
     };
-
     auto store_chunk = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -205,65 +244,138 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     const int li = lane & 31;
     const int lh = lane >> 5;
 
-    load_chunk(0);
-    store_chunk(0);
+    if constexpr (PRO) {
+        const int bimg = m0 / p.HoWo;  // host guarantees Ho*Wo % 128 == 0: one image per tile
+        for (int c = tid; c < p.C1; c += 256) {
+            Tr[c] = p.sc1 ? p.sc1[(size_t)bimg * p.C1 + c] : 1.f;
+            Tr[PRO_MAXC + c] = p.sh1 ? p.sh1[(size_t)bimg * p.C1 + c] : 0.f;
+        }
+        for (int c = tid; c < p.C2; c += 256) {
+            Tr[2 * PRO_MAXC + c] = p.sc2 ? p.sc2[(size_t)bimg * p.C2 + c] : 1.f;
+            Tr[3 * PRO_MAXC + c] = p.sh2 ? p.sh2[(size_t)bimg * p.C2 + c] : 0.f;
+        }
+        __syncthreads();
+    }
+    {
+        const Dec d0 = decode(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) load_a(d0, 0, i);
+        load_b(0);
+        store_chunk(0);
+    }
     __syncthreads();
 
+    // MFMA fragments, double-buffered in registers: group g (4 k-steps) computes from one set
+    // while the reads of group g+1 are in flight into the other.
+    float4 fa0, fa1, fb0[NT], fb1[NT];
+    // GN+SiLU prologue (PRO): each A element of the LDS tile is read by exactly one lane, so the
+    // source's silu(x*scale + shift) is applied to the fragment right after its read — the VALU
+    // then issues in the shadow of the previous group's MFMAs (same work as a store-time pass).
+    auto read_frags = [&](int buf, int g, const Dec& dc, float4& fa, float4 (&fb)[NT]) {
+        const float* Ab = &As[buf][(wv * 32 + li) * LDA + lh * 16 + g * 4];
+        const float* Bb = &Bs[buf][li * LDA + lh * 16 + g * 4];
+        fa = ld4(Ab);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) fb[n] = ld4(Bb + n * 32 * LDA);
+        if constexpr (PRO) {
+            if (dc.tr) {
+                const int ch = dc.cb + lh * 16 + g * 4;
+                const float4 sc = *reinterpret_cast<const float4*>(&Tr[dc.tsel * PRO_MAXC + ch]);
+                const float4 sh = *reinterpret_cast<const float4*>(&Tr[(dc.tsel + 1) * PRO_MAXC + ch]);
+                fa.x = silu_fast(fmaf(fa.x, sc.x, sh.x));
+                fa.y = silu_fast(fmaf(fa.y, sc.y, sh.y));
+                fa.z = silu_fast(fmaf(fa.z, sc.z, sh.z));
+                fa.w = silu_fast(fmaf(fa.w, sc.w, sh.w));
+            }
+        }
+    };
+    auto mfma_group = [&](const float4& a, const float4 (&b)[NT]) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b[n].x, acc[n], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b[n].y, acc[n], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b[n].z, acc[n], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[n].w, acc[n], 0, 0, 0);
+    };
+
+    Dec dc = decode(0);  // decode of the chunk being computed
+    read_frags(0, 0, dc, fa0, fb0);
     for (int c = 0; c < p.nchunks; ++c) {
         const int cur = c & 1;
-        const bool more = c + 1 < p.nchunks;
-        if (more) load_chunk(c + 1);
-        const float* Ab = &As[cur][(wv * 32 + li) * LDA + lh * 16];
-        const float* Bb = &Bs[cur][li * LDA + lh * 16];
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            const float4 a = ld4(Ab + s4 * 4);
-            float4 b[NT];
-#pragma unroll
-            for (int n = 0; n < NT; ++n) b[n] = ld4(Bb + n * 32 * LDA + s4 * 4);
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b[n].x, acc[n], 0, 0, 0);
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b[n].y, acc[n], 0, 0, 0);
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b[n].z, acc[n], 0, 0, 0);
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[n].w, acc[n], 0, 0, 0);
-        }
-        if (more) store_chunk(cur ^ 1);
+        // Branch-free pipeline: always prefetch; the last iteration re-loads its own (valid) chunk
+        // into the idle buffer, which nothing reads.  The next chunk's global loads are spread over
+        // the first MFMA groups so their address VALU issues in the MFMA shadow (T14/T19).
+        const int cn = c + 1 < p.nchunks ? c + 1 : c;
+        const Dec d = decode(cn);
+        read_frags(cur, 1, dc, fa1, fb1);
+        load_a(d, cn, 0);
+        load_a(d, cn, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_group(fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_frags(cur, 2, dc, fa0, fb0);
+        load_a(d, cn, 2);
+        load_a(d, cn, 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_group(fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        read_frags(cur, 3, dc, fa1, fb1);
+        load_b(cn);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_group(fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_group(fa1, fb1);
+        store_chunk(cur ^ 1);
         __syncthreads();
+        dc = d;
+        read_frags(cur ^ 1, 0, dc, fa0, fb0);
     }
 
     // ---- epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
     const bool gn = p.gn != nullptr;
     double* red = reinterpret_cast<double*>(&As[0][0]);  // [4 waves][BN][2] (LDS free after the loop)
+    const bool dense_out = p.osy == 1 && p.osx == 1;
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
         const int co = n0 + n * 32 + li;
         const bool cv = co < p.Cout;
-        const float bco = (cv && p.bias) ? p.bias[co] : 0.f;
-        double s = 0.0, ss = 0.0;
+        const int coc = cv ? co : 0;
+        const float bco = p.bias ? p.bias[coc] : 0.f;
+        size_t oidx[16];
+        bool ok[16];
+        float add[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
             const int m = m0 + wv * 32 + row;
-            if (m < p.M && cv) {
-                const int b = m / p.HoWo;
-                float v = acc[n][r] + bco;
-                if (p.bias_b) v += p.bias_b[(size_t)b * p.Cout + co];
-                size_t oidx;
-                if (p.osy == 1 && p.osx == 1) {
-                    oidx = (size_t)m * p.Cout + co;
-                } else {
-                    const int rr = m - b * p.HoWo;
-                    const int oy = rr / p.Wo, ox = rr - (rr / p.Wo) * p.Wo;
-                    oidx = ((size_t)b * p.Hy * p.Wy + (size_t)(oy * p.osy + p.ooy) * p.Wy + (ox * p.osx + p.oox)) * p.Cout + co;
-                }
-                if (p.resid) v += p.resid[oidx];
-                if (p.act == 1) v = fmaxf(v, 0.f);
-                else if (p.act == 2) v = 1.f / (1.f + expf(-v));
-                else if (p.act == 3) v = silu_f(v);
-                p.y[oidx] = v;
+            ok[r] = m < p.M && cv;
+            const int mm = m < p.M ? m : p.M - 1;
+            const int b = mm / p.HoWo;
+            if (dense_out) {
+                oidx[r] = (size_t)mm * p.Cout + coc;
+            } else {
+                const int rr = mm - b * p.HoWo;
+                const int oy = rr / p.Wo, ox = rr - (rr / p.Wo) * p.Wo;
+                oidx[r] = ((size_t)b * p.Hy * p.Wy + (size_t)(oy * p.osy + p.ooy) * p.Wy + (ox * p.osx + p.oox)) * p.Cout + coc;
+            }
+            add[r] = bco;
+            if (p.bias_b) add[r] += p.bias_b[(size_t)b * p.Cout + coc];
+        }
+        if (p.resid) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) add[r] += p.resid[oidx[r]];
+        }
+        double s = 0.0, ss = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float v = acc[n][r] + add[r];
+            if (p.act == 1) v = fmaxf(v, 0.f);
+            else if (p.act == 2) v = 1.f / (1.f + expf(-v));
+            else if (p.act == 3) v = silu_f(v);
+            if (ok[r]) {
+                p.y[oidx[r]] = v;
                 s += (double)v;
                 ss += (double)v * (double)v;
             }
@@ -302,9 +414,20 @@ template <int NT>
 int launch_nt(const ConvParams& p, int mode, hipStream_t st) {
     const int nm = cdiv(p.M, BM);
     const dim3 grid(nm * p.n_nblk), block(256);
-    if (mode == 0) hipLaunchKernelGGL((k_conv<NT, 0>), grid, block, 0, st, p);
-    else if (mode == 1) hipLaunchKernelGGL((k_conv<NT, 1>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((k_conv<NT, 2>), grid, block, 0, st, p);
+    const bool uni = mode == 0 && p.Cin % BK == 0 && p.C1 % BK == 0;  // chunk-uniform decode
+    const bool pro = p.sc1 || p.sc2;
+    if (pro) {  // validated by the caller: uni && circular
+        hipLaunchKernelGGL((k_conv<NT, 3, true, true>), grid, block, 0, st, p);
+    } else if (p.circular) {
+        if (uni) hipLaunchKernelGGL((k_conv<NT, 3, true, false>), grid, block, 0, st, p);
+        else if (mode == 0) hipLaunchKernelGGL((k_conv<NT, 0, true, false>), grid, block, 0, st, p);
+        else if (mode == 1) hipLaunchKernelGGL((k_conv<NT, 1, true, false>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((k_conv<NT, 2, true, false>), grid, block, 0, st, p);
+    } else {
+        if (uni) hipLaunchKernelGGL((k_conv<NT, 3, false, false>), grid, block, 0, st, p);
+        else if (mode == 0) hipLaunchKernelGGL((k_conv<NT, 0, false, false>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((k_conv<NT, 1, false, false>), grid, block, 0, st, p);
+    }
     return check_launch("tcx_conv2d");
 }
 
@@ -372,7 +495,9 @@ using namespace tcx;
 extern "C" int tcx_conv2d(const float* x1, const float* x2, int Bt, int bmod, int H, int W, int C1, int C2,
                           const float* wpk, const float* bias, const float* bias_b, const float* resid,
                           float* y, int Cout, int cout_pad, int kpad, int ks, int stride, int pad,
-                          int circular, int upsample, int act, double* gn_stats, void* stream) {
+                          int circular, int upsample, int act, double* gn_stats, const float* pro_scale1,
+                          const float* pro_shift1, const float* pro_scale2, const float* pro_shift2,
+                          void* stream) {
     TCX_REQUIRE(x1 && wpk && y, "tcx_conv2d: null pointer");
     TCX_REQUIRE(Bt >= 0 && H > 0 && W > 0 && C1 > 0 && C2 >= 0 && Cout > 0, "tcx_conv2d: bad shape");
     TCX_REQUIRE((C2 == 0) == (x2 == nullptr), "tcx_conv2d: x2/C2 mismatch");
@@ -407,6 +532,15 @@ extern "C" int tcx_conv2d(const float* x1, const float* x2, int Bt, int bmod, in
         mode = 1;
     }
     if (gn_stats) TCX_REQUIRE(p.HoWo % BM == 0, "tcx_conv2d: fused GN stats need Ho*Wo %% 128 == 0");
+    p.sc1 = pro_scale1; p.sh1 = pro_shift1; p.sc2 = pro_scale2; p.sh2 = pro_shift2;
+    if (pro_scale1 || pro_scale2) {
+        TCX_REQUIRE((pro_scale1 != nullptr) == (pro_shift1 != nullptr) &&
+                    (pro_scale2 != nullptr) == (pro_shift2 != nullptr), "tcx_conv2d: prologue scale/shift pairs");
+        TCX_REQUIRE(mode == 0 && Cin % BK == 0 && C1 % BK == 0 && circular && bmod == 0 && p.HoWo % BM == 0 &&
+                    C1 <= PRO_MAXC && C2 <= PRO_MAXC && (pro_scale2 == nullptr || x2 != nullptr),
+                    "tcx_conv2d: fused GN prologue needs Cin,C1 %% 32 == 0, circular, no bmod/upsample, "
+                    "Ho*Wo %% 128 == 0, C <= 384");
+    }
     TCX_REQUIRE(aligned16(wpk), "tcx_conv2d: packed weight must be 16-B aligned");
     return launch_conv(p, cout_pad, mode, (hipStream_t)stream);
 }

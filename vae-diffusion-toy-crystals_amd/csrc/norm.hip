@@ -62,53 +62,18 @@ __global__ __launch_bounds__(256) void k_gn_partials(const float* __restrict__ x
     }
 }
 
-// Per-channel scale/shift of batch b into LDS from the partials.
-__device__ void gn_scale_shift(const double* __restrict__ part, int b, int nsplit, int C, int groups, int HW,
-                               const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                               float* sc, float* sh, double* gstat) {
-    const int cpg = C / groups;
-    const int tid = threadIdx.x;
-    for (int g = tid; g < groups; g += blockDim.x) {
-        double a = 0, q = 0;
-        for (int sp = 0; sp < nsplit; ++sp) {
-            const double* src = part + (((size_t)b * nsplit + sp) * C + g * cpg) * 2;
-            for (int c = 0; c < cpg; ++c) {
-                a += src[2 * c];
-                q += src[2 * c + 1];
-            }
-        }
-        const double n = (double)HW * cpg;
-        const double mean = a / n;
-        double var = q / n - mean * mean;
-        var = var < 0 ? 0 : var;
-        gstat[2 * g] = mean;
-        gstat[2 * g + 1] = 1.0 / sqrt(var + (double)eps);
-    }
-    __syncthreads();
-    for (int c = tid; c < C; c += blockDim.x) {
-        const int g = c / cpg;
-        const float rstd = (float)gstat[2 * g + 1];
-        const float mean = (float)gstat[2 * g];
-        const float gm = gamma ? gamma[c] : 1.f;
-        const float bt = beta ? beta[c] : 0.f;
-        const float scl = rstd * gm;
-        sc[c] = scl;
-        sh[c] = bt - mean * scl;
-    }
-    __syncthreads();
-}
-
 // grid (chunks, Bt); each block normalises pixels [chunk*ppb, ...) of image b.
 __global__ __launch_bounds__(256) void k_gn_apply(const float* __restrict__ x, float* __restrict__ y, int HW, int C,
                                                   int groups, const double* __restrict__ part, int nsplit,
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
                                                   float eps, int silu, int ppb) {
-    extern __shared__ __attribute__((aligned(16))) float lsm[];  // sc[C], sh[C], gstat (double) [2*groups]
+    extern __shared__ __attribute__((aligned(16))) float lsm[];  // sc[C], sh[C], gstat, csum
     float* sc = lsm;
-    float* sh = lsm + C;
-    double* gstat = reinterpret_cast<double*>(lsm + 2 * ((C + 1) & ~1));
+    float* sh = lsm + ((C + 3) & ~3);
+    double* gstat = reinterpret_cast<double*>(lsm + 2 * ((C + 3) & ~3));
+    double* csum = gstat + 2 * groups;
     const int b = blockIdx.y;
-    gn_scale_shift(part, b, nsplit, C, groups, HW, gamma, beta, eps, sc, sh, gstat);
+    gn_scale_shift(part, b, nsplit, C, groups, HW, gamma, beta, eps, sc, sh, gstat, csum);
     const int p0 = blockIdx.x * ppb;
     const int p1 = min(HW, p0 + ppb);
     const size_t base = ((size_t)b * HW + p0) * C;
@@ -128,8 +93,73 @@ __global__ __launch_bounds__(256) void k_gn_apply(const float* __restrict__ x, f
     }
 }
 
+// Streaming GroupNorm apply from per-(b, c) tables: y = act(x * scale + shift).  grid (chunks, Bt).
+__global__ __launch_bounds__(256) void k_gn_apply_tab(const float* __restrict__ x, float* __restrict__ y, int HW, int C,
+                                                      const float* __restrict__ tsc, const float* __restrict__ tsh,
+                                                      int silu, int ppb) {
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    float* sc = lsm;
+    float* sh = lsm + ((C + 3) & ~3);
+    const int b = blockIdx.y;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        sc[c] = tsc[(size_t)b * C + c];
+        sh[c] = tsh[(size_t)b * C + c];
+    }
+    __syncthreads();
+    const int p0 = blockIdx.x * ppb;
+    const int p1 = min(HW, p0 + ppb);
+    const size_t base = ((size_t)b * HW + p0) * C;
+    const int n4 = (p1 - p0) * C / 4;
+    const int C4 = C / 4;
+    int i = threadIdx.x;
+    for (; i + 256 < n4; i += 512) {  // two float4 in flight per thread
+        const int c0 = (i % C4) * 4, c1 = ((i + 256) % C4) * 4;
+        float4 v0 = *reinterpret_cast<const float4*>(x + base + (size_t)i * 4);
+        float4 v1 = *reinterpret_cast<const float4*>(x + base + (size_t)(i + 256) * 4);
+        v0.x = fmaf(v0.x, sc[c0], sh[c0]); v0.y = fmaf(v0.y, sc[c0 + 1], sh[c0 + 1]);
+        v0.z = fmaf(v0.z, sc[c0 + 2], sh[c0 + 2]); v0.w = fmaf(v0.w, sc[c0 + 3], sh[c0 + 3]);
+        v1.x = fmaf(v1.x, sc[c1], sh[c1]); v1.y = fmaf(v1.y, sc[c1 + 1], sh[c1 + 1]);
+        v1.z = fmaf(v1.z, sc[c1 + 2], sh[c1 + 2]); v1.w = fmaf(v1.w, sc[c1 + 3], sh[c1 + 3]);
+        if (silu) {
+            v0.x = silu_f(v0.x); v0.y = silu_f(v0.y); v0.z = silu_f(v0.z); v0.w = silu_f(v0.w);
+            v1.x = silu_f(v1.x); v1.y = silu_f(v1.y); v1.z = silu_f(v1.z); v1.w = silu_f(v1.w);
+        }
+        *reinterpret_cast<float4*>(y + base + (size_t)i * 4) = v0;
+        *reinterpret_cast<float4*>(y + base + (size_t)(i + 256) * 4) = v1;
+    }
+    for (; i < n4; i += 256) {
+        const int c = (i % C4) * 4;
+        float4 v = *reinterpret_cast<const float4*>(x + base + (size_t)i * 4);
+        v.x = fmaf(v.x, sc[c], sh[c]); v.y = fmaf(v.y, sc[c + 1], sh[c + 1]);
+        v.z = fmaf(v.z, sc[c + 2], sh[c + 2]); v.w = fmaf(v.w, sc[c + 3], sh[c + 3]);
+        if (silu) {
+            v.x = silu_f(v.x); v.y = silu_f(v.y); v.z = silu_f(v.z); v.w = silu_f(v.w);
+        }
+        *reinterpret_cast<float4*>(y + base + (size_t)i * 4) = v;
+    }
+}
+
+// One block per image: partials -> per-(b, c) scale/shift tables for a fused GN(+SiLU) prologue.
+__global__ __launch_bounds__(256) void k_gn_finalize(const double* __restrict__ part, int HW, int C, int groups,
+                                                     int nsplit, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     float* __restrict__ scale, float* __restrict__ shift) {
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    float* sc = lsm;
+    float* sh = lsm + ((C + 3) & ~3);
+    double* gstat = reinterpret_cast<double*>(lsm + 2 * ((C + 3) & ~3));
+    double* csum = gstat + 2 * groups;
+    const int b = blockIdx.x;
+    gn_scale_shift(part, b, nsplit, C, groups, HW, gamma, beta, eps, sc, sh, gstat, csum);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        scale[(size_t)b * C + c] = sc[c];
+        shift[(size_t)b * C + c] = sh[c];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ x, float* __restrict__ y, int Bt, int H,
-                                                    int W, int C) {
+                                                    int W, int C, const float* __restrict__ tsc,
+                                                    const float* __restrict__ tsh) {
     const int C4 = C / 4;
     const size_t n = (size_t)Bt * 4 * H * W * C4;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -148,10 +178,19 @@ __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ x,
         const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
         const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
         const float* src = x + (size_t)b * H * W * C + c4 * 4;
-        const float4 a = *reinterpret_cast<const float4*>(src + (size_t)(y0 * W + x0) * C);
-        const float4 bq = *reinterpret_cast<const float4*>(src + (size_t)(y0 * W + x1) * C);
-        const float4 c = *reinterpret_cast<const float4*>(src + (size_t)(y1 * W + x0) * C);
-        const float4 d = *reinterpret_cast<const float4*>(src + (size_t)(y1 * W + x1) * C);
+        float4 a = *reinterpret_cast<const float4*>(src + (size_t)(y0 * W + x0) * C);
+        float4 bq = *reinterpret_cast<const float4*>(src + (size_t)(y0 * W + x1) * C);
+        float4 c = *reinterpret_cast<const float4*>(src + (size_t)(y1 * W + x0) * C);
+        float4 d = *reinterpret_cast<const float4*>(src + (size_t)(y1 * W + x1) * C);
+        if (tsc) {  // fused GN+SiLU of the source (up2's last GroupNorm before us1)
+            const float4 s4 = *reinterpret_cast<const float4*>(tsc + (size_t)b * C + c4 * 4);
+            const float4 h4 = *reinterpret_cast<const float4*>(tsh + (size_t)b * C + c4 * 4);
+            auto tr = [&](float4& v) {
+                v.x = silu_f(fmaf(v.x, s4.x, h4.x)); v.y = silu_f(fmaf(v.y, s4.y, h4.y));
+                v.z = silu_f(fmaf(v.z, s4.z, h4.z)); v.w = silu_f(fmaf(v.w, s4.w, h4.w));
+            };
+            tr(a); tr(bq); tr(c); tr(d);
+        }
         float4 o;
         o.x = ly0 * (lx0 * a.x + lx1 * bq.x) + ly1 * (lx0 * c.x + lx1 * d.x);
         o.y = ly0 * (lx0 * a.y + lx1 * bq.y) + ly1 * (lx0 * c.y + lx1 * d.y);
@@ -220,20 +259,43 @@ extern "C" int tcx_gn_apply(const float* x, float* y, int Bt, int HW, int C, int
     TCX_REQUIRE(C % 4 == 0 && groups > 0 && C % groups == 0, "tcx_gn_apply: bad C/groups");
     TCX_REQUIRE(aligned16(x) && aligned16(y), "tcx_gn_apply: x/y must be 16-B aligned");
     if (Bt == 0) return TCX_OK;
-    const int ppb = std::max(1, 16384 / C);  // ~64 KB of activations per block
+    const int ppb = std::max(1, 65536 / C);  // ~256 KB of activations per block (partials folded once per block)
     const int chunks = cdiv(HW, ppb);
-    const size_t shm = (size_t)2 * ((C + 1) & ~1) * sizeof(float) + (size_t)2 * groups * sizeof(double);
+    const size_t shm = gn_fold_lds_bytes(C, groups);
     hipLaunchKernelGGL(k_gn_apply, dim3(chunks, Bt), dim3(256), shm, (hipStream_t)stream, x, y, HW, C, groups, part,
                        nsplit, gamma, beta, eps, silu, ppb);
     return check_launch("tcx_gn_apply");
 }
 
-extern "C" int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, int C, void* stream) {
+extern "C" int tcx_gn_finalize(const double* part, int Bt, int HW, int C, int groups, int nsplit, const float* gamma,
+                               const float* beta, float eps, float* scale, float* shift, void* stream) {
+    TCX_REQUIRE(part && scale && shift && groups > 0 && C % groups == 0 && nsplit >= 1, "tcx_gn_finalize: bad args");
+    if (Bt == 0) return TCX_OK;
+    const size_t shm = gn_fold_lds_bytes(C, groups);
+    hipLaunchKernelGGL(k_gn_finalize, dim3(Bt), dim3(256), shm, (hipStream_t)stream, part, HW, C, groups, nsplit, gamma,
+                       beta, eps, scale, shift);
+    return check_launch("tcx_gn_finalize");
+}
+
+extern "C" int tcx_gn_apply_tab(const float* x, float* y, int Bt, int HW, int C, const float* scale, const float* shift,
+                                int silu, void* stream) {
+    TCX_REQUIRE(x && y && scale && shift && C % 4 == 0 && aligned16(x) && aligned16(y), "tcx_gn_apply_tab: bad args");
+    if (Bt == 0) return TCX_OK;
+    const int ppb = std::max(1, 32768 / C);  // 128 KB of activations per block
+    const dim3 grid(cdiv(HW, ppb), Bt);
+    const size_t shm = (size_t)2 * ((C + 3) & ~3) * sizeof(float);
+    hipLaunchKernelGGL(k_gn_apply_tab, grid, dim3(256), shm, (hipStream_t)stream, x, y, HW, C, scale, shift, silu, ppb);
+    return check_launch("tcx_gn_apply_tab");
+}
+
+extern "C" int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, int C, const float* scale,
+                              const float* shift, void* stream) {
     TCX_REQUIRE(x && y && C % 4 == 0 && aligned16(x) && aligned16(y), "tcx_upsample2x: bad args");
+    TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x: scale/shift pair");
     const size_t n = (size_t)Bt * 4 * H * W * (C / 4);
     if (n == 0) return TCX_OK;
     const int blocks = (int)std::min<size_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_upsample2x, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, y, Bt, H, W, C);
+    hipLaunchKernelGGL(k_upsample2x, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, y, Bt, H, W, C, scale, shift);
     return check_launch("tcx_upsample2x");
 }
 

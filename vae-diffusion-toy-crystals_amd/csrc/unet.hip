@@ -103,75 +103,71 @@ __global__ __launch_bounds__(256) void k_cond(CondArgs a, const float* __restric
     }
 }
 
-// ---------------------------------------------------------------- GN scale/shift (shared)
-__device__ void gn_fold(const double* __restrict__ part, int b, int nsplit, int C, int groups, int HW,
-                        const float* __restrict__ gamma, const float* __restrict__ beta, float* sc, float* sh,
-                        double* gstat) {
-    const int cpg = C / groups;
-    for (int g = threadIdx.x; g < groups; g += blockDim.x) {
-        double s = 0, q = 0;
-        for (int sp = 0; sp < nsplit; ++sp) {
-            const double* src = part + (((size_t)b * nsplit + sp) * C + g * cpg) * 2;
-            for (int c = 0; c < cpg; ++c) {
-                s += src[2 * c];
-                q += src[2 * c + 1];
+// Head: out conv (C -> 1, 3x3 circular) split into a per-pixel channel reduction here and a
+// 9-tap circular gather in k_step.  grid (HW/128, Bt); block 256.  The 128-pixel x C tile is read
+// coalesced (contiguous 128*C floats), GroupNorm+SiLU applied from the per-image table, staged in
+// LDS; then thread (pixel, tap set) computes r[b][tap][p] = sum_c h[p][c] * w_out[c][tap].
+constexpr int HEAD_PX = 128;
+__global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int HW, int C, const float* __restrict__ tsc,
+                                              const float* __restrict__ tsh, const float* __restrict__ w_out,
+                                              float* __restrict__ r) {
+    extern __shared__ __attribute__((aligned(16))) float hs[];  // tile[128][C+4] | w[9][C] | sc[C] sh[C]
+    const int LD = C + 4;
+    float* tile = hs;
+    float* w = hs + HEAD_PX * LD;
+    float* sc = w + 9 * C;
+    float* sh = sc + C;
+    const int b = blockIdx.y;
+    const int p0 = blockIdx.x * HEAD_PX;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 9 * C; i += 256) {
+        const int c = i / 9, k = i - (i / 9) * 9;  // w_out is [C][9]; stored tap-major
+        w[k * C + c] = w_out[i];
+    }
+    for (int c = tid; c < C; c += 256) {
+        sc[c] = tsc[(size_t)b * C + c];
+        sh[c] = tsh[(size_t)b * C + c];
+    }
+    __syncthreads();
+    const int C4 = C / 4;
+    const int npx = min(HEAD_PX, HW - p0);
+    const float* src = h + ((size_t)b * HW + p0) * C;
+    for (int i = tid; i < npx * C4; i += 256) {
+        const int px = i / C4, c = (i - (i / C4) * C4) * 4;
+        float4 v = *reinterpret_cast<const float4*>(src + (size_t)i * 4);
+        v.x = silu_f(fmaf(v.x, sc[c], sh[c]));
+        v.y = silu_f(fmaf(v.y, sc[c + 1], sh[c + 1]));
+        v.z = silu_f(fmaf(v.z, sc[c + 2], sh[c + 2]));
+        v.w = silu_f(fmaf(v.w, sc[c + 3], sh[c + 3]));
+        *reinterpret_cast<float4*>(&tile[px * LD + c]) = v;
+    }
+    __syncthreads();
+    const int px = tid & (HEAD_PX - 1);
+    const int half = tid >> 7;  // taps 0..4 or 5..8
+    if (px >= npx) return;
+    const int k0 = half ? 5 : 0, k1 = half ? 9 : 5;
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    const float* row = &tile[px * LD];
+    for (int c = 0; c < C; c += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(row + c);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int k = k0 + j;
+            if (k < k1) {
+                const float4 ww = *reinterpret_cast<const float4*>(&w[k * C + c]);
+                float a = acc[j];
+                a = fmaf(v.x, ww.x, a);
+                a = fmaf(v.y, ww.y, a);
+                a = fmaf(v.z, ww.z, a);
+                a = fmaf(v.w, ww.w, a);
+                acc[j] = a;
             }
         }
-        const double n = (double)HW * cpg;
-        const double mean = s / n;
-        double var = q / n - mean * mean;
-        var = var < 0 ? 0 : var;
-        gstat[2 * g] = mean;
-        gstat[2 * g + 1] = 1.0 / sqrt(var + 1e-5);
     }
-    __syncthreads();
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        const int g = c / cpg;
-        const float scl = (float)gstat[2 * g + 1] * gamma[c];
-        sc[c] = scl;
-        sh[c] = beta[c] - (float)gstat[2 * g] * scl;
-    }
-    __syncthreads();
-}
-
-// grid (ceil(HW/256), Bt); one thread per pixel.
-__global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int HW, int C, int groups,
-                                              const double* __restrict__ part, int nsplit,
-                                              const float* __restrict__ gamma, const float* __restrict__ beta,
-                                              const float* __restrict__ w_out, float* __restrict__ r) {
-    extern __shared__ __attribute__((aligned(16))) float hs[];  // sc[C] sh[C] w[C*9] gstat
-    float* sc = hs;
-    float* sh = hs + C;
-    float* w = hs + 2 * C;
-    double* gstat = reinterpret_cast<double*>(hs + ((11 * C + 3) & ~3));
-    const int b = blockIdx.y;
-    for (int i = threadIdx.x; i < 9 * C; i += blockDim.x) w[i] = w_out[i];
-    gn_fold(part, b, nsplit, C, groups, HW, gamma, beta, sc, sh, gstat);
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    if (p >= HW) return;
-    const float* src = h + ((size_t)b * HW + p) * C;
-    float acc[9];
+    float* dst = r + (size_t)b * 9 * HW + p0 + px;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) acc[k] = 0.f;
-    for (int c = 0; c < C; c += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(src + c);
-        const float e0 = silu_f(fmaf(v.x, sc[c], sh[c]));
-        const float e1 = silu_f(fmaf(v.y, sc[c + 1], sh[c + 1]));
-        const float e2 = silu_f(fmaf(v.z, sc[c + 2], sh[c + 2]));
-        const float e3 = silu_f(fmaf(v.w, sc[c + 3], sh[c + 3]));
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            float a = acc[k];
-            a = fmaf(e0, w[(c + 0) * 9 + k], a);
-            a = fmaf(e1, w[(c + 1) * 9 + k], a);
-            a = fmaf(e2, w[(c + 2) * 9 + k], a);
-            a = fmaf(e3, w[(c + 3) * 9 + k], a);
-            acc[k] = a;
-        }
-    }
-    float* dst = r + (size_t)b * 9 * HW + p;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) dst[(size_t)k * HW] = acc[k];
+    for (int j = 0; j < 5; ++j)
+        if (k0 + j < k1) dst[(size_t)(k0 + j) * HW] = acc[j];
 }
 
 // ---------------------------------------------------------------- Philox4x32-10
@@ -293,7 +289,10 @@ struct Plan {
     int Bt, H, W, C, C2, P0, P1, P2;
     float *bias0, *a64, *b64, *h1, *a32, *b32, *h2, *a16, *b16, *qkv, *r;
     double* gn;
+    float* tab;  // GroupNorm scale/shift tables: [11 norms][2][Bt][C2]
     size_t bytes;
+    float* sc(int i) const { return tab + (size_t)(2 * i) * Bt * C2; }
+    float* sh(int i) const { return tab + (size_t)(2 * i + 1) * Bt * C2; }
 };
 
 Plan make_plan(const tcx_unet* net, int Bt, int H, int W, char* base) {
@@ -321,6 +320,7 @@ Plan make_plan(const tcx_unet* net, int Bt, int H, int W, char* base) {
     p.r = (float*)take((size_t)Bt * 9 * p.P0 * f);
     const int maxsplit = std::max(1, p.P0 / 128);
     p.gn = (double*)take((size_t)Bt * maxsplit * std::max(p.C2, 2 * p.C2) * 2 * sizeof(double));
+    p.tab = (float*)take((size_t)22 * Bt * p.C2 * f);
     p.bytes = off;
     return p;
 }
@@ -330,16 +330,16 @@ struct GnRef {
 };
 
 // conv helper: writes GN partials in the epilogue when the tile geometry allows it, else runs
-// the partials kernel afterwards.  Returns nsplit of the partials in `gn`.
+// the partials kernel afterwards; sc/sh{1,2}: fused GN+SiLU prologue tables of the sources.
 int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2, int Bt, int bmod, int H, int W,
-            int stride, int pad, int ups, const float* bias_b, const float* resid, float* y, double* gn,
-            int* nsplit, hipStream_t st) {
-    const int Hi = ups ? 2 * H : H, Wi = ups ? 2 * W : W;
-    const int Ho = (Hi + 2 * pad - cv.ks) / stride + 1, Wo = (Wi + 2 * pad - cv.ks) / stride + 1;
+            int stride, int pad, const float* bias_b, const float* resid, float* y, double* gn, int* nsplit,
+            hipStream_t st, const float* sc1 = nullptr, const float* sh1 = nullptr, const float* sc2 = nullptr,
+            const float* sh2 = nullptr) {
+    const int Ho = (H + 2 * pad - cv.ks) / stride + 1, Wo = (W + 2 * pad - cv.ks) / stride + 1;
     const int HoWo = Ho * Wo;
     const bool fused = gn && HoWo % 128 == 0;
     TCX_TRY(tcx_conv2d(x1, x2, Bt, bmod, H, W, C1, C2, cv.w, cv.b, bias_b, resid, y, cv.cout, cv.cout_pad, cv.kpad,
-                       cv.ks, stride, pad, 1, ups, 0, fused ? gn : nullptr, st));
+                       cv.ks, stride, pad, 1, 0, 0, fused ? gn : nullptr, sc1, sh1, sc2, sh2, st));
     if (gn && !fused) {
         const int ns = std::max(1, HoWo / 512);
         TCX_TRY(tcx_gn_partials(y, Bt, HoWo, cv.cout, ns, gn, st));
@@ -356,16 +356,20 @@ int groups_of(int ch) {
     return 1;
 }
 
-int gn_apply(const tcx_unet* net, int idx, float* y, int Bt, int HW, int C, const double* gn, int ns, int silu,
-             hipStream_t st, const float* src = nullptr) {
-    return tcx_gn_apply(src ? src : y, y, Bt, HW, C, groups_of(C), gn, ns, net->gn_w[idx], net->gn_b[idx], 1e-5f,
-                        silu, st);
+int gn_tab(const tcx_unet* net, const Plan& P, int idx, int HW, int C, const double* gn, int ns, hipStream_t st) {
+    return tcx_gn_finalize(gn, P.Bt, HW, C, groups_of(C), ns, net->gn_w[idx], net->gn_b[idx], 1e-5f, P.sc(idx),
+                           P.sh(idx), st);
 }
 
 // The U-Net body (everything up to and including the head partials r).  Input x [B][H][W] (C=1).
+// GroupNorm+SiLU outputs are never materialised except where a consumer needs the normalised
+// tensor itself (the attention input / residual): every other one is applied by the consuming
+// conv's staging prologue from [Bt][C] scale/shift tables (tcx_gn_finalize), with the statistics
+// coming from the producing conv's epilogue.
 int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const float* t, int t_per_sample,
               const int64_t* y_cat, const float* y_cont, int cfg, hipStream_t st) {
     const int Bt = P.Bt, H = P.H, W = P.W, C = P.C, C2 = P.C2;
+    const int H1 = H / 2, W1 = W / 2, H2 = H / 4, W2 = W / 4;
     // conditioning -> per-batch first-conv bias
     {
         CondArgs a{};
@@ -381,64 +385,109 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     }
     int ns = 1;
     double* gn = P.gn;
-    // down1 (first conv: x_t channel only, maps folded into bias0; bias already inside bias0)
+    // Where a consumer cannot take the fused prologue (channels not a multiple of 32, or a tile
+    // spanning two images at tiny resolutions), the GroupNorm is applied in place instead.
+    auto can = [](int Csrc, int Coth, int HoWo) {
+        return Csrc % 32 == 0 && Coth % 32 == 0 && HoWo % 128 == 0 && Csrc <= 384 && Coth <= 384;
+    };
+    // Measured (profiles/r01_*): on gfx950 fp32 MFMA shares the fp32 VALU rate, so a SiLU
+    // recomputed for every im2col tap (9x per element) costs the conv ~25 %, more than the
+    // separate HBM-bound GroupNorm pass it removes.  The prologue path stays in the ABI
+    // (tcx_conv2d pro_*) but the U-Net materialises each GroupNorm once (fused_gn_prologue=false).
+    constexpr bool fused_gn_prologue = false;
+    bool pro[11] = {};
+    if (fused_gn_prologue) {
+        pro[0] = can(C, 0, P.P0);
+        pro[1] = can(C, 0, P.P1) && can(C, C, P.P0);
+        pro[2] = can(C2, 0, P.P1);
+        pro[3] = can(C2, 0, P.P2) && can(C2, C2, P.P1);
+        pro[4] = can(C2, 0, P.P2);
+        pro[7] = can(C, 0, P.P1);
+        pro[9] = can(C, 0, P.P0);
+    }
+    auto SC = [&](int i) -> const float* { return pro[i] ? P.sc(i) : nullptr; };
+    auto SH = [&](int i) -> const float* { return pro[i] ? P.sh(i) : nullptr; };
+    // finalize the table of norm i, or normalise `y` in place when no prologue can consume it
+    auto norm = [&](int i, float* y, int HW, int Cn) -> int {
+        TCX_TRY(gn_tab(net, P, i, HW, Cn, gn, ns, st));
+        if (pro[i]) return TCX_OK;
+        return tcx_gn_apply_tab(y, y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, st);
+    };
+    // down1 (first conv: x_t channel only, maps folded into bias0; the conv bias is inside bias0)
     {
         const tcx_conv& c0 = net->down1_0;
+        const bool fz = (H * W) % 128 == 0;
         TCX_TRY(tcx_conv2d(x, nullptr, Bt, B, H, W, 1, 0, c0.w, nullptr, P.bias0, nullptr, P.a64, c0.cout, c0.cout_pad,
-                           c0.kpad, 3, 1, 1, 1, 0, 0, (H * W) % 128 == 0 ? gn : nullptr, st));
-        if ((H * W) % 128 == 0) ns = H * W / 128;
+                           c0.kpad, 3, 1, 1, 1, 0, 0, fz ? gn : nullptr, nullptr, nullptr, nullptr, nullptr, st));
+        if (fz) ns = H * W / 128;
         else { ns = std::max(1, H * W / 512); TCX_TRY(tcx_gn_partials(P.a64, Bt, H * W, C, ns, gn, st)); }
     }
-    TCX_TRY(gn_apply(net, 0, P.a64, Bt, P.P0, C, gn, ns, 1, st));
-    TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, 0, nullptr, nullptr, P.h1, gn, &ns, st));
-    TCX_TRY(gn_apply(net, 1, P.h1, Bt, P.P0, C, gn, ns, 1, st));
-    // ds1: 4x4/s2 circular
-    TCX_TRY(conv_gn(net->ds1, P.h1, nullptr, C, 0, Bt, 0, H, W, 2, 1, 0, nullptr, nullptr, P.a32, nullptr, &ns, st));
-    const int H1 = H / 2, W1 = W / 2, H2 = H / 4, W2 = W / 4;
+    TCX_TRY(norm(0, P.a64, P.P0, C));
+    TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.h1, gn, &ns, st,
+                    SC(0), SH(0)));
+    TCX_TRY(norm(1, P.h1, P.P0, C));  // h1 stays raw; its two consumers apply table 1
+    // ds1: 4x4/s2 circular on silu(gn(h1))
+    TCX_TRY(conv_gn(net->ds1, P.h1, nullptr, C, 0, Bt, 0, H, W, 2, 1, nullptr, nullptr, P.a32, nullptr, &ns, st,
+                    SC(1), SH(1)));
     // down2
-    TCX_TRY(conv_gn(net->down2_0, P.a32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, 0, nullptr, nullptr, P.b32, gn, &ns, st));
-    TCX_TRY(gn_apply(net, 2, P.b32, Bt, P.P1, C2, gn, ns, 1, st));
-    TCX_TRY(conv_gn(net->down2_1, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, 0, nullptr, nullptr, P.h2, gn, &ns, st));
-    TCX_TRY(gn_apply(net, 3, P.h2, Bt, P.P1, C2, gn, ns, 1, st));
+    TCX_TRY(conv_gn(net->down2_0, P.a32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st));
+    TCX_TRY(norm(2, P.b32, P.P1, C2));
+    TCX_TRY(conv_gn(net->down2_1, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.h2, gn, &ns, st,
+                    SC(2), SH(2)));
+    TCX_TRY(norm(3, P.h2, P.P1, C2));  // h2 raw; consumers apply table 3
     // ds2
-    TCX_TRY(conv_gn(net->ds2, P.h2, nullptr, C2, 0, Bt, 0, H1, W1, 2, 1, 0, nullptr, nullptr, P.a16, nullptr, &ns, st));
+    TCX_TRY(conv_gn(net->ds2, P.h2, nullptr, C2, 0, Bt, 0, H1, W1, 2, 1, nullptr, nullptr, P.a16, nullptr, &ns, st,
+                    SC(3), SH(3)));
     // mid
-    TCX_TRY(conv_gn(net->mid_0, P.a16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, 0, nullptr, nullptr, P.b16, gn, &ns, st));
-    TCX_TRY(gn_apply(net, 4, P.b16, Bt, P.P2, C2, gn, ns, 1, st));
-    TCX_TRY(conv_gn(net->mid_1, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, 0, nullptr, nullptr, P.a16, gn, &ns, st));
-    TCX_TRY(gn_apply(net, 5, P.a16, Bt, P.P2, C2, gn, ns, 1, st));
+    TCX_TRY(conv_gn(net->mid_0, P.a16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, nullptr, nullptr, P.b16, gn, &ns, st));
+    TCX_TRY(norm(4, P.b16, P.P2, C2));
+    TCX_TRY(conv_gn(net->mid_1, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, nullptr, nullptr, P.a16, gn, &ns, st,
+                    SC(4), SH(4)));
+    // the attention block needs the normalised tensor itself (input of attn.norm and residual)
+    TCX_TRY(gn_tab(net, P, 5, P.P2, C2, gn, ns, st));
+    TCX_TRY(tcx_gn_apply_tab(P.a16, P.a16, Bt, P.P2, C2, P.sc(5), P.sh(5), 1, st));
     // attention: x_in = a16; b16 = GN(x_in); qkv = 1x1; b16 = attn; a16 = x_in + proj(b16)
     {
         const int ns_a = std::max(1, P.P2 / 256);
         TCX_TRY(tcx_gn_partials(P.a16, Bt, P.P2, C2, ns_a, gn, st));
-        TCX_TRY(gn_apply(net, 6, P.b16, Bt, P.P2, C2, gn, ns_a, 0, st, P.a16));
+        TCX_TRY(gn_tab(net, P, 6, P.P2, C2, gn, ns_a, st));
+        TCX_TRY(tcx_gn_apply_tab(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, st));
         const tcx_conv& q = net->qkv;
         TCX_TRY(tcx_conv2d(P.b16, nullptr, Bt, 0, H2, W2, C2, 0, q.w, q.b, nullptr, nullptr, P.qkv, q.cout, q.cout_pad,
-                           q.kpad, 1, 1, 0, 1, 0, 0, nullptr, st));
+                           q.kpad, 1, 1, 0, 1, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, st));
         TCX_TRY(tcx_attention(P.qkv, P.b16, Bt, P.P2, C2, net->heads, st));
         const tcx_conv& pr = net->proj;
         TCX_TRY(tcx_conv2d(P.b16, nullptr, Bt, 0, H2, W2, C2, 0, pr.w, pr.b, nullptr, P.a16, P.a16, pr.cout,
-                           pr.cout_pad, pr.kpad, 1, 1, 0, 1, 0, 0, nullptr, st));
+                           pr.cout_pad, pr.kpad, 1, 1, 0, 1, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, st));
     }
-    // us2 (bilinear x2 fused into the conv's A load) -> a32 [C2]
-    TCX_TRY(conv_gn(net->us2, P.a16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, 1, nullptr, nullptr, P.a32, nullptr, &ns, st));
-    // up2 on cat[a32, h2]
-    TCX_TRY(conv_gn(net->up2_0, P.a32, P.h2, C2, C2, Bt, 0, H1, W1, 1, 1, 0, nullptr, nullptr, P.b32, gn, &ns, st));
-    TCX_TRY(gn_apply(net, 7, P.b32, Bt, P.P1, C, gn, ns, 1, st));
-    TCX_TRY(conv_gn(net->up2_1, P.b32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, 0, nullptr, nullptr, P.a32, gn, &ns, st));
-    TCX_TRY(gn_apply(net, 8, P.a32, Bt, P.P1, C, gn, ns, 1, st));
-    // us1 -> a64 [C]
-    TCX_TRY(conv_gn(net->us1, P.a32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, 1, nullptr, nullptr, P.a64, nullptr, &ns, st));
-    // up1 on cat[a64, h1]
-    TCX_TRY(conv_gn(net->up1_0, P.a64, P.h1, C, C, Bt, 0, H, W, 1, 1, 0, nullptr, nullptr, P.b64, gn, &ns, st));
-    TCX_TRY(gn_apply(net, 9, P.b64, Bt, P.P0, C, gn, ns, 1, st));
-    TCX_TRY(conv_gn(net->up1_1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, 0, nullptr, nullptr, P.a64, gn, &ns, st));
+    // us2: bilinear x2 (edge-clamped) into the free b32 buffer, then the circular 3x3 conv -> a32.
+    // (The upsample-on-load conv variant re-reads 4 source taps per im2col element and measured
+    // slower than this separate 250 MB pass.)
+    TCX_TRY(tcx_upsample2x(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, st));
+    TCX_TRY(conv_gn(net->us2, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, nullptr, &ns, st));
+    // up2 on cat[a32, silu(gn(h2))]
+    TCX_TRY(conv_gn(net->up2_0, P.a32, P.h2, C2, C2, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st,
+                    nullptr, nullptr, SC(3), SH(3)));
+    TCX_TRY(norm(7, P.b32, P.P1, C));
+    TCX_TRY(conv_gn(net->up2_1, P.b32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, gn, &ns, st,
+                    SC(7), SH(7)));
+    // us1: upsample silu(gn(a32)) into the free b64 buffer (GN applied on the taps), conv -> a64 [C]
+    TCX_TRY(gn_tab(net, P, 8, P.P1, C, gn, ns, st));
+    TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, P.sc(8), P.sh(8), st));
+    TCX_TRY(conv_gn(net->us1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, nullptr, &ns, st));
+    // up1 on cat[a64, silu(gn(h1))]
+    TCX_TRY(conv_gn(net->up1_0, P.a64, P.h1, C, C, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.b64, gn, &ns, st, nullptr,
+                    nullptr, SC(1), SH(1)));
+    TCX_TRY(norm(9, P.b64, P.P0, C));
+    TCX_TRY(conv_gn(net->up1_1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, gn, &ns, st,
+                    SC(9), SH(9)));
     // head: GN(up1.net.4)+SiLU fused with the out conv's channel reduction
     {
-        const size_t shm = (size_t)((11 * C + 3) & ~3) * sizeof(float) + 2 * 8 * sizeof(double) + 64;
-        const dim3 grid(cdiv(P.P0, 256), Bt);
-        hipLaunchKernelGGL(k_head, grid, dim3(256), shm, st, P.a64, P.P0, C, groups_of(C), gn, ns, net->gn_w[10],
-                           net->gn_b[10], net->out_w, P.r);
+        TCX_TRY(gn_tab(net, P, 10, P.P0, C, gn, ns, st));
+        TCX_REQUIRE(C % 4 == 0, "head: C %% 4");
+        const size_t shm = ((size_t)HEAD_PX * (C + 4) + 11 * (size_t)C) * sizeof(float);
+        const dim3 grid(cdiv(P.P0, HEAD_PX), Bt);
+        hipLaunchKernelGGL(k_head, grid, dim3(256), shm, st, P.a64, P.P0, C, P.sc(10), P.sh(10), net->out_w, P.r);
         TCX_TRY(check_launch("k_head"));
     }
     return TCX_OK;

@@ -51,13 +51,16 @@ _SIGS = {
     "tcx_prof_read": (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                               ctypes.POINTER(ctypes.c_double)]),
     "tcx_conv2d": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp, c_fp, c_int,
-                           c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp]),
+                           c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp, c_fp,
+                           c_fp]),
     "tcx_pack_conv_weight": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_pack_convT_weight": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_convT2x": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_gn_partials": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),
     "tcx_gn_apply": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_int, c_fp, c_fp, c_float, c_int, c_fp]),
-    "tcx_upsample2x": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_gn_apply_tab": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp]),
+    "tcx_gn_finalize": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_float, c_fp, c_fp, c_fp]),
+    "tcx_upsample2x": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
     "tcx_attention": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_unet_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int]),
     "tcx_unet_eval": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_fp, c_fp, c_int, c_int, c_int,

@@ -103,7 +103,7 @@ class _VAEBase(nn.Module):
             Ho, Wo = H // 2, W // 2
             y = torch.empty((B, Ho, Wo, cout), device=x.device, dtype=torch.float32)
             check(lib().tcx_conv2d(ptr(h), None, B, 0, H, W, cin, 0, ptr(wpk), ptr(b), None, None, ptr(y), cout, cpad,
-                                   kpad, 4, 2, 1, 0, 0, 1, None, st), "enc conv")
+                                   kpad, 4, 2, 1, 0, 0, 1, None, None, None, None, None, st), "enc conv")
             h, H, W = y, Ho, Wo
         return h.reshape(B, -1)
 
