@@ -59,9 +59,13 @@ def bench(name, H, C1, C2, Co, ks, s, pad, ups, reps=20, gn=True):
     return us, fl
 
 
+only = os.environ.get("LAYER")
+reps = int(os.environ.get("REPS", "20"))
 tot_us = tot_fl = 0
 for l in LAYERS:
-    us, fl = bench(*l)
+    if only and l[0] != only:
+        continue
+    us, fl = bench(*l, reps=reps)
     if l[0] not in ("us2(pre)",):
         tot_us += us; tot_fl += fl
 print(f"TOTAL {tot_us:.1f} us  {tot_fl / tot_us / 1e6:.1f} TF (mid counted once)")

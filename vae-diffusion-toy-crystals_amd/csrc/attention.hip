@@ -9,7 +9,144 @@
 namespace tcx {
 namespace {
 
-constexpr int QROWS = 64;  // query rows per block (4 lanes each)
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------------------------
+// MFMA attention (fp32 v_mfma_f32_32x32x2_f32): one block per (head, batch), one wave per 32
+// queries, K and V of the head staged in LDS once.
+//   S^T = K Q^T : A = K rows (keys) from LDS, B = Q^T held in registers (query on the lane);
+//                 the K-dim d is split by lane half: half h owns d in [h*D/2, (h+1)*D/2).
+//   softmax over keys = over the 16 accumulator registers x N/32 tiles of a lane + one xor-32
+//                 shuffle (both lane halves hold the same query).
+//   O^T = V^T P^T: the probability accumulators ARE the B operands (key = (r&3)+8(r>>2)+4h of
+//                 tile n, query on the lane), A = V^T read from LDS with the same key order.
+// ---------------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(512) void k_attention_mfma(const float* __restrict__ qkv, float* __restrict__ out, int N,
+                                                        int C, float scale) {
+    constexpr int HD = D / 2;           // d per lane half
+    constexpr int KS = D + 4;           // K row stride in LDS ((D+4)/4 odd: conflict-free b128)
+    constexpr int DT = (D + 31) / 32;   // 32-row tiles of O^T
+    constexpr int VS = DT * 32;         // V row stride (zero padded to the tile)
+    constexpr int MAXT = 8;             // key tiles (N <= 256)
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* Ks = sm;
+    float* Vs = sm + (size_t)N * KS;
+    const int b = blockIdx.y, h = blockIdx.x;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const size_t rs = 3 * (size_t)C;
+    const float* base = qkv + (size_t)b * N * rs;
+    constexpr int D4 = D / 4;
+    for (int i = tid; i < N * D4; i += nthr) {
+        const int j = i / D4, d4 = i - (i / D4) * D4;
+        const float* src = base + (size_t)j * rs + h * D + d4 * 4;
+        *reinterpret_cast<float4*>(Ks + j * KS + d4 * 4) = *reinterpret_cast<const float4*>(src + C);
+        *reinterpret_cast<float4*>(Vs + j * VS + d4 * 4) = *reinterpret_cast<const float4*>(src + 2 * C);
+    }
+    if (VS > D) {
+        for (int i = tid; i < N * (VS - D); i += nthr) {
+            const int j = i / (VS - D), e = i - (i / (VS - D)) * (VS - D);
+            Vs[j * VS + D + e] = 0.f;
+        }
+    }
+    __syncthreads();
+    const int lane = tid & 63, w = tid >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    const int q = w * 32 + li;
+    const int nkt = N / 32;
+    // Q^T fragment: this lane's query, d in [HD*lh, HD*lh + HD)
+    float qf[HD];
+    {
+        const float* qs = base + (size_t)q * rs + h * D + HD * lh;
+#pragma unroll
+        for (int s4 = 0; s4 < HD / 4; ++s4) {
+            const float4 v = *reinterpret_cast<const float4*>(qs + 4 * s4);
+            qf[4 * s4 + 0] = v.x; qf[4 * s4 + 1] = v.y; qf[4 * s4 + 2] = v.z; qf[4 * s4 + 3] = v.w;
+        }
+    }
+    f32x16 sacc[MAXT];
+#pragma unroll
+    for (int n = 0; n < MAXT; ++n) {
+        sacc[n] = (f32x16){};
+        if (n < nkt) {
+            const float* kr = Ks + (n * 32 + li) * KS + HD * lh;
+#pragma unroll
+            for (int s4 = 0; s4 < HD / 4; ++s4) {
+                const float4 kv = *reinterpret_cast<const float4*>(kr + 4 * s4);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qf[4 * s4 + 0], sacc[n], 0, 0, 0);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qf[4 * s4 + 1], sacc[n], 0, 0, 0);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qf[4 * s4 + 2], sacc[n], 0, 0, 0);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qf[4 * s4 + 3], sacc[n], 0, 0, 0);
+            }
+        }
+    }
+    // softmax over the keys of query q: exp((s - max) * scale), scale = 1/sqrt(D) > 0
+    float m = -INFINITY;
+#pragma unroll
+    for (int n = 0; n < MAXT; ++n)
+        if (n < nkt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) m = fmaxf(m, sacc[n][r]);
+        }
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float l = 0.f;
+#pragma unroll
+    for (int n = 0; n < MAXT; ++n)
+        if (n < nkt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float pv = expf((sacc[n][r] - m) * scale);
+                sacc[n][r] = pv;
+                l += pv;
+            }
+        }
+    l += __shfl_xor(l, 32);
+    // O^T[d][q] = sum_key V[key][d] P^T[key][q]
+    f32x16 oacc[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) oacc[t] = (f32x16){};
+#pragma unroll
+    for (int n = 0; n < MAXT; ++n)
+        if (n < nkt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = n * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const float* vr = Vs + key * VS + li;
+#pragma unroll
+                for (int t = 0; t < DT; ++t)
+                    oacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr[t * 32], sacc[n][r], oacc[t], 0, 0, 0);
+            }
+        }
+    const float inv = 1.f / l;
+    float* dst = out + ((size_t)b * N + q) * C + h * D;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (d < D) dst[d] = oacc[t][r] * inv;
+        }
+}
+
+template <int D>
+int launch_attn_mfma(const float* qkv, float* out, int Bt, int N, int C, int heads, hipStream_t st) {
+    const float scale = (float)(1.0 / std::sqrt((double)D));
+    constexpr int KS = D + 4, VS = ((D + 31) / 32) * 32;
+    const size_t shm = (size_t)N * (KS + VS) * sizeof(float);
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_mfma<D>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
+            set_error("tcx_attention: cannot enable 160 KB dynamic LDS");
+            return TCX_EHIP;
+        }
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_attention_mfma<D>), dim3(heads, Bt), dim3(2 * N), shm, st, qkv, out, N, C, scale);
+    return check_launch("tcx_attention(mfma)");
+}
+
+constexpr int QROWS = 64;  // query rows per block (4 lanes each) of the VALU fallback
 constexpr int MAXK = 64;   // keys per lane (N <= 256)
 
 template <int D>
@@ -138,6 +275,17 @@ extern "C" int tcx_attention(const float* qkv, float* out, int Bt, int N, int C,
     if (Bt == 0) return TCX_OK;
     const int D = C / heads;
     hipStream_t st = (hipStream_t)stream;
+    if (N % 32 == 0) {  // MFMA path (every U-Net bottleneck: N = (H/4)*(W/4))
+        switch (D) {
+            case 8: return launch_attn_mfma<8>(qkv, out, Bt, N, C, heads, st);
+            case 16: return launch_attn_mfma<16>(qkv, out, Bt, N, C, heads, st);
+            case 24: return launch_attn_mfma<24>(qkv, out, Bt, N, C, heads, st);
+            case 32: return launch_attn_mfma<32>(qkv, out, Bt, N, C, heads, st);
+            case 48: return launch_attn_mfma<48>(qkv, out, Bt, N, C, heads, st);
+            case 64: return launch_attn_mfma<64>(qkv, out, Bt, N, C, heads, st);
+            default: break;
+        }
+    }
     switch (D) {
         case 8: return launch_attn<8>(qkv, out, Bt, N, C, heads, st);
         case 16: return launch_attn<16>(qkv, out, Bt, N, C, heads, st);

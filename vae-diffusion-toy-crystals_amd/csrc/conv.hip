@@ -55,11 +55,25 @@ struct ConvParams {
     // GroupNorm+SiLU prologue of each source: x -> silu(x * scale[b][c] + shift[b][c]) applied
     // when the staged chunk is written to LDS (tables from tcx_gn_finalize; null = raw source)
     const float *sc1, *sh1, *sc2, *sh2;
+    unsigned bytes1, bytes2, bytesw;  // buffer extents for the MODE 3 raw-buffer loads
 };
 
 constexpr int PRO_MAXC = 384;  // max channels per source for the fused GN prologue
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Raw buffer load (32-bit byte offset, hardware range check: an offset past num_records reads 0)
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const float* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)bytes, 0x00020000);
+}
+// 0x80000000: beyond every num_records (extents are < 2^31) with or without the SGPR offset
+// added, and no 32-bit wrap -> the load returns zeros
+constexpr int kOOB = (int)0x80000000u;
+constexpr int MAXTAP = 16;  // MODE 3 offset table: up to 4x4 kernels
 
 __device__ __forceinline__ float4 f4_fma(float s, float4 a, float4 acc) {
     return make_float4(fmaf(s, a.x, acc.x), fmaf(s, a.y, acc.y), fmaf(s, a.z, acc.z), fmaf(s, a.w, acc.w));
@@ -80,8 +94,11 @@ __device__ __forceinline__ void bilin_axis(int d, int n, int& i0, int& i1, float
 // MODE 0: float4 loads, per-lane (tap, ci) decode (Cin % 4 == 0)
 // MODE 1: scalar loads, any Cin (the Cin = 1 first convs)
 // MODE 2: float4 loads through a bilinear x2 upsample of the source
-// MODE 3: float4 loads, chunk-uniform (SGPR) decode: Cin % 32 == 0 and C1 % 32 == 0, so a
-//         32-deep K chunk is one tap of one source (every 3x3/4x4 layer of the U-Net)
+// MODE 3: float4 raw-buffer loads, chunk-uniform (SGPR) decode: Cin % 32 == 0, C1 % 32 == 0 and
+//         C2 in {0, C1}, so a 32-deep K chunk is one tap of one source (every 3x3/4x4 layer of
+//         the U-Net).  The byte offset of each (tap, tile pixel) is built once per workgroup in
+//         an LDS table; per chunk a thread reads its 4 pixels' offsets with one ds_read_b128 and
+//         the channel offset rides in the scalar soffset — no per-chunk im2col VALU.
 template <int NT, int MODE, bool CIRC, bool PRO>
 __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     constexpr int BN = 32 * NT;
@@ -89,6 +106,8 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDA];
     // fused GN prologue tables of this tile's image: [src1 scale, src1 shift, src2 scale, src2 shift]
     __shared__ __attribute__((aligned(16))) float Tr[PRO ? 4 * PRO_MAXC : 4];
+    // MODE 3: [tap][prow][i] byte offset of tile pixel prow + 32 i at that tap (kOOB if masked)
+    __shared__ __attribute__((aligned(16))) int Ptab[MODE == 3 ? MAXTAP * BM : 4];
 
     const int nwg = gridDim.x;
     const int tile = xcd_remap(blockIdx.x, nwg);
@@ -130,6 +149,8 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
         int tsel;  // which prologue table (0 = source 1, 2 = source 2)
         bool tr;   // apply the GN+SiLU prologue to this chunk
         int cb;    // chunk's first channel within its source (MODE 3)
+        int tap;   // chunk's tap (MODE 3, uniform)
+        bool s1;   // chunk comes from source 1 (MODE 3, uniform)
     };
     auto decode = [&](int c) -> Dec {
         Dec d;
@@ -139,15 +160,17 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
             const int ci0 = kc - tap * p.Cin;
             d.kval = tap < p.ks * p.ks;
             tap = d.kval ? tap : 0;
+            d.tap = tap;
             d.dy = tap / p.ks;
             d.dx = tap - d.dy * p.ks;
             const bool s1 = ci0 < p.C1;
             d.src = s1 ? p.x1 : p.x2;
             d.cs = s1 ? p.C1 : p.C2;
-            d.cc = (s1 ? ci0 : ci0 - p.C1) + k4 * 4;
+            d.cc = (s1 ? ci0 : ci0 - p.C1) * 4;  // byte offset within the pixel (soffset)
             d.tsel = s1 ? 0 : 2;
             d.tr = s1 ? p.sc1 != nullptr : p.sc2 != nullptr;
             d.cb = s1 ? ci0 : ci0 - p.C1;
+            d.s1 = s1;
         } else {
             const int k = c * BK + k4 * 4;
             int tap = k / p.Cin;
@@ -163,8 +186,46 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
             d.tsel = 0;
             d.tr = false;
             d.cb = 0;
+            d.tap = 0;
+            d.s1 = s1;
         }
         return d;
+    };
+
+    __amdgpu_buffer_rsrc_t r1, r2, rw;
+    int boffw[NT];
+    int4 poff;  // MODE 3: byte offsets of the thread's 4 pixels at the prefetched chunk's tap
+    if constexpr (MODE == 3) {
+        r1 = mk_rsrc(p.x1, p.bytes1);
+        r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
+        rw = mk_rsrc(p.w, p.bytesw);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) boffw[j] = ((n0 + prow + 32 * j) * p.kpad + k4 * 4) * 4;
+        const int ntap = p.ks * p.ks;
+        const int rowb = p.C1 * 4;  // bytes per source pixel (C2 == C1 when there are two)
+        for (int e = tid; e < ntap * BM; e += 256) {
+            const int tap = e / BM, q = e - tap * BM;
+            const int m = m0 + q;
+            const int mm = m < p.M ? m : 0;
+            const int b = mm / p.HoWo;
+            const int r = mm - b * p.HoWo;
+            const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+            const int bs = p.bmod > 0 ? b % p.bmod : b;
+            const int dy = tap / p.ks, dx = tap - (tap / p.ks) * p.ks;
+            int yr = oy * p.stride - p.pad_y + dy, xr = ox * p.stride - p.pad_x + dx;
+            bool ok = m < p.M;
+            if (CIRC) {
+                yr = wrap_idx(yr, p.Hi);
+                xr = wrap_idx(xr, p.Wi);
+            } else {
+                ok = ok && yr >= 0 && yr < p.Hi && xr >= 0 && xr < p.Wi;
+            }
+            Ptab[tap * BM + (q & 31) * 4 + (q >> 5)] = ok ? ((bs * p.H + yr) * p.W + xr) * rowb : kOOB;
+        }
+        __syncthreads();
+    }
+    auto read_poff = [&](const Dec& d) {
+        poff = *reinterpret_cast<const int4*>(&Ptab[d.tap * BM + prow * 4]);
     };
 
     // A gather for pixel row i (all loads unconditional: masked elements read g_zero4; a
@@ -190,6 +251,10 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
                 v[e] = *(ok ? a : g_zero4);
             }
             ra[i] = make_float4(v[0], v[1], v[2], v[3]);
+        } else if constexpr (MODE == 3) {
+            // masked pixels carry kOOB: the buffer unit returns zeros (kpad == K: no K tail)
+            const int po = i == 0 ? poff.x : i == 1 ? poff.y : i == 2 ? poff.z : poff.w;
+            ra[i] = bld4(d.s1 ? r1 : r2, po + k4 * 16, d.cc);
         } else {
             const int yr = piy[i] + d.dy, xr = pix[i] + d.dx;
             const bool inb = yr >= 0 && yr < p.Hi && xr >= 0 && xr < p.Wi;
@@ -220,10 +285,15 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
         }
     };
     auto load_b = [&](int c) {
+        if constexpr (MODE == 3) {
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const int co = n0 + prow + 32 * j;
-            rb[j] = ld4(p.w + (size_t)co * p.kpad + c * BK + k4 * 4);
+            for (int j = 0; j < NT; ++j) rb[j] = bld4(rw, boffw[j], c * BK * 4);
+        } else {
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int co = n0 + prow + 32 * j;
+                rb[j] = ld4(p.w + (size_t)co * p.kpad + c * BK + k4 * 4);
+            }
         }
     };
     auto store_chunk = [&](int buf) {
@@ -258,6 +328,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     }
     {
         const Dec d0 = decode(0);
+        if constexpr (MODE == 3) read_poff(d0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) load_a(d0, 0, i);
         load_b(0);
@@ -309,6 +380,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
         // the first MFMA groups so their address VALU issues in the MFMA shadow (T14/T19).
         const int cn = c + 1 < p.nchunks ? c + 1 : c;
         const Dec d = decode(cn);
+        if constexpr (MODE == 3) read_poff(d);
         read_frags(cur, 1, dc, fa1, fb1);
         load_a(d, cn, 0);
         load_a(d, cn, 1);
@@ -337,12 +409,15 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     const bool gn = p.gn != nullptr;
     double* red = reinterpret_cast<double*>(&As[0][0]);  // [4 waves][BN][2] (LDS free after the loop)
     const bool dense_out = p.osy == 1 && p.osx == 1;
+    const bool one_img = p.HoWo % BM == 0;  // the whole 128-pixel tile belongs to image m0 / HoWo
+    const int btile = m0 / p.HoWo;
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
         const int co = n0 + n * 32 + li;
         const bool cv = co < p.Cout;
         const int coc = cv ? co : 0;
         const float bco = p.bias ? p.bias[coc] : 0.f;
+        const float bbt = (p.bias_b && one_img) ? p.bias_b[(size_t)btile * p.Cout + coc] : 0.f;
         size_t oidx[16];
         bool ok[16];
         float add[16];
@@ -352,16 +427,17 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
             const int m = m0 + wv * 32 + row;
             ok[r] = m < p.M && cv;
             const int mm = m < p.M ? m : p.M - 1;
-            const int b = mm / p.HoWo;
+            add[r] = bco + bbt;
             if (dense_out) {
                 oidx[r] = (size_t)mm * p.Cout + coc;
+                if (p.bias_b && !one_img) add[r] += p.bias_b[(size_t)(mm / p.HoWo) * p.Cout + coc];
             } else {
+                const int b = mm / p.HoWo;
                 const int rr = mm - b * p.HoWo;
                 const int oy = rr / p.Wo, ox = rr - (rr / p.Wo) * p.Wo;
                 oidx[r] = ((size_t)b * p.Hy * p.Wy + (size_t)(oy * p.osy + p.ooy) * p.Wy + (ox * p.osx + p.oox)) * p.Cout + coc;
+                if (p.bias_b) add[r] += p.bias_b[(size_t)b * p.Cout + coc] - bbt;
             }
-            add[r] = bco;
-            if (p.bias_b) add[r] += p.bias_b[(size_t)b * p.Cout + coc];
         }
         if (p.resid) {
 #pragma unroll
@@ -414,7 +490,10 @@ template <int NT>
 int launch_nt(const ConvParams& p, int mode, hipStream_t st) {
     const int nm = cdiv(p.M, BM);
     const dim3 grid(nm * p.n_nblk), block(256);
-    const bool uni = mode == 0 && p.Cin % BK == 0 && p.C1 % BK == 0;  // chunk-uniform decode
+    // chunk-uniform decode + raw-buffer loads (byte extents must fit the 32-bit offsets)
+    const bool uni = mode == 0 && p.Cin % BK == 0 && p.C1 % BK == 0 && (p.C2 == 0 || p.C2 == p.C1) &&
+                     p.ks * p.ks <= MAXTAP && p.kpad == p.ks * p.ks * p.Cin && p.Hi == p.H && p.Wi == p.W &&
+                     p.bytes1 && (p.C2 == 0 || p.bytes2) && p.bytesw;
     const bool pro = p.sc1 || p.sc2;
     if (pro) {  // validated by the caller: uni && circular
         hipLaunchKernelGGL((k_conv<NT, 3, true, true>), grid, block, 0, st, p);
@@ -533,13 +612,24 @@ extern "C" int tcx_conv2d(const float* x1, const float* x2, int Bt, int bmod, in
     }
     if (gn_stats) TCX_REQUIRE(p.HoWo % BM == 0, "tcx_conv2d: fused GN stats need Ho*Wo %% 128 == 0");
     p.sc1 = pro_scale1; p.sh1 = pro_shift1; p.sc2 = pro_scale2; p.sh2 = pro_shift2;
+    {
+        const size_t bsrc = bmod > 0 ? (size_t)bmod : (size_t)Bt;
+        const size_t lim = (size_t)1 << 31;
+        const size_t b1 = bsrc * H * W * C1 * sizeof(float), b2 = bsrc * H * W * C2 * sizeof(float);
+        const size_t bw = (size_t)cout_pad * kpad * sizeof(float);
+        p.bytes1 = b1 < lim ? (unsigned)b1 : 0u;
+        p.bytes2 = b2 < lim ? (unsigned)b2 : 0u;
+        p.bytesw = bw < lim ? (unsigned)bw : 0u;
+    }
     if (pro_scale1 || pro_scale2) {
         TCX_REQUIRE((pro_scale1 != nullptr) == (pro_shift1 != nullptr) &&
                     (pro_scale2 != nullptr) == (pro_shift2 != nullptr), "tcx_conv2d: prologue scale/shift pairs");
         TCX_REQUIRE(mode == 0 && Cin % BK == 0 && C1 % BK == 0 && circular && bmod == 0 && p.HoWo % BM == 0 &&
-                    C1 <= PRO_MAXC && C2 <= PRO_MAXC && (pro_scale2 == nullptr || x2 != nullptr),
-                    "tcx_conv2d: fused GN prologue needs Cin,C1 %% 32 == 0, circular, no bmod/upsample, "
-                    "Ho*Wo %% 128 == 0, C <= 384");
+                    C1 <= PRO_MAXC && C2 <= PRO_MAXC && (pro_scale2 == nullptr || x2 != nullptr) &&
+                    (C2 == 0 || C2 == C1) && ks * ks <= MAXTAP && kpad == ks * ks * Cin &&
+                    p.bytes1 && (C2 == 0 || p.bytes2) && p.bytesw,
+                    "tcx_conv2d: fused GN prologue needs Cin,C1 %% 32 == 0, C2 in {0,C1}, kpad == K, circular, "
+                    "no bmod/upsample, Ho*Wo %% 128 == 0, C <= 384, extents < 2 GiB");
     }
     TCX_REQUIRE(aligned16(wpk), "tcx_conv2d: packed weight must be 16-B aligned");
     return launch_conv(p, cout_pad, mode, (hipStream_t)stream);

@@ -103,11 +103,95 @@ __global__ __launch_bounds__(256) void k_cond(CondArgs a, const float* __restric
     }
 }
 
+// First conv of down1 (17 -> C0, 3x3 circular) with the 16 constant map channels already folded
+// into bias_b: y[b,p,co] = bias_b[b][co] + sum_tap w0[co][tap] * x[b % bmod][wrap(p + tap)].
+// Output-write bound (C0 floats per input float): a 64-pixel x C0 tile is built in LDS (small, so
+// several blocks per CU overlap their load/compute/store phases) and written as one contiguous
+// block; per-channel {sum, sumsq} (fp64) of the tile feed the following GroupNorm.
+// grid (HW/64, Bt); block 256 = 64 pixels x 4 channel quarters; needs HW % 128 == 0, C0 % 16 == 0.
+constexpr int FIRST_PX = 64;
+__global__ __launch_bounds__(256) void k_conv_first(const float* __restrict__ x, int bmod, int H, int W, int C0,
+                                                    const float* __restrict__ w0, int kpad,
+                                                    const float* __restrict__ bias_b, float* __restrict__ y,
+                                                    double* __restrict__ gn) {
+    extern __shared__ __attribute__((aligned(16))) float fs[];  // tile[64][C0+4] | w[9][C0] | red[4][C0][2] (dbl)
+    const int LD = C0 + 4;
+    float* tile = fs;
+    float* w = fs + FIRST_PX * LD;
+    double* red = reinterpret_cast<double*>(w + 9 * C0);
+    const int HW = H * W;
+    const int b = blockIdx.y;
+    const int p0 = blockIdx.x * FIRST_PX;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 9 * C0; i += 256) {
+        const int co = i / 9, k = i - (i / 9) * 9;  // w0 packed [co][kpad] with k = tap (Cin = 1)
+        w[k * C0 + co] = w0[(size_t)co * kpad + k];
+    }
+    __syncthreads();
+    const int px = tid & (FIRST_PX - 1), qtr = tid >> 6;
+    const int p = p0 + px;
+    const int yy = p / W, xx = p - (p / W) * W;
+    const float* xb = x + (size_t)(b % bmod) * HW;
+    float xv[9];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) xv[dy * 3 + dx] = xb[wrap_idx(yy + dy - 1, H) * W + wrap_idx(xx + dx - 1, W)];
+    const int cq = C0 / 4;
+    const float* bb = bias_b + (size_t)b * C0;
+    for (int c = qtr * cq; c < (qtr + 1) * cq; c += 4) {
+        float4 a = *reinterpret_cast<const float4*>(bb + c);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const float4 wk = *reinterpret_cast<const float4*>(&w[k * C0 + c]);  // broadcast read
+            a.x = fmaf(wk.x, xv[k], a.x);
+            a.y = fmaf(wk.y, xv[k], a.y);
+            a.z = fmaf(wk.z, xv[k], a.z);
+            a.w = fmaf(wk.w, xv[k], a.w);
+        }
+        *reinterpret_cast<float4*>(&tile[px * LD + c]) = a;
+    }
+    __syncthreads();
+    float* dst = y + ((size_t)b * HW + p0) * C0;
+    const int C4 = C0 / 4;
+    for (int i = tid; i < FIRST_PX * C4; i += 256) {
+        const int r = i / C4, c = (i - (i / C4) * C4) * 4;
+        *reinterpret_cast<float4*>(dst + (size_t)i * 4) = *reinterpret_cast<const float4*>(&tile[r * LD + c]);
+    }
+    if (gn) {  // 128-pixel GN split = 2 tiles: tile t contributes to split blockIdx.x / 2 (atomic-free:
+               // each half-split is written to its own slot and summed by the consumer's fold)
+        const int nsplit = HW / FIRST_PX;
+        for (int i = tid; i < 4 * C0; i += 256) {
+            const int c = i % C0, part = i / C0;  // 4 row quarters of 16 pixels
+            double s = 0.0, q = 0.0;
+            for (int r = part * 16; r < part * 16 + 16; ++r) {
+                const double v = tile[r * LD + c];
+                s += v;
+                q += v * v;
+            }
+            red[(part * C0 + c) * 2] = s;
+            red[(part * C0 + c) * 2 + 1] = q;
+        }
+        __syncthreads();
+        for (int c = tid; c < C0; c += 256) {
+            double s = 0.0, q = 0.0;
+#pragma unroll
+            for (int part = 0; part < 4; ++part) {
+                s += red[(part * C0 + c) * 2];
+                q += red[(part * C0 + c) * 2 + 1];
+            }
+            double* g = gn + (((size_t)b * nsplit + blockIdx.x) * C0 + c) * 2;
+            g[0] = s;
+            g[1] = q;
+        }
+    }
+}
+
 // Head: out conv (C -> 1, 3x3 circular) split into a per-pixel channel reduction here and a
 // 9-tap circular gather in k_step.  grid (HW/128, Bt); block 256.  The 128-pixel x C tile is read
 // coalesced (contiguous 128*C floats), GroupNorm+SiLU applied from the per-image table, staged in
 // LDS; then thread (pixel, tap set) computes r[b][tap][p] = sum_c h[p][c] * w_out[c][tap].
-constexpr int HEAD_PX = 128;
+constexpr int HEAD_PX = 64;
 __global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int HW, int C, const float* __restrict__ tsc,
                                               const float* __restrict__ tsh, const float* __restrict__ w_out,
                                               float* __restrict__ r) {
@@ -143,18 +227,17 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int H
     }
     __syncthreads();
     const int px = tid & (HEAD_PX - 1);
-    const int half = tid >> 7;  // taps 0..4 or 5..8
+    const int tg = tid >> 6;  // tap group: taps tg, tg + 4, (tg + 8 for group 0)
     if (px >= npx) return;
-    const int k0 = half ? 5 : 0, k1 = half ? 9 : 5;
-    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    const int nk = tg == 0 ? 3 : 2;
+    float acc[3] = {0.f, 0.f, 0.f};
     const float* row = &tile[px * LD];
     for (int c = 0; c < C; c += 4) {
         const float4 v = *reinterpret_cast<const float4*>(row + c);
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int k = k0 + j;
-            if (k < k1) {
-                const float4 ww = *reinterpret_cast<const float4*>(&w[k * C + c]);
+        for (int j = 0; j < 3; ++j) {
+            if (j < nk) {
+                const float4 ww = *reinterpret_cast<const float4*>(&w[(tg + 4 * j) * C + c]);  // broadcast
                 float a = acc[j];
                 a = fmaf(v.x, ww.x, a);
                 a = fmaf(v.y, ww.y, a);
@@ -166,8 +249,8 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int H
     }
     float* dst = r + (size_t)b * 9 * HW + p0 + px;
 #pragma unroll
-    for (int j = 0; j < 5; ++j)
-        if (k0 + j < k1) dst[(size_t)(k0 + j) * HW] = acc[j];
+    for (int j = 0; j < 3; ++j)
+        if (j < nk) dst[(size_t)(tg + 4 * j) * HW] = acc[j];
 }
 
 // ---------------------------------------------------------------- Philox4x32-10
@@ -416,11 +499,18 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // down1 (first conv: x_t channel only, maps folded into bias0; the conv bias is inside bias0)
     {
         const tcx_conv& c0 = net->down1_0;
-        const bool fz = (H * W) % 128 == 0;
-        TCX_TRY(tcx_conv2d(x, nullptr, Bt, B, H, W, 1, 0, c0.w, nullptr, P.bias0, nullptr, P.a64, c0.cout, c0.cout_pad,
-                           c0.kpad, 3, 1, 1, 1, 0, 0, fz ? gn : nullptr, nullptr, nullptr, nullptr, nullptr, st));
-        if (fz) ns = H * W / 128;
-        else { ns = std::max(1, H * W / 512); TCX_TRY(tcx_gn_partials(P.a64, Bt, H * W, C, ns, gn, st)); }
+        if ((H * W) % FIRST_PX == 0 && C % 16 == 0 && c0.kpad == 32) {
+            const size_t shm = ((size_t)FIRST_PX * (C + 4) + 9 * (size_t)C) * sizeof(float) + 8 * (size_t)C * sizeof(double);
+            hipLaunchKernelGGL(k_conv_first, dim3(H * W / FIRST_PX, Bt), dim3(256), shm, st, x, B, H, W, C, c0.w,
+                               c0.kpad, P.bias0, P.a64, gn);
+            TCX_TRY(check_launch("k_conv_first"));
+            ns = H * W / FIRST_PX;
+        } else {
+            TCX_TRY(tcx_conv2d(x, nullptr, Bt, B, H, W, 1, 0, c0.w, nullptr, P.bias0, nullptr, P.a64, c0.cout,
+                               c0.cout_pad, c0.kpad, 3, 1, 1, 1, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, st));
+            ns = std::max(1, H * W / 512);
+            TCX_TRY(tcx_gn_partials(P.a64, Bt, H * W, C, ns, gn, st));
+        }
     }
     TCX_TRY(norm(0, P.a64, P.P0, C));
     TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.h1, gn, &ns, st,
@@ -471,9 +561,10 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     TCX_TRY(norm(7, P.b32, P.P1, C));
     TCX_TRY(conv_gn(net->up2_1, P.b32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, gn, &ns, st,
                     SC(7), SH(7)));
-    // us1: upsample silu(gn(a32)) into the free b64 buffer (GN applied on the taps), conv -> a64 [C]
-    TCX_TRY(gn_tab(net, P, 8, P.P1, C, gn, ns, st));
-    TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, P.sc(8), P.sh(8), st));
+    // us1: GN+SiLU of up2's output in place (1x per element; the upsample-side transform
+    // recomputed it for 4 taps per output and measured 3x slower), upsample into the free b64, conv
+    TCX_TRY(norm(8, P.a32, P.P1, C));
+    TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, st));
     TCX_TRY(conv_gn(net->us1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, nullptr, &ns, st));
     // up1 on cat[a64, silu(gn(h1))]
     TCX_TRY(conv_gn(net->up1_0, P.a64, P.h1, C, C, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.b64, gn, &ns, st, nullptr,
