@@ -201,6 +201,152 @@ int tcx_linear(const float* x1, int K1, const float* x2, int K2, const float* wp
 int tcx_layernorm_film(const float* x, float* y, int M, int Wd, const float* ln_w,
                        const float* ln_b, const float* gb, int ld_gb, float eps, void* stream);
 
+/* ------------------------------------------------------------------ training path (backward)
+ * The reference trains with torch autograd (loss.backward(), scripts/train_*.py); these are the
+ * native kernels behind the package's autograd Functions.  Activations NHWC fp32 contiguous. */
+
+/* Batched strided fp32-MFMA GEMM: for z in [0,batch): C_z = alpha * A_z B_z + beta * C_z (+ bias[n]).
+ * Element A_z(m,k) = A[off_a(z) + m*sa_m + k*sa_k], B_z(k,n) = B[off_b(z) + k*sb_k + n*sb_n],
+ * C_z(m,n) = C[off_c(z) + m*sc_m + n*sc_n], off_x(z) = (z / bdiv)*sx_hi + (z % bdiv)*sx_lo.
+ * Replaces nn.Linear forward/backward (every model) and the SDPA products Q K^T, P V and their
+ * backward (sde_score_model.py:150-157). */
+int tcx_gemm(int M, int N, int K, float alpha, const float* A, long long sa_m, long long sa_k,
+             const float* B, long long sb_k, long long sb_n, float beta, float* C, long long sc_m,
+             long long sc_n, const float* bias, int batch, int bdiv, long long sa_hi, long long sa_lo,
+             long long sb_hi, long long sb_lo, long long sc_hi, long long sc_lo, void* stream);
+
+/* Conv2d weight gradient dw[Cout][C1+C2][ks][ks] (= beta*dw + ...) from the NHWC input
+ * [x1 | x2] [Bt][H][W][C1+C2] and the output gradient dy [Bt][Ho][Wo][Cout] (circular or zero
+ * padding).  Also the ConvTranspose2d weight gradient (input/output roles swapped).  Backward of
+ * nn.Conv2d (sde_score_model.py:102-105,133-134,208-225; vae.py:19-26) / ConvTranspose2d (vae.py:35-42). */
+size_t tcx_conv_wgrad_workspace(int Bt, int Ho, int Wo, int Cin, int Cout, int ks);
+int tcx_conv_wgrad(const float* x1, const float* x2, int Bt, int H, int W, int C1, int C2, const float* dy,
+                   int Cout, int ks, int stride, int pad, int circular, float beta, float* dw, void* ws,
+                   size_t ws_bytes, void* stream);
+
+/* Stride-1 Conv2d data gradient as a forward conv: packs the flipped, transposed weight rows
+ * ci in [ci_lo, ci_lo + n_ci) of w [Cout][Cin][ks][ks] to wpk[cout_pad][kpad] with
+ * k = (dy*ks + dx)*Cout + co, value w[co][ci][ks-1-dy][ks-1-dx]; run tcx_conv2d(dy_out, ...,
+ * pad = ks-1-pad) with it.  Two-source (concat) inputs get one pack per source. */
+int tcx_pack_conv_dgrad_weight(const float* w, float* wpk, int Cout, int Cin, int ks, int ci_lo, int n_ci,
+                               int cout_pad, int kpad, void* stream);
+
+/* ConvTranspose2d(4, 2, 1) with circular (1) or zero (0) padding of the input grid: the data
+ * gradient of the stride-2 circular downsample convs (ds1/ds2, sde_score_model.py:208,210; the
+ * weight [Cout][Cin][4][4] packed by tcx_pack_convT_weight(w, wpk, Cout, Cin, ...)) and of the
+ * VAE encoder convs (zero padding). */
+int tcx_conv_transpose2x(const float* x, int Bt, int H, int W, int Cin, const float* wpk4, const float* bias,
+                         float* y, int Cout, int cout_pad, int kpad, int act, int circular, void* stream);
+
+/* GroupNorm forward statistics from fp64 partials: scale/shift tables [Bt][C] and per-(batch,
+ * group) mean / rstd [Bt][groups] saved for the backward (nn.GroupNorm, sde_score_model.py:103). */
+int tcx_gn_stats(const double* part, int Bt, int HW, int C, int groups, int nsplit, const float* gamma,
+                 const float* beta, float eps, float* scale, float* shift, float* mean, float* rstd,
+                 void* stream);
+
+/* Backward of y = silu?(GroupNorm(x)) (silu = 1: the _ConvBlock GN+SiLU pair, :103-105; 0: the
+ * attention norm, :150).  dgamma/dbeta optional. */
+size_t tcx_gn_bwd_workspace(int Bt, int HW, int C);
+int tcx_gn_bwd(const float* x, const float* dy, const float* scale, const float* shift, const float* mean,
+               const float* rstd, const float* gamma, int Bt, int HW, int C, int groups, int silu, float* dx,
+               float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
+
+/* Adjoint of tcx_upsample2x (nn.Upsample(2, bilinear, align_corners=False), :217-222). */
+int tcx_upsample2x_bwd(const float* dy, float* dx, int Bt, int H, int W, int C, void* stream);
+
+/* Column sums of x [Bt][HW][C]: per_batch[Bt][C] and/or total[C] (= beta*total + sum): conv/linear
+ * bias gradients and the folded constant-map channels of the first conv. */
+size_t tcx_colsum_workspace(int Bt, int HW, int C);
+int tcx_colsum(const float* x, int Bt, int HW, int C, float* per_batch, float* total, float beta, void* ws,
+               size_t ws_bytes, void* stream);
+
+/* Row softmax and its backward (SDPA, :150-157): P = softmax(S); dS = P * (dP - rowsum(dP * P)). */
+int tcx_softmax_rows(const float* S, float* P, long long rows, int n, void* stream);
+int tcx_softmax_bwd_rows(const float* P, const float* dP, float* dS, long long rows, int n, void* stream);
+
+/* Elementwise activation (1 ReLU, 2 Sigmoid, 3 SiLU) and its backward from the pre-activation. */
+int tcx_act_fwd(const float* z, float* y, size_t n, int act, void* stream);
+int tcx_act_bwd(const float* z, const float* dy, float* dz, size_t n, int act, void* stream);
+
+/* mean((a - b)^2) into out[0] (fp64 fixed-order reduction) and its gradient w.r.t. a:
+ * da = grad_out[0] * 2 (a - b) / n (sde_score_model.py:399, train_vae.py:309,
+ * train_diffusion_prior.py:265).  tcx_mse_loss needs >= 8 KiB + 256 B of workspace. */
+int tcx_mse_loss(const float* a, const float* b, size_t n, float* out, void* ws, size_t ws_bytes, void* stream);
+int tcx_mse_bwd(const float* a, const float* b, size_t n, const float* grad_out, float* da, void* stream);
+
+/* nn.Embedding backward: dW[rows][E] = sum over b with idx[b] == row of dout[b] (deterministic). */
+int tcx_embedding_bwd(const int64_t* idx, const float* dout, int B, int rows, int E, float* dW, void* stream);
+
+/* LayerNorm(+FiLM) forward saving mean/rstd, and its backward (FiLMResBlock / out_norm,
+ * diffusion_prior.py:39-54,113).  Backward writes dx, per-row dwrow = dl*xhat and dbrow = dl (sum them
+ * over rows with tcx_colsum for the LN weight/bias grads) and, with FiLM, dgb [M][2Wd] = [dh*l | dh]. */
+int tcx_ln_fwd(const float* x, float* y, int M, int Wd, const float* w, const float* b, const float* gb,
+               int ld_gb, float eps, float* mean, float* rstd, void* stream);
+int tcx_ln_bwd(const float* x, const float* dh, int M, int Wd, const float* w, const float* b, const float* gb,
+               int ld_gb, const float* mean, const float* rstd, float* dx, float* dwrow, float* dbrow, float* dgb,
+               void* stream);
+
+/* Multi-tensor optimiser steps over a DEVICE table of tensors.
+ * tcx_adam: torch.optim.Adam (amsgrad off) step `step` (1-based) on every {p, g, m, v, n}.
+ * tcx_ema:  p = p*decay + (1-decay)*g for every entry ({p_ema, p_model}; m/v unused)
+ * (train_sde_score_model.py:233-240). */
+typedef struct tcx_adam_tensor {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    long long n;
+} tcx_adam_tensor;
+int tcx_adam(const tcx_adam_tensor* table, int ntensors, long long max_n, float lr, float beta1, float beta2,
+             float eps, float weight_decay, long long step, void* stream);
+int tcx_ema(const tcx_adam_tensor* table, int ntensors, long long max_n, float decay, void* stream);
+
+/* ---- small training-path kernels (conditioning inputs, layout, losses) */
+/* score-net conditioning inputs (sde_score_model.py:17-32,66-79): te = timestep_embedding(t, E),
+ * yv = theta-sincos rewrite of y_cont, yc = clamp(y_cat, 0, n_types). */
+int tcx_cond_inputs(const float* t, const int64_t* y_cat, const float* y_cont, int B, int E, int n_types, int ycd,
+                    float* te, float* yv, int64_t* yc, void* stream);
+/* prior timestep embedding [sin, cos](t * freqs) (diffusion_prior.py:11-25; freqs from the host). */
+int tcx_prior_temb(const int64_t* t, const float* freqs, int B, int E, float* te, void* stream);
+/* nn.Embedding forward (row gather). */
+int tcx_embedding_fwd(const int64_t* idx, const float* W, int B, int E, float* out, void* stream);
+/* dst[r][c] = beta*dst + src with row strides: torch.cat / chunk of feature columns. */
+int tcx_copy2d(const float* src, long long ld_src, float* dst, long long ld_dst, int rows, int cols, float beta,
+               void* stream);
+/* dst[b][c][r] = src[b][r][c]: NHWC <-> NCHW at the VAE flatten (vae.py:51,72). */
+int tcx_transpose_bhc(const float* src, float* dst, int B, int R, int C, void* stream);
+/* First conv with the 16 constant map channels folded (sde_score_model.py:246): forward bias and backward. */
+int tcx_first_conv_bias(const float* maps, const float* w, const float* bias, int B, int C0, int nm, int ks,
+                        float* bias_b, void* stream);
+int tcx_first_conv_bwd(const float* S, const float* maps, const float* w, const float* dwx, int B, int C0, int nm,
+                       int ks, float* dmaps, float* dw, float* db, void* stream);
+/* diffusion_loss_eps data path (sde_score_model.py:380-389): t = u^p, x_t = alpha(t)(2x0-1) + sigma(t) eps;
+ * half_dbeta = 0.5*(beta_max - beta_min). */
+int tcx_qsample_vp(const float* x0, const float* eps, const float* u, float t_power, float beta_min,
+                   float half_dbeta, int B, int HW, float* t_out, float* x_t, void* stream);
+/* CFG condition dropout (:392-397); r = the rand(B) draws (NULL: no drop). */
+int tcx_cond_drop(const int64_t* y_cat, const float* y_cont, const float* r, float p, int B, int ycd, int n_types,
+                  int64_t* out_cat, float* out_cont, void* stream);
+/* prior training q_sample with t = clamp(long(u^2 T), 0, T-1) (train_diffusion_prior.py:256-260). */
+int tcx_prior_qsample(const float* z0, const float* eps, const float* u, const float* sqrt_ab, const float* sqrt_1mab,
+                      int T, int B, int Z, int64_t* t_out, float* z_t, void* stream);
+/* VAE reparameterise (vae.py:57-60) and kl_stats (train_vae.py:17-36) with their backward. */
+int tcx_reparam(const float* mu, const float* lv, const float* eps, size_t n, float* z, void* stream);
+int tcx_reparam_bwd(const float* lv, const float* eps, const float* dz, size_t n, float* dmu, float* dlv, float beta,
+                    void* stream);
+int tcx_vae_kl(const float* mu, const float* lv, int B, int Z, float free_bits, float* out, void* stream);
+int tcx_vae_kl_bwd(const float* mu, const float* lv, int B, int Z, float free_bits, const float* grad_out, float* dmu,
+                   float* dlv, float beta, void* stream);
+
+/* CondVAE._y_vec [one_hot | y_cont] with the optional training keep mask (vae.py:45-48,65-67). */
+int tcx_vae_yvec(const int64_t* y_cat, const float* y_cont, const float* keep_u, float cond_drop, int B, int n_types,
+                 int ycd, float* out, void* stream);
+/* DDIM eta=0 update in place (diffusion_prior.py:226-250); last != 0 returns z0_pred. */
+int tcx_ddim_step(float* z, const float* eps, size_t n, float abar_t, float abar_prev, int last, void* stream);
+/* DiffusionSchedule.q_sample with given integer t (diffusion_prior.py:194-201). */
+int tcx_q_sample(const float* z0, const int64_t* t, const float* eps, const float* sqrt_ab, const float* sqrt_1mab,
+                 int B, int Z, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,6 +24,8 @@ Reference call sites reproduced (file:line in /root/reference):
   CondVAE / VAE                        src/toycrystals/models/vae.py:8-134
   kl_stats + VAE loss                  scripts/train_vae.py:17-36,309-312
   DiffusionPriorFiLM / ddim_sample     src/toycrystals/models/diffusion_prior.py:57-252
+  score / VAE / prior training steps   scripts/train_sde_score_model.py:217-240,
+                                       scripts/train_vae.py:299-312, scripts/train_diffusion_prior.py:251-277
 """
 from __future__ import annotations
 
@@ -321,6 +323,133 @@ def gen_prior(name: str, width: int, n_blocks: int, store_weights: bool) -> None
          width=np.int64(width), n_blocks=np.int64(n_blocks), **ck, **extra)
 
 
+# ---------------------------------------------------------------- training (backward) goldens
+def _grad_sample(name: str, g: torch.Tensor, k: int = 64) -> dict:
+    """Checksums + k fixed-index samples of a gradient (full tensors for small ones)."""
+    a = g.detach().double().reshape(-1).numpy()
+    out = {"gck/" + name: np.array([a.sum(), np.abs(a).sum(), float(a.size)])}
+    if a.size <= 4096:
+        out["g/" + name] = g.detach().numpy()
+    else:
+        idx = np.random.RandomState(abs(hash(name)) % (2 ** 31)).choice(a.size, size=k, replace=False)
+        idx.sort()
+        out["gi/" + name] = idx.astype(np.int64)
+        out["gs/" + name] = a[idx].astype(np.float32)
+    return out
+
+
+def gen_train_score(name: str) -> None:
+    """diffusion_loss_eps backward (all parameter grads) + two torch.optim.Adam steps + EMA
+    (train_sde_score_model.py:217-240) at base_ch=16, draws recorded."""
+    torch.manual_seed(0)
+    model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=16)
+    perturb_norms(model, 5)
+    ck = sd_checksums(model)
+    ema = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=16)
+    ema.load_state_dict(model.state_dict())
+    sde = ref_sde.VPSDE(0.1, 30.0)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    g = torch.Generator().manual_seed(23)
+    B = 3
+    x0 = torch.rand(B, 1, 64, 64, generator=g)
+    y_cat, y_cont = cond_inputs(B, null_last=False)
+    out = {}
+    for step in range(2):
+        torch.manual_seed(100 + step)
+        u = torch.rand((B,))
+        eps = torch.randn((B, 1, 64, 64))
+        drop_u = torch.rand((B,))
+        torch.manual_seed(100 + step)
+        loss = ref_sde.diffusion_loss_eps(model, sde, x0, y_cat, y_cont, p_uncond=0.5, t_power=1.0)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if step == 0:
+            for k, p in model.named_parameters():
+                out["g/" + k] = p.grad.numpy().copy()
+        opt.step()
+        with torch.no_grad():
+            for pe, p in zip(ema.parameters(), model.parameters()):
+                pe.data.mul_(0.9).add_(p.data, alpha=1.0 - 0.9)
+        out[f"u{step}"] = u.numpy()
+        out[f"eps{step}"] = eps.numpy()
+        out[f"drop{step}"] = drop_u.numpy()
+        out[f"loss{step}"] = np.float64(loss.item())
+    keep = ("down1.net.0.weight", "mid.net.1.weight", "attn.qkv.weight", "cond_emb.cat_emb.weight",
+            "up1.net.3.bias", "out.weight", "time_mlp.0.weight")
+    for k, p in model.named_parameters():
+        if k in keep:
+            out["p2/" + k] = p.detach().numpy().copy()
+    for (k, _), pe in zip(model.named_parameters(), ema.parameters()):
+        if k in keep:
+            out["ema2/" + k] = pe.detach().numpy().copy()
+    save(name, x0=x0.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), p_uncond=np.float64(0.5), lr=np.float64(1e-3),
+         ema_decay=np.float64(0.9), base_ch=np.int64(16), **ck, **out)
+
+
+def gen_train_vae(name: str) -> None:
+    """CondVAE training step (train_vae.py:299-312): forward in train mode with cond_drop=0.1,
+    recon + beta * kl_used (free bits 0.05), backward.  Draws (reparam eps, keep mask u) recorded."""
+    torch.manual_seed(0)
+    model = ref_vae.CondVAE(z_dim=32, n_types=4, y_cont_dim=4, cond_drop=0.1)
+    ck = sd_checksums(model)
+    model.train()
+    g = torch.Generator().manual_seed(41)
+    B = 4
+    x = torch.rand(B, 1, 64, 64, generator=g)
+    y_cat = torch.tensor([0, 1, 2, 3])
+    y_cont = torch.zeros(B, 4)
+    y_cont[:, 1] = torch.rand(B, generator=g)
+    torch.manual_seed(9)
+    rep_eps = torch.randn(B, 32)
+    keep_u = torch.rand((B, 1))
+    torch.manual_seed(9)
+    x_hat, mu, logvar = model(x, y_cat, y_cont)
+    sys.path.insert(0, "/root/reference")
+    from scripts.train_vae import kl_stats
+    recon = torch.mean((x_hat - x) ** 2)
+    kl_used, kl_raw = kl_stats(mu, logvar, free_bits=0.05)
+    beta = 3e-4 * min(1.0, (0 + 1) / 5.0)
+    loss = recon + beta * kl_used
+    loss.backward()
+    gs = {}
+    for k, p in model.named_parameters():
+        gs.update(_grad_sample(k, p.grad))
+    save(name, x=x.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), rep_eps=rep_eps.numpy(),
+         keep_u=keep_u.numpy(), x_hat=x_hat.detach().numpy(), mu=mu.detach().numpy(),
+         logvar=logvar.detach().numpy(), loss=np.float64(loss.item()), recon=np.float64(recon.item()),
+         kl_used=np.float64(kl_used.item()), beta=np.float64(beta), free_bits=np.float64(0.05), **ck, **gs)
+
+
+def gen_train_prior(name: str) -> None:
+    """Prior training step (train_diffusion_prior.py:251-277): t = clamp(long(u^2 T)), q_sample,
+    MSE, backward; width 64, 2 blocks, T = 200 (the CLI default), stored weights (perturbed norms)."""
+    torch.manual_seed(0)
+    model = ref_prior.DiffusionPriorFiLM(z_dim=32, n_types=4, y_cont_dim=4, t_emb_dim=64, width=64, n_blocks=2,
+                                         y_cat_emb_dim=64)
+    perturb_norms(model, 13)
+    ck = sd_checksums(model)
+    model.train()
+    sched = ref_prior.DiffusionSchedule.linear(T=200, beta_start=1e-4, beta_end=1.0, device=torch.device("cpu"))
+    g = torch.Generator().manual_seed(51)
+    B = 6
+    z0 = torch.randn(B, 32, generator=g)
+    y_cat = torch.tensor([0, 1, 2, 3, 1, 0])
+    y_cont = torch.zeros(B, 4)
+    y_cont[:, 1] = torch.rand(B, generator=g)
+    torch.manual_seed(61)
+    u = torch.rand((B,))
+    t = torch.clamp((u ** 2 * 200).long(), 0, 199)
+    eps = torch.randn_like(z0)
+    z_t = sched.q_sample(z0=z0, t=t, eps=eps)
+    eps_pred = model(z_t, t, y_cat, y_cont)
+    loss = torch.mean((eps_pred - eps) ** 2)
+    loss.backward()
+    grads = {"g/" + k: p.grad.numpy() for k, p in model.named_parameters()}
+    save(name, z0=z0.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), u=u.numpy(), t=t.numpy(), eps=eps.numpy(),
+         z_t=z_t.detach().numpy(), eps_pred=eps_pred.detach().numpy(), loss=np.float64(loss.item()),
+         T=np.int64(200), beta_end=np.float64(1.0), **ck, **grads)
+
+
 def main() -> int:
     torch.set_num_threads(8)
     which = set(sys.argv[1:])
@@ -355,6 +484,10 @@ def main() -> int:
     if want("prior"):
         gen_prior("prior_w64_b2", 64, 2, store_weights=True)
         gen_prior("prior_w1024_b8", 1024, 8, store_weights=False)
+    if want("train"):
+        gen_train_score("train16_b3")
+        gen_train_vae("train_condvae_b4")
+        gen_train_prior("train_prior_w64")
     return 0
 
 

@@ -40,12 +40,16 @@ def rel_err(a, ref):
 
 @pytest.mark.parametrize("name,base,stored", [("unet16_b3", 16, True), ("unet96_b2", 96, False),
                                               ("unet32_b2_h32", 32, False)])
-def test_unet_forward_vs_reference(golden, name, base, stored):
+@pytest.mark.parametrize("grad", [False, True], ids=["fused", "autograd"])
+def test_unet_forward_vs_reference(golden, name, base, stored, grad):
+    """The fused evaluator (no grad) and the autograd training chain (grad) against the reference."""
     g = golden(name)
     sd = {k[2:]: v for k, v in g.items() if k.startswith("w/")} if stored else None
     m = unet(base, sd)
-    with torch.no_grad():
-        eps = m(cu(g["x_t"]), cu(g["t"]), cu(g["y_cat"]), cu(g["y_cont"])).cpu().numpy()
+    with torch.set_grad_enabled(grad):
+        eps = m(cu(g["x_t"]), cu(g["t"]), cu(g["y_cat"]), cu(g["y_cont"]))
+        assert eps.requires_grad == grad
+        eps = eps.detach().cpu().numpy()
     assert eps.shape == g["eps"].shape
     assert rel_err(eps, g["eps"]) < 2e-5
 
@@ -163,23 +167,27 @@ def test_t_end_validation():
                                           torch.zeros(2, 4).cuda(), (2, 1, 64, 64), t_end=1.5)
 
 
+@pytest.mark.parametrize("grad", [False, True], ids=["fused", "autograd"])
 @pytest.mark.parametrize("name,cond", [("condvae_b4", True), ("vae_b4", False)])
-def test_vae_vs_reference(golden, name, cond):
+def test_vae_vs_reference(golden, name, cond, grad):
+    """Both forward paths: the fused no-grad evaluator and the autograd training chain."""
     from toycrystals_amd.models.vae import CondVAE, VAE
     g = golden(name)
     torch.manual_seed(0)
     m = (CondVAE(z_dim=32, n_types=4, y_cont_dim=4, cond_drop=0.0) if cond else VAE(z_dim=32)).cuda().eval()
     x = cu(g["x"])
-    if cond:
-        mu, lv = m.encode(x, cu(g["y_cat"]), cu(g["y_cont"]))
-    else:
-        mu, lv = m.encode(x)
-    assert rel_err(mu.cpu().numpy(), g["mu"]) < 2e-5
-    assert rel_err(lv.cpu().numpy(), g["logvar"]) < 2e-5
-    z = mu + torch.exp(0.5 * lv) * cu(g["rep_eps"])
-    x_hat = m.decode(z, cu(g["y_cat"]), cu(g["y_cont"])) if cond else m.decode(z)
-    assert np.abs(x_hat.cpu().numpy() - g["x_hat"]).max() < 2e-5
-    recon = torch.mean((x_hat - x) ** 2).item()
+    with torch.set_grad_enabled(grad):
+        if cond:
+            mu, lv = m.encode(x, cu(g["y_cat"]), cu(g["y_cont"]))
+        else:
+            mu, lv = m.encode(x)
+        assert mu.requires_grad == grad
+        assert rel_err(mu.detach().cpu().numpy(), g["mu"]) < 2e-5
+        assert rel_err(lv.detach().cpu().numpy(), g["logvar"]) < 2e-5
+        z = m.reparameterise(mu, lv, cu(g["rep_eps"]))
+        x_hat = m.decode(z, cu(g["y_cat"]), cu(g["y_cont"])) if cond else m.decode(z)
+        assert np.abs(x_hat.detach().cpu().numpy() - g["x_hat"]).max() < 2e-5
+        recon = torch.mean((x_hat.detach() - x) ** 2).item()
     assert abs(recon - float(g["recon"])) < 1e-6
 
 
@@ -192,8 +200,12 @@ def test_prior_vs_reference(golden, name, width, stored):
     if stored:
         m.load_state_dict({k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w/")})
     m = m.cuda().eval()
-    eps = m(cu(g["z_t"]), cu(g["t"]), cu(g["y_cat"]), cu(g["y_cont"])).cpu().numpy()
-    assert rel_err(eps, g["eps"]) < 2e-4  # the t=999 sinusoid phase carries ~1e-4 (see oracle test)
+    eps = m(cu(g["z_t"]), cu(g["t"]), cu(g["y_cat"]), cu(g["y_cont"]))
+    assert eps.requires_grad  # autograd training chain
+    assert rel_err(eps.detach().cpu().numpy(), g["eps"]) < 2e-4  # t=999 sinusoid phase ~1e-4 (oracle test)
+    with torch.no_grad():  # fused evaluator
+        eps = m(cu(g["z_t"]), cu(g["t"]), cu(g["y_cat"]), cu(g["y_cont"])).cpu().numpy()
+    assert rel_err(eps, g["eps"]) < 2e-4
     sch = DiffusionSchedule.linear(1000, 1e-4, 0.05, torch.device("cuda"))
     z0 = sch.ddim_sample(m, cu(g["y_cat"]), cu(g["y_cont"]), n_steps=int(g["ddim_steps"]),
                          z_init=cu(g["ddim_z_init"])).cpu().numpy()

@@ -1,0 +1,422 @@
+"""GPU: the training path (libtcx autograd Functions) — every backward op against torch's CPU
+autograd in float64 on the same inputs, then whole training steps against the reference goldens
+(tests/golden/train*.npz, produced by importing the reference: make_goldens.py `train`).
+
+Tolerances (fp32 kernels vs float64 / the fp32 CPU reference):
+  * per-op outputs and gradients: 2e-5 x max(1, |ref|max) (reduction-order noise of fp32)
+  * score-model parameter gradients (base_ch 16, B 3): 1e-4 x max(|g|max over the tensor, 1e-3);
+    the loss 1e-5 relative; two Adam steps + EMA on the parameters: max 5e-5 and mean 1e-6
+    absolute.  Adam moves a weight by up to lr = 1e-3 per step and normalises by sqrt(v) + eps,
+    so where a gradient is ~eps (an embedding row touched by one sample of three) fp32
+    reduction-order noise in g is a visible fraction of the step (observed 1.2e-5 = 1.2 % of lr
+    on one element); the mean bound checks the update everywhere else.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def cu(a, dtype=torch.float32):
+    t = torch.from_numpy(np.ascontiguousarray(a)) if isinstance(a, np.ndarray) else a
+    return t.to(dtype).cuda() if dtype is not None else t.cuda()
+
+
+def err(a, ref):
+    a = a.detach().double().cpu() if torch.is_tensor(a) else torch.as_tensor(a).double()
+    ref = ref.detach().double().cpu() if torch.is_tensor(ref) else torch.as_tensor(ref).double()
+    return float((a - ref).abs().max()) / max(1.0, float(ref.abs().max()))
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+def _conv_case(C1, C2, Cout, ks, stride, pad, circular, H, B=2, resid=False, seed=0):
+    from toycrystals_amd import functional as TF
+    g = torch.Generator().manual_seed(seed)
+    x1 = torch.randn(B, C1, H, H, generator=g, dtype=torch.float64)
+    x2 = torch.randn(B, C2, H, H, generator=g, dtype=torch.float64) if C2 else None
+    w = torch.randn(Cout, C1 + C2, ks, ks, generator=g, dtype=torch.float64) / math.sqrt((C1 + C2) * ks * ks)
+    b = torch.randn(Cout, generator=g, dtype=torch.float64)
+    xin = torch.cat([x1, x2], 1) if C2 else x1
+    Ho = (H + 2 * pad - ks) // stride + 1
+    r = torch.randn(B, Cout, Ho, Ho, generator=g, dtype=torch.float64) if resid else None
+    gy = torch.randn(B, Cout, Ho, Ho, generator=g, dtype=torch.float64)
+    # reference: torch CPU float64 autograd
+    xr = [t.clone().requires_grad_() for t in ([x1] + ([x2] if C2 else []))]
+    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
+    xi = torch.cat(xr, 1) if C2 else xr[0]
+    if circular and pad:
+        y_ref = F.conv2d(F.pad(xi, (pad,) * 4, mode="circular"), wr, br, stride=stride)
+    else:
+        y_ref = F.conv2d(xi, wr, br, stride=stride, padding=pad)
+    if resid:
+        y_ref = y_ref + r
+    y_ref.backward(gy)
+    # device path
+    dx = [cu(nhwc(t)).requires_grad_() for t in ([x1] + ([x2] if C2 else []))]
+    dw, db = cu(w).requires_grad_(), cu(b).requires_grad_()
+    y = TF.Conv2dFn.apply(dx[0], dx[1] if C2 else None, dw, db, cu(nhwc(r)) if resid else None, stride, pad,
+                          1 if circular else 0)
+    y.backward(cu(nhwc(gy)))
+    assert err(nchw(y), y_ref) < 2e-5
+    assert err(nchw(dx[0].grad), xr[0].grad) < 2e-5
+    if C2:
+        assert err(nchw(dx[1].grad), xr[1].grad) < 2e-5
+    assert err(dw.grad, wr.grad) < 2e-5
+    assert err(db.grad, br.grad) < 2e-5
+
+
+@pytest.mark.parametrize("C1,C2,Cout,ks,stride,pad,circ,H", [
+    (32, 0, 32, 3, 1, 1, True, 16),     # _ConvBlock conv
+    (32, 32, 16, 3, 1, 1, True, 16),    # skip-concat conv (up2/up1 first conv)
+    (16, 0, 16, 4, 2, 1, True, 16),     # ds1/ds2
+    (32, 0, 96, 1, 1, 0, False, 8),     # attention qkv
+    (16, 0, 1, 3, 1, 1, True, 16),      # out conv (Cout = 1)
+    (1, 0, 32, 4, 2, 1, False, 16),     # VAE enc first conv (Cin = 1, zero pad)
+    (32, 0, 64, 4, 2, 1, False, 8),     # VAE enc conv
+    (12, 0, 20, 3, 1, 1, True, 12),     # odd channel counts (scalar / unaligned paths)
+])
+def test_conv2d_fn_vs_torch(C1, C2, Cout, ks, stride, pad, circ, H):
+    _conv_case(C1, C2, Cout, ks, stride, pad, circ, H)
+
+
+def test_conv2d_fn_resid():
+    _conv_case(32, 0, 32, 1, 1, 0, False, 8, resid=True)
+
+
+@pytest.mark.parametrize("Cin,Cout,H", [(64, 32, 8), (32, 1, 16), (256, 128, 4)])
+def test_conv_transpose_fn_vs_torch(Cin, Cout, H):
+    from toycrystals_amd import functional as TF
+    g = torch.Generator().manual_seed(3)
+    B = 2
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+    w = torch.randn(Cin, Cout, 4, 4, generator=g, dtype=torch.float64) / math.sqrt(Cin * 4)
+    b = torch.randn(Cout, generator=g, dtype=torch.float64)
+    gy = torch.randn(B, Cout, 2 * H, 2 * H, generator=g, dtype=torch.float64)
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    y_ref = F.conv_transpose2d(xr, wr, br, stride=2, padding=1)
+    y_ref.backward(gy)
+    xd, wd, bd = cu(nhwc(x)).requires_grad_(), cu(w).requires_grad_(), cu(b).requires_grad_()
+    y = TF.ConvTranspose2xFn.apply(xd, wd, bd)
+    y.backward(cu(nhwc(gy)))
+    assert err(nchw(y), y_ref) < 2e-5
+    assert err(nchw(xd.grad), xr.grad) < 2e-5
+    assert err(wd.grad, wr.grad) < 2e-5
+    assert err(bd.grad, br.grad) < 2e-5
+
+
+def test_first_conv_fn_vs_torch():
+    from toycrystals_amd import functional as TF
+    g = torch.Generator().manual_seed(5)
+    B, H, C0, nm = 3, 16, 32, 16
+    x = torch.randn(B, 1, H, H, generator=g, dtype=torch.float64)
+    maps = torch.randn(B, nm, generator=g, dtype=torch.float64)
+    w = torch.randn(C0, 1 + nm, 3, 3, generator=g, dtype=torch.float64) / 10
+    b = torch.randn(C0, generator=g, dtype=torch.float64)
+    gy = torch.randn(B, C0, H, H, generator=g, dtype=torch.float64)
+    mr, wr, br = maps.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    xin = torch.cat([x, mr[:, :, None, None].expand(B, nm, H, H)], 1)
+    y_ref = F.conv2d(F.pad(xin, (1, 1, 1, 1), mode="circular"), wr, br)
+    y_ref.backward(gy)
+    md, wd, bd = cu(maps).requires_grad_(), cu(w).requires_grad_(), cu(b).requires_grad_()
+    y = TF.FirstConvFn.apply(cu(nhwc(x)), md, wd, bd)
+    y.backward(cu(nhwc(gy)))
+    assert err(nchw(y), y_ref) < 2e-5
+    assert err(md.grad, mr.grad) < 2e-5
+    assert err(wd.grad, wr.grad) < 2e-5
+    assert err(bd.grad, br.grad) < 2e-5
+
+
+@pytest.mark.parametrize("C,groups,silu,H", [(32, 8, 1, 16), (64, 8, 0, 8), (96, 8, 1, 8), (16, 4, 1, 32)])
+def test_group_norm_act_fn_vs_torch(C, groups, silu, H):
+    from toycrystals_amd import functional as TF
+    g = torch.Generator().manual_seed(7)
+    B = 3
+    x = torch.randn(B, C, H, H, generator=g, dtype=torch.float64) * 2 + 0.5
+    gm = 1 + 0.2 * torch.randn(C, generator=g, dtype=torch.float64)
+    bt = 0.2 * torch.randn(C, generator=g, dtype=torch.float64)
+    gy = torch.randn(B, C, H, H, generator=g, dtype=torch.float64)
+    xr, gr, br = x.clone().requires_grad_(), gm.clone().requires_grad_(), bt.clone().requires_grad_()
+    y_ref = F.group_norm(xr, groups, gr, br, 1e-5)
+    if silu:
+        y_ref = F.silu(y_ref)
+    y_ref.backward(gy)
+    xd, gd, bd = cu(nhwc(x)).requires_grad_(), cu(gm).requires_grad_(), cu(bt).requires_grad_()
+    y = TF.GroupNormActFn.apply(xd, gd, bd, groups, 1e-5, silu)
+    y.backward(cu(nhwc(gy)))
+    assert err(nchw(y), y_ref) < 2e-5
+    assert err(nchw(xd.grad), xr.grad) < 2e-5
+    assert err(gd.grad, gr.grad) < 2e-5
+    assert err(bd.grad, br.grad) < 2e-5
+
+
+@pytest.mark.parametrize("H,C", [(8, 32), (16, 16), (4, 8)])
+def test_upsample_fn_vs_torch(H, C):
+    from toycrystals_amd import functional as TF
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, C, H, H, generator=g, dtype=torch.float64)
+    gy = torch.randn(2, C, 2 * H, 2 * H, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_()
+    y_ref = F.interpolate(xr, scale_factor=2, mode="bilinear", align_corners=False)
+    y_ref.backward(gy)
+    xd = cu(nhwc(x)).requires_grad_()
+    y = TF.Upsample2xFn.apply(xd)
+    y.backward(cu(nhwc(gy)))
+    assert err(nchw(y), y_ref) < 2e-5
+    assert err(nchw(xd.grad), xr.grad) < 2e-5
+
+
+@pytest.mark.parametrize("B,N,C,heads", [(2, 64, 32, 4), (3, 256, 192, 4)])
+def test_attention_fn_vs_torch(B, N, C, heads):
+    from toycrystals_amd import functional as TF
+    g = torch.Generator().manual_seed(11)
+    qkv = torch.randn(B, N, 3 * C, generator=g, dtype=torch.float64)
+    gy = torch.randn(B, N, C, generator=g, dtype=torch.float64)
+    qr = qkv.clone().requires_grad_()
+    d = C // heads
+    q, k, v = qr.split(C, dim=2)
+    sh = lambda t: t.view(B, N, heads, d).transpose(1, 2)  # noqa: E731  head h = channels h*d..
+    y_ref = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(B, N, C)
+    y_ref.backward(gy)
+    qd = cu(qkv).requires_grad_()
+    y = TF.AttentionFn.apply(qd, heads)
+    y.backward(cu(gy))
+    assert err(y, y_ref) < 2e-5
+    assert err(qd.grad, qr.grad) < 2e-5
+
+
+@pytest.mark.parametrize("M,K,N,act", [(5, 128, 128, 3), (256, 1024, 4096, 0), (7, 13, 6, 1), (4, 40, 32, 2)])
+def test_linear_act_fn_vs_torch(M, K, N, act):
+    from toycrystals_amd import functional as TF
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(M, K, generator=g, dtype=torch.float64)
+    w = torch.randn(N, K, generator=g, dtype=torch.float64) / math.sqrt(K)
+    b = torch.randn(N, generator=g, dtype=torch.float64)
+    gy = torch.randn(M, N, generator=g, dtype=torch.float64)
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    y_ref = F.linear(xr, wr, br)
+    y_ref = [y_ref, F.relu(y_ref), torch.sigmoid(y_ref), F.silu(y_ref)][act]
+    y_ref.backward(gy)
+    xd, wd, bd = cu(x).requires_grad_(), cu(w).requires_grad_(), cu(b).requires_grad_()
+    y = TF.LinearFn.apply(xd, wd, bd)
+    if act:
+        y = TF.ActFn.apply(y, act)
+    y.backward(cu(gy))
+    assert err(y, y_ref) < 2e-5
+    assert err(xd.grad, xr.grad) < 2e-5
+    assert err(wd.grad, wr.grad) < 2e-5
+    assert err(bd.grad, br.grad) < 2e-5
+
+
+def test_gemm_strided_batched_vs_torch():
+    from toycrystals_amd.functional import gemm
+    g = torch.Generator().manual_seed(15)
+    A = torch.randn(6, 37, 29, generator=g)
+    Bm = torch.randn(6, 29, 45, generator=g)
+    C = torch.randn(6, 37, 45, generator=g)
+    bias = torch.randn(45, generator=g)
+    ref = 0.5 * A.double() @ Bm.double() + 2.0 * C.double() + bias.double()
+    Ad, Bd, Cd, bd = cu(A), cu(Bm), cu(C), cu(bias)
+    # A^T-strided view of the same data: pass A as (m, k) with strides (29, 1); B as (k, n) = (45, 1)
+    gemm(37, 45, 29, Ad, 29, 1, Bd, 45, 1, Cd, 45, 1, alpha=0.5, beta=2.0, bias=bd, batch=6, bdiv=3,
+         a_hl=(3 * 37 * 29, 37 * 29), b_hl=(3 * 29 * 45, 29 * 45), c_hl=(3 * 37 * 45, 37 * 45))
+    assert err(Cd, ref) < 2e-5
+
+
+def test_embedding_cat_layernorm_film_vs_torch():
+    from toycrystals_amd import functional as TF
+    g = torch.Generator().manual_seed(17)
+    W = torch.randn(5, 24, generator=g, dtype=torch.float64)
+    idx = torch.tensor([0, 3, 3, 4, 1, 0])
+    other = torch.randn(6, 40, generator=g, dtype=torch.float64)
+    lnw = 1 + 0.2 * torch.randn(64, generator=g, dtype=torch.float64)
+    lnb = 0.2 * torch.randn(64, generator=g, dtype=torch.float64)
+    gb = torch.randn(6, 128, generator=g, dtype=torch.float64) * 0.3
+    gy = torch.randn(6, 64, generator=g, dtype=torch.float64)
+    Wr, orr, lwr, lbr, gbr = [t.clone().requires_grad_() for t in (W, other, lnw, lnb, gb)]
+    h = torch.cat([F.embedding(idx, Wr), orr], 1)
+    gm, bt = gbr.chunk(2, dim=-1)
+    y_ref = F.layer_norm(h, (64,), lwr, lbr, 1e-5) * (1.0 + gm) + bt
+    y_ref.backward(gy)
+    Wd, od, lwd, lbd, gbd = [cu(t).requires_grad_() for t in (W, other, lnw, lnb, gb)]
+    hd = TF.cat_cols(TF.EmbeddingFn.apply(idx.cuda(), Wd), od)
+    y = TF.LayerNormFiLMFn.apply(hd, lwd, lbd, gbd, 1e-5)
+    y.backward(cu(gy))
+    assert err(y, y_ref) < 2e-5
+    for a, r in ((Wd, Wr), (od, orr), (lwd, lwr), (lbd, lbr), (gbd, gbr)):
+        assert err(a.grad, r.grad) < 2e-5
+
+
+def test_mse_loss_fn_vs_torch():
+    from toycrystals_amd import functional as TF
+    g = torch.Generator().manual_seed(19)
+    a = torch.randn(3, 1, 64, 64, generator=g, dtype=torch.float64)
+    b = torch.randn(3, 1, 64, 64, generator=g, dtype=torch.float64)
+    ar = a.clone().requires_grad_()
+    l_ref = F.mse_loss(ar, b)
+    (l_ref * 3.0).backward()
+    ad = cu(a).requires_grad_()
+    l = TF.mse_loss(ad, cu(b))
+    (l * 3.0).backward()
+    assert abs(float(l.detach()) - float(l_ref)) < 1e-6 * max(1.0, float(l_ref))
+    assert err(ad.grad, ar.grad) < 2e-5
+
+
+# ---------------------------------------------------------------- whole training steps vs goldens
+def _perturb_norms(model, seed):
+    """tests/golden/make_goldens.py:perturb_norms (same module order as the reference)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, (torch.nn.GroupNorm, torch.nn.LayerNorm)):
+                m.weight.copy_(1.0 + 0.2 * torch.randn(m.weight.shape, generator=g))
+                m.bias.copy_(0.2 * torch.randn(m.bias.shape, generator=g))
+
+
+def _check_checksums(model, gd):
+    for k, v in model.state_dict().items():
+        ck = gd["ck/" + k]
+        vv = v.detach().double().cpu()
+        assert abs(vv.sum().item() - ck[0]) <= 1e-9 * max(1.0, ck[1]), k
+
+
+def test_score_training_step_vs_reference(golden):
+    from toycrystals_amd.models.sde_score_model import CondUNetTiny, VPSDE, diffusion_loss_eps
+    from toycrystals_amd.optim import Adam, ema_update
+    gd = golden("train16_b3")
+    torch.manual_seed(0)
+    model = CondUNetTiny(4, 4, 16)
+    _perturb_norms(model, 5)
+    _check_checksums(model, gd)
+    model = model.cuda()
+    torch.manual_seed(0)
+    ema = CondUNetTiny(4, 4, 16).cuda()
+    ema.load_state_dict(model.state_dict())
+    sde = VPSDE(0.1, 30.0)
+    opt = Adam(model.parameters(), lr=float(gd["lr"]))
+    x0, y_cat, y_cont = cu(gd["x0"]), cu(gd["y_cat"], torch.int64), cu(gd["y_cont"])
+    for step in range(2):
+        draws = (cu(gd[f"u{step}"]), cu(gd[f"eps{step}"]), cu(gd[f"drop{step}"]))
+        loss = diffusion_loss_eps(model, sde, x0, y_cat, y_cont, p_uncond=float(gd["p_uncond"]), draws=draws)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        assert abs(float(loss) - float(gd[f"loss{step}"])) <= 1e-5 * float(gd[f"loss{step}"])
+        if step == 0:
+            for k, p in model.named_parameters():
+                ref = gd["g/" + k]
+                tol = 1e-4 * max(float(np.abs(ref).max()), 1e-3)
+                got = p.grad.detach().cpu().numpy()
+                assert float(np.abs(got - ref).max()) <= tol, (k, float(np.abs(got - ref).max()), tol)
+        opt.step()
+        ema_update(ema, model, float(gd["ema_decay"]))
+    names = dict(model.named_parameters())
+    enames = dict(ema.named_parameters())
+    for key in gd:
+        if key.startswith("p2/") or key.startswith("ema2/"):
+            k = key.split("/", 1)[1]
+            got = (names if key.startswith("p2/") else enames)[k].detach().cpu().numpy()
+            d = np.abs(got - gd[key])
+            assert float(d.max()) < 5e-5 and float(d.mean()) < 1e-6, (key, float(d.max()), float(d.mean()))
+
+
+def test_adam_matches_torch_adam():
+    """Fused Adam vs torch.optim.Adam (CPU, fp32) over 5 steps with weight decay."""
+    from toycrystals_amd.optim import Adam
+    g = torch.Generator().manual_seed(21)
+    ps = [torch.randn(n, generator=g) for n in (1, 33, 4096, 70000)]
+    grads = [[torch.randn(p.shape, generator=g) for p in ps] for _ in range(5)]
+    ref = [torch.nn.Parameter(p.clone()) for p in ps]
+    dev = [torch.nn.Parameter(p.clone().cuda()) for p in ps]
+    o_ref = torch.optim.Adam(ref, lr=3e-3, betas=(0.8, 0.99), eps=1e-6, weight_decay=0.01)
+    o_dev = Adam(dev, lr=3e-3, betas=(0.8, 0.99), eps=1e-6, weight_decay=0.01)
+    for s in range(5):
+        for p, q, gg in zip(ref, dev, grads[s]):
+            p.grad = gg.clone()
+            q.grad = gg.clone().cuda()
+        o_ref.step()
+        o_dev.step()
+    for p, q in zip(ref, dev):
+        assert float((p.detach() - q.detach().cpu()).abs().max()) < 1e-6
+    sd = o_dev.state_dict()
+    assert set(sd["state"][0].keys()) == {"step", "exp_avg", "exp_avg_sq"}
+    assert float(sd["state"][0]["step"]) == 5.0
+
+
+def _cmp_grad_samples(name, grad, gd, rel=1e-4):
+    g = grad.detach().double().cpu().reshape(-1).numpy()
+    ck = gd["gck/" + name]
+    assert abs(np.abs(g).sum() - ck[1]) <= rel * max(ck[1], 1e-12) + 1e-9, (name, np.abs(g).sum(), ck[1])
+    if "g/" + name in gd:
+        ref = gd["g/" + name].reshape(-1)
+        assert float(np.abs(g - ref).max()) <= rel * max(float(np.abs(ref).max()), 1e-8), name
+    else:
+        ref = gd["gs/" + name].astype(np.float64)
+        got = g[gd["gi/" + name]]
+        assert float(np.abs(got - ref).max()) <= rel * max(float(np.abs(ref).max()), 1e-8) + 1e-12, name
+
+
+def test_condvae_training_step_vs_reference(golden):
+    """CondVAE train-mode forward (cond_drop 0.1, injected draws) + recon + beta*kl_used(free bits)
+    backward vs the reference (train_vae.py:299-312)."""
+    from toycrystals_amd import functional as TF
+    from toycrystals_amd.models.vae import CondVAE
+    gd = golden("train_condvae_b4")
+    torch.manual_seed(0)
+    m = CondVAE(z_dim=32, n_types=4, y_cont_dim=4, cond_drop=0.1)
+    _check_checksums(m, gd)
+    m = m.cuda().train()
+    x, y_cat, y_cont = cu(gd["x"]), cu(gd["y_cat"], torch.int64), cu(gd["y_cont"])
+    x_hat, mu, logvar = m(x, y_cat, y_cont, draws=(cu(gd["rep_eps"]), cu(gd["keep_u"])))
+    recon = TF.mse_loss(x_hat, x)
+    kl_used, kl_raw = TF.kl_stats(mu, logvar, free_bits=float(gd["free_bits"]))
+    loss = recon + float(gd["beta"]) * kl_used
+    loss.backward()
+    assert err(x_hat, torch.from_numpy(gd["x_hat"])) < 2e-5
+    assert err(mu, torch.from_numpy(gd["mu"])) < 2e-5
+    assert err(logvar, torch.from_numpy(gd["logvar"])) < 2e-5
+    assert abs(float(loss.detach()) - float(gd["loss"])) <= 1e-5 * float(gd["loss"])
+    assert abs(float(kl_used.detach()) - float(gd["kl_used"])) <= 1e-5 * float(gd["kl_used"])
+    for k, p in m.named_parameters():
+        _cmp_grad_samples(k, p.grad, gd)
+
+
+def test_prior_training_step_vs_reference(golden):
+    """FiLM prior training step (train_diffusion_prior.py:251-277): t from u, q_sample, MSE, backward."""
+    from toycrystals_amd import functional as TF
+    from toycrystals_amd.models.diffusion_prior import DiffusionPriorFiLM, DiffusionSchedule
+    gd = golden("train_prior_w64")
+    torch.manual_seed(0)
+    m = DiffusionPriorFiLM(z_dim=32, n_types=4, y_cont_dim=4, t_emb_dim=64, width=64, n_blocks=2, y_cat_emb_dim=64)
+    _perturb_norms(m, 13)
+    _check_checksums(m, gd)
+    m = m.cuda().train()
+    T = int(gd["T"])
+    sched = DiffusionSchedule.linear(T=T, beta_start=1e-4, beta_end=float(gd["beta_end"]), device=torch.device("cuda"))
+    from toycrystals_amd._lib import check, lib, ptr, stream_ptr
+    z0, eps, u = cu(gd["z0"]), cu(gd["eps"]), cu(gd["u"])
+    B, Z = z0.shape
+    t = torch.empty((B,), device="cuda", dtype=torch.int64)
+    z_t = torch.empty_like(z0)
+    check(lib().tcx_prior_qsample(ptr(z0), ptr(eps), ptr(u), ptr(sched.sqrt_alpha_bars),
+                                  ptr(sched.sqrt_one_minus_alpha_bars), T, B, Z, ptr(t), ptr(z_t), stream_ptr()), "qs")
+    assert torch.equal(t.cpu(), torch.from_numpy(gd["t"]))
+    assert err(z_t, torch.from_numpy(gd["z_t"])) < 2e-6
+    eps_pred = m(z_t, t, cu(gd["y_cat"], torch.int64), cu(gd["y_cont"]))
+    loss = TF.mse_loss(eps_pred, eps)
+    loss.backward()
+    assert err(eps_pred, torch.from_numpy(gd["eps_pred"])) < 2e-5
+    assert abs(float(loss.detach()) - float(gd["loss"])) <= 1e-5 * float(gd["loss"])
+    for k, p in m.named_parameters():
+        ref = gd["g/" + k]
+        got = p.grad.detach().cpu().numpy()
+        assert float(np.abs(got - ref).max()) <= 1e-4 * max(float(np.abs(ref).max()), 1e-6), k

@@ -566,6 +566,24 @@ __global__ void k_pack_convT(const float* __restrict__ w, float* __restrict__ wp
     }
 }
 
+// Data gradient of a stride-1 conv as a forward conv over dY: output channel ci' (= ci_lo + ci'),
+// k = (dy*ks + dx)*Cout + co, value w[co][ci][ks-1-dy][ks-1-dx] (flipped taps, swapped channels).
+__global__ void k_pack_conv_dgrad(const float* __restrict__ w, float* __restrict__ wpk, int Cout, int Cin, int ks,
+                                  int ci_lo, int n_ci, int cout_pad, int kpad) {
+    const size_t n = (size_t)cout_pad * kpad;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(i / kpad);
+        const int k = (int)(i - (size_t)r * kpad);
+        const int tap = k / Cout, co = k - (k / Cout) * Cout;
+        float v = 0.f;
+        if (r < n_ci && tap < ks * ks) {
+            const int dy = tap / ks, dx = tap - (tap / ks) * ks;
+            v = w[(((size_t)co * Cin + ci_lo + r) * ks + (ks - 1 - dy)) * ks + (ks - 1 - dx)];
+        }
+        wpk[i] = v;
+    }
+}
+
 }  // namespace
 }  // namespace tcx
 
@@ -637,6 +655,12 @@ extern "C" int tcx_conv2d(const float* x1, const float* x2, int Bt, int bmod, in
 
 extern "C" int tcx_convT2x(const float* x, int Bt, int H, int W, int Cin, const float* wpk4, const float* bias,
                            float* y, int Cout, int cout_pad, int kpad, int act, void* stream) {
+    return tcx_conv_transpose2x(x, Bt, H, W, Cin, wpk4, bias, y, Cout, cout_pad, kpad, act, 0, stream);
+}
+
+extern "C" int tcx_conv_transpose2x(const float* x, int Bt, int H, int W, int Cin, const float* wpk4,
+                                    const float* bias, float* y, int Cout, int cout_pad, int kpad, int act,
+                                    int circular, void* stream) {
     TCX_REQUIRE(x && wpk4 && y, "tcx_convT2x: null pointer");
     TCX_REQUIRE(cout_pad >= Cout && cout_pad % 32 == 0 && kpad % BK == 0 && kpad >= 4 * Cin, "tcx_convT2x: bad padding");
     for (int ph = 0; ph < 4; ++ph) {
@@ -648,10 +672,16 @@ extern "C" int tcx_convT2x(const float* x, int Bt, int H, int W, int Cin, const 
         p.w = wpk4 + (size_t)ph * cout_pad * kpad;
         p.bias = bias; p.bias_b = nullptr; p.resid = nullptr; p.y = y;
         p.Cout = Cout; p.kpad = kpad; p.nchunks = kpad / BK;
-        p.ks = 2; p.stride = 1; p.pad_y = 1 - ry; p.pad_x = 1 - rx; p.circular = 0;
+        p.ks = 2; p.stride = 1; p.pad_y = 1 - ry; p.pad_x = 1 - rx; p.circular = circular;
         p.Hy = 2 * H; p.Wy = 2 * W; p.osy = 2; p.ooy = ry; p.osx = 2; p.oox = rx;
         p.act = act; p.gn = nullptr; p.nsplit = 1;
         const bool vec_ok = (Cin % 4 == 0) && aligned16(x);
+        {
+            const size_t lim = (size_t)1 << 31;
+            const size_t b1 = (size_t)Bt * H * W * Cin * sizeof(float), bw = (size_t)cout_pad * kpad * sizeof(float);
+            p.bytes1 = b1 < lim ? (unsigned)b1 : 0u;
+            p.bytesw = bw < lim && aligned16(p.w) ? (unsigned)bw : 0u;
+        }
         TCX_TRY(launch_conv(p, cout_pad, vec_ok ? 0 : 1, (hipStream_t)stream));
     }
     return TCX_OK;
@@ -692,4 +722,15 @@ extern "C" int tcx_linear(const float* x1, int K1, const float* x2, int K2, cons
     const bool vec_ok = (K1 % 4 == 0) && (K2 % 4 == 0) && aligned16(x1) && (!x2 || aligned16(x2));
     TCX_REQUIRE(vec_ok || x2 == nullptr, "tcx_linear: two-source form needs K1,K2 %% 4 == 0 and aligned rows");
     return launch_conv(p, npad, vec_ok ? 0 : 1, (hipStream_t)stream);
+}
+
+extern "C" int tcx_pack_conv_dgrad_weight(const float* w, float* wpk, int Cout, int Cin, int ks, int ci_lo, int n_ci,
+                                          int cout_pad, int kpad, void* stream) {
+    TCX_REQUIRE(w && wpk && ci_lo >= 0 && n_ci > 0 && ci_lo + n_ci <= Cin && cout_pad >= n_ci &&
+                kpad >= ks * ks * Cout, "tcx_pack_conv_dgrad_weight: bad args");
+    const size_t n = (size_t)cout_pad * kpad;
+    const int blocks = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_pack_conv_dgrad, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, wpk, Cout, Cin, ks, ci_lo,
+                       n_ci, cout_pad, kpad);
+    return check_launch("tcx_pack_conv_dgrad_weight");
 }

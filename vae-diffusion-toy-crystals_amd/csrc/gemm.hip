@@ -1,0 +1,486 @@
+// fp32-MFMA GEMMs for the training path (gfx950, v_mfma_f32_32x32x2_f32).
+//
+// k_gemm   — batched, arbitrarily strided C = alpha * op(A) op(B) + beta * C (+ bias[n]).  Serves
+//            the Linear layers forward and backward of every model (dX = dY W, dW = dY^T X) and the
+//            attention products (S = Q K^T, O = P V and their backward) of SelfAttention2d
+//            (/root/reference/src/toycrystals/models/sde_score_model.py:150-157).
+// k_wgrad  — convolution weight gradient dW[co][ci][ky][kx] = sum_m dY[m][co] * im2col(X)[m][k]
+//            (the backward of every nn.Conv2d / nn.ConvTranspose2d of sde_score_model.py and
+//            models/vae.py), an implicit GEMM whose reduction runs over output pixels: split over
+//            pixel ranges into [split][K][Cout] partials, then a fixed-order reduction (deterministic).
+//
+// Both use the conv kernel's tile scheme: 128 x 32*NT output tile, 4 waves x (32 rows x 32*NT),
+// 32-deep reduction chunks staged through LDS rows padded to 36 floats, register-staged double
+// buffering.  Operands whose reduction dimension is not the contiguous one are loaded as float4
+// along the contiguous dimension and transposed on the LDS store.
+#include "common.hpp"
+
+namespace tcx {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int GBM = 128;
+constexpr int GBK = 32;
+constexpr int GLD = 36;
+
+struct GemmParams {
+    int M, N, K;
+    float alpha, beta;
+    const float* A;
+    long long sam, sak;
+    const float* B;
+    long long sbk, sbn;
+    float* C;
+    long long scm, scn;
+    const float* bias;
+    int bdiv;  // batch z -> (z / bdiv, z % bdiv) offsets
+    long long sah, sal, sbh, sbl, sch, scl;
+    int nmblk, nnblk;
+};
+
+__device__ __forceinline__ float4 ld4g(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// LA / LB: 0 = float4 along the reduction dim, 1 = float4 along the row (M or N) dim, 2 = scalar
+template <int NT, int LA, int LB>
+__global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
+    constexpr int BN = 32 * NT;
+    __shared__ __attribute__((aligned(16))) float As[2][GBM * GLD];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN * GLD];
+    const int z = blockIdx.y;
+    const int zh = z / p.bdiv, zl = z - zh * p.bdiv;
+    const float* A = p.A + zh * p.sah + zl * p.sal;
+    const float* B = p.B + zh * p.sbh + zl * p.sbl;
+    float* C = p.C + zh * p.sch + zl * p.scl;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mblk = tile / p.nnblk, nblk = tile - (tile / p.nnblk) * p.nnblk;
+    const int m0 = mblk * GBM, n0 = nblk * BN;
+    const int tid = threadIdx.x;
+
+    float ra[16];
+    float rb[4 * NT];
+    auto load = [&](int k0) {
+        // A tile: 128 rows x 32 k
+        if constexpr (LA == 0) {
+            const int k4 = tid & 7, pr = tid >> 3;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = m0 + pr + 32 * i, k = k0 + 4 * k4;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (m < p.M && k < p.K) v = ld4g(A + m * p.sam + k);
+                ra[4 * i] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
+            }
+        } else if constexpr (LA == 1) {
+            const int kk = tid & 31, q = tid >> 5;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = m0 + 4 * (q + 8 * i), k = k0 + kk;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (m < p.M && k < p.K) v = ld4g(A + m + k * p.sak);
+                ra[4 * i] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int e = tid + 256 * i, m = m0 + (e >> 5), k = k0 + (e & 31);
+                ra[i] = (m < p.M && k < p.K) ? A[m * p.sam + k * p.sak] : 0.f;
+            }
+        }
+        // B tile: BN rows (n) x 32 k
+        if constexpr (LB == 0) {
+            const int k4 = tid & 7, pr = tid >> 3;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int n = n0 + pr + 32 * j, k = k0 + 4 * k4;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (n < p.N && k < p.K) v = ld4g(B + n * p.sbn + k);
+                rb[4 * j] = v.x; rb[4 * j + 1] = v.y; rb[4 * j + 2] = v.z; rb[4 * j + 3] = v.w;
+            }
+        } else if constexpr (LB == 1) {
+            const int kk = tid & 31, q = tid >> 5;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int n = n0 + 4 * (q + 8 * j), k = k0 + kk;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (n < p.N && k < p.K) v = ld4g(B + n + k * p.sbk);
+                rb[4 * j] = v.x; rb[4 * j + 1] = v.y; rb[4 * j + 2] = v.z; rb[4 * j + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4 * NT; ++j) {
+                const int e = tid + 256 * j, n = n0 + (e >> 5), k = k0 + (e & 31);
+                rb[j] = (n < p.N && k < p.K) ? B[n * p.sbn + k * p.sbk] : 0.f;
+            }
+        }
+    };
+    auto store = [&](int buf) {
+        if constexpr (LA == 0) {
+            const int k4 = tid & 7, pr = tid >> 3;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<float4*>(&As[buf][(pr + 32 * i) * GLD + 4 * k4]) =
+                    make_float4(ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]);
+        } else if constexpr (LA == 1) {
+            const int kk = tid & 31, q = tid >> 5;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) As[buf][(4 * (q + 8 * i) + e) * GLD + kk] = ra[4 * i + e];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int e = tid + 256 * i;
+                As[buf][(e >> 5) * GLD + (e & 31)] = ra[i];
+            }
+        }
+        if constexpr (LB == 0) {
+            const int k4 = tid & 7, pr = tid >> 3;
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                *reinterpret_cast<float4*>(&Bs[buf][(pr + 32 * j) * GLD + 4 * k4]) =
+                    make_float4(rb[4 * j], rb[4 * j + 1], rb[4 * j + 2], rb[4 * j + 3]);
+        } else if constexpr (LB == 1) {
+            const int kk = tid & 31, q = tid >> 5;
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Bs[buf][(4 * (q + 8 * j) + e) * GLD + kk] = rb[4 * j + e];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4 * NT; ++j) {
+                const int e = tid + 256 * j;
+                Bs[buf][(e >> 5) * GLD + (e & 31)] = rb[j];
+            }
+        }
+    };
+
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
+    const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
+    const int nch = (p.K + GBK - 1) / GBK;
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        const int cur = c & 1;
+        if (c + 1 < nch) load((c + 1) * GBK);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 fa = *reinterpret_cast<const float4*>(&As[cur][(wv * 32 + li) * GLD + lh * 16 + g * 4]);
+            float4 fb[NT];
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                fb[n] = *reinterpret_cast<const float4*>(&Bs[cur][(n * 32 + li) * GLD + lh * 16 + g * 4]);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.x, fb[n].x, acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.y, fb[n].y, acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.z, fb[n].z, acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.w, fb[n].w, acc[n], 0, 0, 0);
+        }
+        if (c + 1 < nch) store(cur ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int col = n0 + n * 32 + li;
+        if (col >= p.N) continue;
+        const float bv = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row < p.M) {
+                float* cp = C + row * p.scm + col * p.scn;
+                float v = p.alpha * acc[n][r];
+                if (p.beta != 0.f) v += p.beta * *cp;
+                *cp = v + bv;
+            }
+        }
+    }
+}
+
+template <int NT>
+int launch_gemm_nt(const GemmParams& p, int la, int lb, int batch, hipStream_t st) {
+    const dim3 grid(p.nmblk * p.nnblk, batch);
+#define TCX_G(A_, B_) hipLaunchKernelGGL((k_gemm<NT, A_, B_>), grid, dim3(256), 0, st, p)
+    if (la == 0 && lb == 0) TCX_G(0, 0);
+    else if (la == 0 && lb == 1) TCX_G(0, 1);
+    else if (la == 0) TCX_G(0, 2);
+    else if (la == 1 && lb == 0) TCX_G(1, 0);
+    else if (la == 1 && lb == 1) TCX_G(1, 1);
+    else if (la == 1) TCX_G(1, 2);
+    else if (lb == 0) TCX_G(2, 0);
+    else if (lb == 1) TCX_G(2, 1);
+    else TCX_G(2, 2);
+#undef TCX_G
+    return check_launch("tcx_gemm");
+}
+
+// ---------------------------------------------------------------- conv weight gradient
+struct WgParams {
+    const float *x1, *x2;
+    int C1, C2, Cin, H, W, Ho, Wo, HoWo, M;
+    int ks, stride, pad, circular;
+    const float* dy;
+    int Cout, K;
+    float* part;  // [nsplit][K][Cout]
+    int nsplit, cps;  // splits, 32-pixel chunks per split
+    int nkblk, ncblk;
+};
+
+// ASC: scalar im2col gather (Cin % 4 != 0); BSC: scalar dY loads (Cout % 4 != 0)
+template <int NT, bool ASC, bool BSC>
+__global__ __launch_bounds__(256, 2) void k_wgrad(WgParams p) {
+    constexpr int BN = 32 * NT;
+    __shared__ __attribute__((aligned(16))) float As[2][GBM * GLD];  // [k row][pixel]
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN * GLD];   // [co row][pixel]
+    const int split = blockIdx.y;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kblk = tile / p.ncblk, cblk = tile - (tile / p.ncblk) * p.ncblk;
+    const int k0 = kblk * GBM, c0 = cblk * BN;
+    const int tid = threadIdx.x;
+    const int px = tid & 31, q = tid >> 5;  // pixel column, quad row group
+    const int chunk0 = split * p.cps;
+    const int nch_all = (p.M + 31) / 32;
+    const int chunk1 = min(chunk0 + p.cps, nch_all);
+
+    // per-thread im2col rows: 4 quads of 4 k each (k = k0 + 4 (q + 8 i) + e)
+    int tdy[16], tdx[16], tci[16];
+    bool tsrc1[16], tkv[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int k = k0 + 4 * (q + 8 * i) + e;
+            const int kk = k < p.K ? k : 0;
+            const int tap = kk / p.Cin, ci = kk - (kk / p.Cin) * p.Cin;
+            tdy[4 * i + e] = tap / p.ks;
+            tdx[4 * i + e] = tap - (tap / p.ks) * p.ks;
+            tsrc1[4 * i + e] = ci < p.C1;
+            tci[4 * i + e] = ci < p.C1 ? ci : ci - p.C1;
+            tkv[4 * i + e] = k < p.K;
+        }
+    float ra[16];
+    float rb[4 * NT];
+    auto load = [&](int c) {
+        const int m = c * 32 + px;
+        const bool mv = m < p.M;
+        const int mm = mv ? m : 0;
+        const int b = mm / p.HoWo, r = mm - (mm / p.HoWo) * p.HoWo;
+        const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+        const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
+        auto addr = [&](int j, bool& ok) -> const float* {
+            int yy = iy0 + tdy[j], xx = ix0 + tdx[j];
+            ok = mv && tkv[j];
+            if (p.circular) {
+                yy = wrap_idx(yy, p.H);
+                xx = wrap_idx(xx, p.W);
+            } else {
+                ok = ok && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
+            }
+            const size_t pix = ((size_t)b * p.H + (ok ? yy : 0)) * p.W + (ok ? xx : 0);
+            return tsrc1[j] ? p.x1 + pix * p.C1 + tci[j] : p.x2 + pix * p.C2 + tci[j];
+        };
+        if constexpr (!ASC) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                bool ok;
+                const float* a = addr(4 * i, ok);
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (ok) v = ld4g(a);
+                ra[4 * i] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                bool ok;
+                const float* a = addr(j, ok);
+                ra[j] = ok ? *a : 0.f;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int co = c0 + 4 * (q + 8 * j);
+            if constexpr (!BSC) {
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (mv && co < p.Cout) v = ld4g(p.dy + (size_t)m * p.Cout + co);
+                rb[4 * j] = v.x; rb[4 * j + 1] = v.y; rb[4 * j + 2] = v.z; rb[4 * j + 3] = v.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    rb[4 * j + e] = (mv && co + e < p.Cout) ? p.dy[(size_t)m * p.Cout + co + e] : 0.f;
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) As[buf][(4 * (q + 8 * i) + e) * GLD + px] = ra[4 * i + e];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Bs[buf][(4 * (q + 8 * j) + e) * GLD + px] = rb[4 * j + e];
+    };
+
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
+    const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
+    if (chunk0 < chunk1) {
+        load(chunk0);
+        store(0);
+    }
+    __syncthreads();
+    for (int c = chunk0; c < chunk1; ++c) {
+        const int cur = (c - chunk0) & 1;
+        if (c + 1 < chunk1) load(c + 1);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 fa = *reinterpret_cast<const float4*>(&As[cur][(wv * 32 + li) * GLD + lh * 16 + g * 4]);
+            float4 fb[NT];
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                fb[n] = *reinterpret_cast<const float4*>(&Bs[cur][(n * 32 + li) * GLD + lh * 16 + g * 4]);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.x, fb[n].x, acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.y, fb[n].y, acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.z, fb[n].z, acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.w, fb[n].w, acc[n], 0, 0, 0);
+        }
+        if (c + 1 < chunk1) store(cur ^ 1);
+        __syncthreads();
+    }
+    float* dst = p.part + (size_t)split * p.K * p.Cout;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int co = c0 + n * 32 + li;
+        if (co >= p.Cout) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = k0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (k < p.K) dst[(size_t)k * p.Cout + co] = acc[n][r];
+        }
+    }
+}
+
+// dw[co][ci][ky][kx] = beta * dw + sum_s part[s][k][co], k = (ky*ks + kx)*Cin + ci (fixed order)
+__global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int K, int Cout, int Cin, int ks,
+                               float beta, float* __restrict__ dw) {
+    const size_t n = (size_t)K * Cout;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int k = (int)(i / Cout), co = (int)(i - (size_t)k * Cout);
+        float s = 0.f;
+        for (int sp = 0; sp < nsplit; ++sp) s += part[(size_t)sp * n + i];
+        const int tap = k / Cin, ci = k - tap * Cin;
+        const size_t o = ((size_t)co * Cin + ci) * ks * ks + tap;
+        dw[o] = beta != 0.f ? beta * dw[o] + s : s;
+    }
+}
+
+void wgrad_plan(int M, int K, int Cout, int* nt, int* nsplit, int* cps, int* nkblk, int* ncblk) {
+    *nt = Cout <= 32 ? 1 : (Cout <= 64 ? 2 : 3);
+    *nkblk = cdiv(K, GBM);
+    *ncblk = cdiv(Cout, 32 * *nt);
+    const int tiles = *nkblk * *ncblk;
+    const int nch = cdiv(std::max(M, 1), 32);
+    int ns = std::max(1, cdiv(2048, tiles));
+    ns = std::min(ns, std::max(1, nch / 8));  // >= 8 chunks per split
+    *cps = cdiv(nch, ns);
+    *nsplit = cdiv(nch, *cps);
+}
+
+}  // namespace
+}  // namespace tcx
+
+using namespace tcx;
+
+extern "C" int tcx_gemm(int M, int N, int K, float alpha, const float* A, long long sa_m, long long sa_k,
+                        const float* B, long long sb_k, long long sb_n, float beta, float* C, long long sc_m,
+                        long long sc_n, const float* bias, int batch, int bdiv, long long sa_hi, long long sa_lo,
+                        long long sb_hi, long long sb_lo, long long sc_hi, long long sc_lo, void* stream) {
+    TCX_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 0 && bdiv >= 1, "tcx_gemm: bad sizes");
+    TCX_REQUIRE(C && (K == 0 || (A && B)), "tcx_gemm: null pointer");
+    if (M == 0 || N == 0 || batch == 0) return TCX_OK;
+    GemmParams p{};
+    p.M = M; p.N = N; p.K = K; p.alpha = alpha; p.beta = beta;
+    p.A = A; p.sam = sa_m; p.sak = sa_k; p.B = B; p.sbk = sb_k; p.sbn = sb_n;
+    p.C = C; p.scm = sc_m; p.scn = sc_n; p.bias = bias;
+    p.bdiv = bdiv; p.sah = sa_hi; p.sal = sa_lo; p.sbh = sb_hi; p.sbl = sb_lo; p.sch = sc_hi; p.scl = sc_lo;
+    auto mul4 = [](long long v) { return v % 4 == 0; };
+    const bool zA = mul4(sa_hi) && mul4(sa_lo) && aligned16(A);
+    const bool zB = mul4(sb_hi) && mul4(sb_lo) && aligned16(B);
+    int la = 2, lb = 2;
+    if (K > 0) {
+        if (sa_k == 1 && K % 4 == 0 && mul4(sa_m) && zA) la = 0;
+        else if (sa_m == 1 && M % 4 == 0 && mul4(sa_k) && zA) la = 1;
+        if (sb_k == 1 && K % 4 == 0 && mul4(sb_n) && zB) lb = 0;
+        else if (sb_n == 1 && N % 4 == 0 && mul4(sb_k) && zB) lb = 1;
+    }
+    const int nt = N <= 32 ? 1 : (N <= 64 ? 2 : 3);
+    p.nmblk = cdiv(M, GBM);
+    p.nnblk = cdiv(N, 32 * nt);
+    hipStream_t st = (hipStream_t)stream;
+    if (K == 0) {  // C = beta * C + bias: run the kernel with an empty reduction
+        la = 2; lb = 2;
+    }
+    if (nt == 3) return launch_gemm_nt<3>(p, la, lb, batch, st);
+    if (nt == 2) return launch_gemm_nt<2>(p, la, lb, batch, st);
+    return launch_gemm_nt<1>(p, la, lb, batch, st);
+}
+
+extern "C" size_t tcx_conv_wgrad_workspace(int Bt, int Ho, int Wo, int Cin, int Cout, int ks) {
+    int nt, ns, cps, nk, nc;
+    const int K = ks * ks * Cin;
+    wgrad_plan(Bt * Ho * Wo, K, Cout, &nt, &ns, &cps, &nk, &nc);
+    return (size_t)ns * K * Cout * sizeof(float) + 256;
+}
+
+extern "C" int tcx_conv_wgrad(const float* x1, const float* x2, int Bt, int H, int W, int C1, int C2,
+                              const float* dy, int Cout, int ks, int stride, int pad, int circular, float beta,
+                              float* dw, void* ws, size_t ws_bytes, void* stream) {
+    TCX_REQUIRE(x1 && dy && dw && ws, "tcx_conv_wgrad: null pointer");
+    TCX_REQUIRE((C2 == 0) == (x2 == nullptr) && C1 > 0 && C2 >= 0 && Cout > 0 && Bt >= 0, "tcx_conv_wgrad: bad shape");
+    TCX_REQUIRE(ks >= 1 && stride >= 1 && pad >= 0, "tcx_conv_wgrad: bad geometry");
+    WgParams p{};
+    p.x1 = x1; p.x2 = x2; p.C1 = C1; p.C2 = C2; p.Cin = C1 + C2; p.H = H; p.W = W;
+    p.Ho = (H + 2 * pad - ks) / stride + 1;
+    p.Wo = (W + 2 * pad - ks) / stride + 1;
+    TCX_REQUIRE(p.Ho > 0 && p.Wo > 0, "tcx_conv_wgrad: empty output");
+    p.HoWo = p.Ho * p.Wo; p.M = Bt * p.HoWo;
+    p.ks = ks; p.stride = stride; p.pad = pad; p.circular = circular;
+    p.dy = dy; p.Cout = Cout; p.K = ks * ks * p.Cin;
+    int nt;
+    wgrad_plan(p.M, p.K, Cout, &nt, &p.nsplit, &p.cps, &p.nkblk, &p.ncblk);
+    const size_t need = (size_t)p.nsplit * p.K * Cout * sizeof(float);
+    char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
+    TCX_REQUIRE(need + (base - (char*)ws) <= ws_bytes, "tcx_conv_wgrad: workspace too small (%zu < %zu)", ws_bytes,
+                need + 256);
+    p.part = reinterpret_cast<float*>(base);
+    const bool asc = (C1 % 4 != 0) || (C2 % 4 != 0) || !aligned16(x1) || (x2 && !aligned16(x2));
+    const bool bsc = (Cout % 4 != 0) || !aligned16(dy);
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(p.nkblk * p.ncblk, p.nsplit);
+#define TCX_W(NT_)                                                                                     \
+    do {                                                                                               \
+        if (!asc && !bsc) hipLaunchKernelGGL((k_wgrad<NT_, false, false>), grid, dim3(256), 0, st, p); \
+        else if (!asc) hipLaunchKernelGGL((k_wgrad<NT_, false, true>), grid, dim3(256), 0, st, p);     \
+        else if (!bsc) hipLaunchKernelGGL((k_wgrad<NT_, true, false>), grid, dim3(256), 0, st, p);     \
+        else hipLaunchKernelGGL((k_wgrad<NT_, true, true>), grid, dim3(256), 0, st, p);                \
+    } while (0)
+    if (nt == 3) TCX_W(3);
+    else if (nt == 2) TCX_W(2);
+    else TCX_W(1);
+#undef TCX_W
+    TCX_TRY(check_launch("tcx_conv_wgrad"));
+    const size_t n = (size_t)p.K * Cout;
+    const int blocks = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, st, p.part, p.nsplit, p.K, Cout, p.Cin, ks, beta,
+                       dw);
+    return check_launch("tcx_conv_wgrad reduce");
+}

@@ -21,6 +21,7 @@ c_int = ctypes.c_int
 c_float = ctypes.c_float
 c_size = ctypes.c_size_t
 c_u64 = ctypes.c_uint64
+c_ll = ctypes.c_longlong
 
 TCX_SCAL = 8
 
@@ -41,6 +42,10 @@ class TcxUnet(ctypes.Structure):
                                        "cout_b", "map_wsum")]
                 + [(n, TcxConv) for n in _CONV_NAMES]
                 + [("out_w", c_fp), ("out_b", c_float), ("gn_w", c_fp * 11), ("gn_b", c_fp * 11)])
+
+
+class TcxAdamTensor(ctypes.Structure):
+    _fields_ = [("p", c_fp), ("g", c_fp), ("m", c_fp), ("v", c_fp), ("n", c_ll)]
 
 
 # name -> (restype, argtypes)
@@ -72,6 +77,52 @@ _SIGS = {
     "tcx_randn": (c_int, [c_fp, c_size, c_u64, c_u64, c_fp]),
     "tcx_linear": (c_int, [c_fp, c_int, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_layernorm_film": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_float, c_fp]),
+    # training path
+    "tcx_gemm": (c_int, [c_int, c_int, c_int, c_float, c_fp, c_ll, c_ll, c_fp, c_ll, c_ll, c_float, c_fp, c_ll, c_ll,
+                         c_fp, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_fp]),
+    "tcx_conv_wgrad_workspace": (c_size, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "tcx_conv_wgrad": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_int, c_int, c_int, c_int, c_int,
+                               c_float, c_fp, c_fp, c_size, c_fp]),
+    "tcx_pack_conv_dgrad_weight": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_conv_transpose2x": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int,
+                                     c_int, c_fp]),
+    "tcx_gn_stats": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_float, c_fp, c_fp, c_fp, c_fp,
+                             c_fp]),
+    "tcx_gn_bwd_workspace": (c_size, [c_int, c_int, c_int]),
+    "tcx_gn_bwd": (c_int, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp,
+                           c_fp, c_fp, c_size, c_fp]),
+    "tcx_upsample2x_bwd": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_colsum_workspace": (c_size, [c_int, c_int, c_int]),
+    "tcx_colsum": (c_int, [c_fp, c_int, c_int, c_int, c_fp, c_fp, c_float, c_fp, c_size, c_fp]),
+    "tcx_softmax_rows": (c_int, [c_fp, c_fp, c_ll, c_int, c_fp]),
+    "tcx_softmax_bwd_rows": (c_int, [c_fp, c_fp, c_fp, c_ll, c_int, c_fp]),
+    "tcx_act_fwd": (c_int, [c_fp, c_fp, c_size, c_int, c_fp]),
+    "tcx_act_bwd": (c_int, [c_fp, c_fp, c_fp, c_size, c_int, c_fp]),
+    "tcx_mse_loss": (c_int, [c_fp, c_fp, c_size, c_fp, c_fp, c_size, c_fp]),
+    "tcx_mse_bwd": (c_int, [c_fp, c_fp, c_size, c_fp, c_fp, c_fp]),
+    "tcx_embedding_bwd": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp]),
+    "tcx_ln_fwd": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_float, c_fp, c_fp, c_fp]),
+    "tcx_ln_bwd": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp,
+                           c_fp]),
+    "tcx_adam": (c_int, [c_fp, c_int, c_ll, c_float, c_float, c_float, c_float, c_float, c_ll, c_fp]),
+    "tcx_ema": (c_int, [c_fp, c_int, c_ll, c_float, c_fp]),
+    "tcx_cond_inputs": (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
+    "tcx_prior_temb": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp]),
+    "tcx_embedding_fwd": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp]),
+    "tcx_copy2d": (c_int, [c_fp, c_ll, c_fp, c_ll, c_int, c_int, c_float, c_fp]),
+    "tcx_transpose_bhc": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp]),
+    "tcx_first_conv_bias": (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),
+    "tcx_first_conv_bwd": (c_int, [c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
+    "tcx_qsample_vp": (c_int, [c_fp, c_fp, c_fp, c_float, c_float, c_float, c_int, c_int, c_fp, c_fp, c_fp]),
+    "tcx_cond_drop": (c_int, [c_fp, c_fp, c_fp, c_float, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
+    "tcx_prior_qsample": (c_int, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
+    "tcx_reparam": (c_int, [c_fp, c_fp, c_fp, c_size, c_fp, c_fp]),
+    "tcx_reparam_bwd": (c_int, [c_fp, c_fp, c_fp, c_size, c_fp, c_fp, c_float, c_fp]),
+    "tcx_vae_kl": (c_int, [c_fp, c_fp, c_int, c_int, c_float, c_fp, c_fp]),
+    "tcx_vae_kl_bwd": (c_int, [c_fp, c_fp, c_int, c_int, c_float, c_fp, c_fp, c_fp, c_float, c_fp]),
+    "tcx_vae_yvec": (c_int, [c_fp, c_fp, c_fp, c_float, c_int, c_int, c_int, c_fp, c_fp]),
+    "tcx_ddim_step": (c_int, [c_fp, c_fp, c_size, c_float, c_float, c_int, c_fp]),
+    "tcx_q_sample": (c_int, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_fp, c_fp]),
 }
 
 _lib = None

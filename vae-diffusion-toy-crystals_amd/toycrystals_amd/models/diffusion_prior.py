@@ -6,8 +6,11 @@ state_dict keys, seeded init).  The forward runs in libtcx as fp32-MFMA GEMMs:
   all n_blocks FiLM `cond` linears ONE [B,2W] x [2W, n_blocks*2W] GEMM  (:47, cond shared)
   per block LN+FiLM (tcx_layernorm_film), fc1+SiLU, fc2 + residual epilogue (:49-54)
   out LayerNorm, out_proj                                              (:125-126)
-The [B,64] sinusoid of the integer t (:11-25) and the y_cat embedding row gather are host
-plumbing of a few hundred bytes per sample.  Backward is not implemented this round.
+The integer-t sinusoid (:11-25), the y_cat row gather, q_sample and the DDIM update run in
+libtcx kernels too (tcx_prior_temb / tcx_embedding_fwd / tcx_q_sample / tcx_ddim_step).
+Training: with autograd on, the same forward runs as a chain of libtcx autograd Functions
+(functional.py): GEMM linears, per-block LayerNorm+FiLM with its fused backward, residual
+added in the fc2 GEMM (beta = 1).
 """
 from __future__ import annotations
 
@@ -18,7 +21,29 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import functional as TF
 from .._lib import check, lib, ptr, require_gpu_tensor, stream_ptr
+
+_FREQS = {}
+
+
+def _temb_freqs(dim: int, device) -> torch.Tensor:
+    """exp(-linspace(0, ln 1e4, half)) with the reference's fp32 torch arithmetic, cached on device."""
+    key = (dim, torch.device(device))
+    if key not in _FREQS:
+        half = dim // 2
+        f = torch.exp(torch.linspace(0, math.log(10_000), steps=half, dtype=torch.float32) * (-1.0))
+        _FREQS[key] = f.to(device)
+    return _FREQS[key]
+
+
+def _temb_dev(t: torch.Tensor, dim: int) -> torch.Tensor:
+    t = t.to(torch.int64).contiguous()
+    B = t.shape[0]
+    te = torch.empty((B, dim), device=t.device, dtype=torch.float32)
+    check(lib().tcx_prior_temb(ptr(t), ptr(_temb_freqs(dim, t.device)), B, dim, ptr(te), stream_ptr(t.device)),
+          "tcx_prior_temb")
+    return te
 
 
 def timestep_embedding(t: torch.Tensor, dim: int) -> torch.Tensor:
@@ -130,17 +155,42 @@ class DiffusionPriorFiLM(nn.Module):
             self._pk_key = key
         return self._pk
 
-    @torch.no_grad()
     def forward(self, z_t: torch.Tensor, t: torch.Tensor, y_cat: torch.Tensor, y_cont: torch.Tensor) -> torch.Tensor:
         require_gpu_tensor(z_t, "z_t")
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            return self._forward_train(z_t, t, y_cat, y_cont)
+        with torch.no_grad():
+            return self._forward_eval(z_t, t, y_cat, y_cont)
+
+    def _forward_train(self, z_t, t, y_cat, y_cont):
+        """Differentiable forward (diffusion_prior.py:108-127) on libtcx autograd Functions."""
+        te = _temb_dev(t, self.t_emb_dim)
+        t_feat = TF.linear(TF.act(TF.linear(te, self.t_mlp[0]), TF.ACT_SILU), self.t_mlp[2])
+        ycf = TF.EmbeddingFn.apply(y_cat.to(torch.int64), self.y_cat_emb.weight)
+        ycont = TF.linear(TF.act(TF.linear(y_cont.to(torch.float32), self.y_cont_mlp[0]), TF.ACT_SILU),
+                          self.y_cont_mlp[2])
+        y_feat = TF.linear(TF.act(TF.linear(TF.cat_cols(ycf, ycont), self.y_fuse[0]), TF.ACT_SILU), self.y_fuse[2])
+        cond = TF.cat_cols(t_feat, y_feat)
+        h = TF.linear(z_t.to(torch.float32), self.in_proj)
+        for blk in self.blocks:
+            gb = TF.linear(cond, blk.cond)  # [gamma | beta] = cond(cond).chunk(2)
+            hn = TF.LayerNormFiLMFn.apply(h, blk.norm.weight, blk.norm.bias, gb, blk.norm.eps)
+            h = TF.linear(TF.act(TF.linear(hn, blk.fc1), TF.ACT_SILU), blk.fc2, resid=h)
+        hn = TF.LayerNormFiLMFn.apply(h, self.out_norm.weight, self.out_norm.bias, None, self.out_norm.eps)
+        return TF.linear(hn, self.out_proj)
+
+    def _forward_eval(self, z_t, t, y_cat, y_cont):
         pk = self._tcx(z_t.device)
         st = stream_ptr(z_t.device)
         W = self.width
-        te = timestep_embedding(t, self.t_emb_dim).contiguous()
+        te = _temb_dev(t, self.t_emb_dim)
         t_feat = _lin(_lin(te, None, pk.t_mlp[0], act=3), None, pk.t_mlp[1], act=0)
         yc = _lin(_lin(y_cont.to(torch.float32).contiguous(), None, pk.y_cont_mlp[0], act=3), None,
                   pk.y_cont_mlp[1], act=0)
-        ycat_feat = pk.y_cat_emb.index_select(0, y_cat.to(torch.int64)).contiguous()
+        yci = y_cat.to(torch.int64).contiguous()
+        ycat_feat = torch.empty((yci.shape[0], pk.y_cat_emb.shape[1]), device=z_t.device, dtype=torch.float32)
+        check(lib().tcx_embedding_fwd(ptr(yci), ptr(pk.y_cat_emb), yci.shape[0], pk.y_cat_emb.shape[1],
+                                      ptr(ycat_feat), st), "tcx_embedding_fwd")
         y_feat = _lin(_lin(ycat_feat, yc, pk.y_fuse[0], act=3), None, pk.y_fuse[1], act=0)
         gb_all = _lin(t_feat, y_feat, pk.cond_all, act=0)  # [B, n_blocks*2W]
         h = _lin(z_t.to(torch.float32).contiguous(), None, pk.in_proj, act=0)
@@ -179,31 +229,40 @@ class DiffusionSchedule:
                                  sqrt_one_minus_alpha_bars=mv(torch.sqrt(1.0 - alpha_bars)))
 
     def q_sample(self, z0: torch.Tensor, t: torch.Tensor, eps: torch.Tensor) -> torch.Tensor:
-        a = self.sqrt_alpha_bars[t].unsqueeze(1)
-        b = self.sqrt_one_minus_alpha_bars[t].unsqueeze(1)
-        return a * z0 + b * eps
+        """z_t = sqrt(abar_t) z0 + sqrt(1 - abar_t) eps (diffusion_prior.py:194-201)."""
+        z0 = z0.to(torch.float32).contiguous()
+        eps = eps.to(device=z0.device, dtype=torch.float32).contiguous()
+        t = t.to(device=z0.device, dtype=torch.int64).contiguous()
+        out = torch.empty_like(z0)
+        check(lib().tcx_q_sample(ptr(z0), ptr(t), ptr(eps), ptr(self.sqrt_alpha_bars),
+                                 ptr(self.sqrt_one_minus_alpha_bars), z0.shape[0], z0.shape[1], ptr(out),
+                                 stream_ptr(z0.device)), "tcx_q_sample")
+        return out
 
     @torch.no_grad()
     def ddim_sample(self, model: nn.Module, y_cat: torch.Tensor, y_cont: torch.Tensor, n_steps: int = 50,
                     eta: float = 0.0, z_init: torch.Tensor | None = None) -> torch.Tensor:
+        """DDIM (eta = 0) over the rounded, de-duplicated linspace grid (diffusion_prior.py:203-252)."""
         model.eval()
         device = self.betas.device
         B = int(y_cat.shape[0])
         z = torch.randn((B, model.z_dim), device=device) if z_init is None else z_init.to(device).float()
+        z = z.contiguous().clone()
         T = int(self.betas.shape[0])
         ts = torch.round(torch.linspace(T - 1, 0, steps=n_steps)).to(torch.int64)
         ts = torch.unique_consecutive(ts).tolist()
         n = len(ts)
+        abar = self.alpha_bars.detach().float().cpu()
+        st = stream_ptr(device)
         for i in range(n):
             t = torch.full((B,), ts[i], device=device, dtype=torch.int64)
-            eps_pred = model(z, t, y_cat, y_cont)
-            abar_t = self.alpha_bars[t].unsqueeze(1)
-            z0_pred = (z - torch.sqrt(1.0 - abar_t) * eps_pred) / (torch.sqrt(abar_t) + 1e-8)
-            if i == n - 1:
-                z = z0_pred
-                break
-            abar_prev = self.alpha_bars[torch.full((B,), ts[i + 1], device=device, dtype=torch.int64)].unsqueeze(1)
-            if eta != 0.0:
+            eps_pred = model(z, t, y_cat, y_cont).contiguous()
+            last = i == n - 1
+            if not last and eta != 0.0:
                 raise NotImplementedError("eta != 0 not implemented in this minimal version")
-            z = torch.sqrt(abar_prev) * z0_pred + torch.sqrt(1.0 - abar_prev) * eps_pred
+            a_prev = float(abar[ts[i + 1]]) if not last else 1.0
+            check(lib().tcx_ddim_step(ptr(z), ptr(eps_pred), z.numel(), float(abar[ts[i]]), a_prev, 1 if last else 0,
+                                      st), "tcx_ddim_step")
+            if last:
+                break
         return z

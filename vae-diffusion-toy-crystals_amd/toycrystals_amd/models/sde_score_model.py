@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from .. import _lib
+from .. import functional as TF
 from .._lib import TCX_SCAL, TcxConv, TcxUnet, check, lib, ptr, require_gpu_tensor, stream_ptr
 
 
@@ -185,19 +186,6 @@ class _UNetPack:
         return self.ws, self.ws.numel()
 
 
-class _EpsNoGrad(torch.autograd.Function):
-    """Forward through libtcx; the HIP backward (dgrad/wgrad with circular halos) is a later
-    milestone, so differentiating through it raises instead of silently falling back."""
-
-    @staticmethod
-    def forward(ctx, eps, *params):  # noqa: D401
-        return eps
-
-    @staticmethod
-    def backward(ctx, grad):
-        raise NotImplementedError("CondUNetTiny backward on MI355X is not implemented yet (forward/sampling only)")
-
-
 class CondUNetTiny(nn.Module):
     """Tiny conditional U-Net predicting eps_hat = eps_theta(x_t, t, c) (sde_score_model.py:170-266)."""
 
@@ -259,10 +247,57 @@ class CondUNetTiny(nn.Module):
 
     def forward(self, x_t: torch.Tensor, t: torch.Tensor, y_cat: torch.Tensor, y_cont: torch.Tensor) -> torch.Tensor:
         x, t, y_cat, y_cont = self._check_inputs(x_t, t, y_cat, y_cont)
-        eps = _eval_eps(self, x, t, 1, y_cat, y_cont, 0.0)
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            eps = _EpsNoGrad.apply(eps, *[p for p in self.parameters() if p.requires_grad])
-        return eps
+            return self._forward_train(x, t, y_cat, y_cont)
+        return _eval_eps(self, x, t, 1, y_cat, y_cont, 0.0)
+
+    # ---------------------------------------------------------------- training forward
+    def _forward_train(self, x: torch.Tensor, t: torch.Tensor, y_cat: torch.Tensor,
+                       y_cont: torch.Tensor) -> torch.Tensor:
+        """Differentiable forward (sde_score_model.py:243-266) as a chain of libtcx autograd
+        Functions (functional.py); activations NHWC.  Same arithmetic as the fused evaluator,
+        with every intermediate kept for the backward."""
+        B, _, H, W = x.shape
+        E = self.cond_emb.emb_dim
+        ce = self.cond_emb
+        # conditioning (:195-202, :35-82, :227-241)
+        te = torch.empty((B, E), device=x.device)
+        yv = torch.empty((B, self.y_cont_dim), device=x.device)
+        yc = torch.empty((B,), device=x.device, dtype=torch.int64)
+        check(lib().tcx_cond_inputs(ptr(t), ptr(y_cat), ptr(y_cont), B, E, self.n_types, self.y_cont_dim, ptr(te),
+                                    ptr(yv), ptr(yc), stream_ptr(x.device)), "tcx_cond_inputs")
+        temb = TF.linear(TF.act(TF.linear(te, self.time_mlp[0]), TF.ACT_SILU), self.time_mlp[2])
+        t_map = TF.linear(temb, self.to_time_map)
+        e_cat = TF.EmbeddingFn.apply(yc, ce.cat_emb.weight)
+        e_cont = TF.linear(TF.act(TF.linear(yv, ce.cont_mlp[0]), TF.ACT_SILU), ce.cont_mlp[2])
+        cemb = TF.linear(TF.act(TF.cat_cols(e_cat, e_cont), TF.ACT_SILU), ce.out[1])
+        c_map = TF.linear(cemb, self.to_cond_map)
+        maps = TF.cat_cols(t_map, c_map)  # channel order of torch.cat([x_t, t_map, c_map]) (:246)
+
+        def block(h, blk, x2=None):
+            h = TF.group_norm_act(TF.conv2d(h, x2, blk.net[0]), blk.net[1], True)
+            return TF.group_norm_act(TF.conv2d(h, None, blk.net[3]), blk.net[4], True)
+
+        d1 = self.down1.net
+        h = TF.FirstConvFn.apply(x.view(B, H, W, 1), maps, d1[0].weight, d1[0].bias)
+        h = TF.group_norm_act(h, d1[1], True)
+        h1 = TF.group_norm_act(TF.conv2d(h, None, d1[3]), d1[4], True)
+        h = TF.conv2d(h1, None, self.ds1)
+        h2 = block(h, self.down2)
+        h = TF.conv2d(h2, None, self.ds2)
+        h = block(h, self.mid)
+        # attention (:140-167): x_in + proj(SDPA(qkv(GN(x_in))))
+        at = self.attn
+        Bq, Hq, Wq, Cq = h.shape
+        qkv = TF.conv2d(TF.group_norm_act(h, at.norm, False), None, at.qkv)
+        a = TF.AttentionFn.apply(qkv.view(Bq, Hq * Wq, 3 * Cq), at.num_heads)
+        h = TF.conv2d(a.view(Bq, Hq, Wq, Cq), None, at.proj, resid=h)
+        h = TF.conv2d(TF.Upsample2xFn.apply(h), None, self.us2_conv)
+        h = block(h, self.up2, x2=h2)
+        h = TF.conv2d(TF.Upsample2xFn.apply(h), None, self.us1_conv)
+        h = block(h, self.up1, x2=h1)
+        eps = TF.conv2d(h, None, self.out)  # [B, H, W, 1] == [B, 1, H, W]
+        return eps.view(B, 1, H, W)
 
 
 def _eval_eps(model: CondUNetTiny, x, t, t_per_sample, y_cat, y_cont, guidance: float) -> torch.Tensor:
@@ -350,27 +385,45 @@ def save_sde_samples(model: CondUNetTiny, sde: VPSDE, out_path: str, device: tor
 
 
 def diffusion_loss_eps(model: CondUNetTiny, sde: VPSDE, x0: torch.Tensor, y_cat: torch.Tensor,
-                       y_cont: torch.Tensor, p_uncond: float = 0.1, t_power: float = 1.0) -> torch.Tensor:
+                       y_cont: torch.Tensor, p_uncond: float = 0.1, t_power: float = 1.0, *,
+                       draws: Optional[Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]] = None
+                       ) -> torch.Tensor:
     """Eps-prediction denoising loss with CFG condition dropout (sde_score_model.py:358-399).
-    Same RNG draw order as the reference (u, eps, drop).  Forward value only this round."""
+
+    Same RNG draw order as the reference: u = rand(B), eps = randn_like(x0), then (p_uncond > 0)
+    rand(B) for the dropout, from torch's generator on x0's device.  `draws=(u, eps, drop_u)`
+    injects them instead (parity runs against the reference's CPU draws).  The data path
+    (t = u^p, alpha/sigma, x_t, dropout, MSE and its gradient) runs in libtcx kernels."""
+    require_gpu_tensor(x0, "x0")
     device = x0.device
     B = x0.shape[0]
-    x0 = x0 * 2.0 - 1.0
-    u = torch.rand((B,), device=device)
-    t = u ** float(t_power)
-    eps = torch.randn_like(x0)
-    a = sde.alpha(t).view(B, 1, 1, 1)
-    s = sde.sigma(t).view(B, 1, 1, 1)
-    x_t = a * x0 + s * eps
-    if p_uncond > 0.0:
-        drop = (torch.rand((B,), device=device) < p_uncond)
-        if drop.any():
-            y_cat = y_cat.clone()
-            y_cont = y_cont.clone()
-            y_cat[drop] = model.n_types
-            y_cont[drop] = 0.0
-    eps_hat = model(x_t, t, y_cat, y_cont)
-    return torch.mean((eps_hat - eps) ** 2)
+    if draws is None:
+        u = torch.rand((B,), device=device)
+        eps = torch.randn_like(x0)
+        drop_u = torch.rand((B,), device=device) if p_uncond > 0.0 else None
+    else:
+        u, eps, drop_u = draws
+        u = u.to(device=device, dtype=torch.float32).contiguous()
+        eps = eps.to(device=device, dtype=torch.float32).contiguous()
+        drop_u = drop_u.to(device=device, dtype=torch.float32).contiguous() if (
+            drop_u is not None and p_uncond > 0.0) else None
+    x0 = x0.to(torch.float32).contiguous()
+    eps = eps.contiguous()
+    HW = x0[0].numel()
+    st = stream_ptr(device)
+    L = lib()
+    t = torch.empty((B,), device=device)
+    x_t = torch.empty_like(x0)
+    check(L.tcx_qsample_vp(ptr(x0), ptr(eps), ptr(u), float(t_power), float(sde.beta_min),
+                           float(0.5 * (sde.beta_max - sde.beta_min)), B, HW, ptr(t), ptr(x_t), st), "tcx_qsample_vp")
+    yc = torch.empty((B,), device=device, dtype=torch.int64)
+    yv = torch.empty((B, y_cont.shape[1]), device=device)
+    y_cat = y_cat.to(device=device, dtype=torch.int64).contiguous()
+    y_cont = y_cont.to(device=device, dtype=torch.float32).contiguous()
+    check(L.tcx_cond_drop(ptr(y_cat), ptr(y_cont), ptr(drop_u), float(p_uncond), B, y_cont.shape[1], model.n_types,
+                          ptr(yc), ptr(yv), st), "tcx_cond_drop")
+    eps_hat = model(x_t, t, yc, yv)
+    return TF.mse_loss(eps_hat, eps)
 
 
 @torch.no_grad()

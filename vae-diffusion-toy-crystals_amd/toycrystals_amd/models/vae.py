@@ -7,8 +7,13 @@ with fused ReLU, the decoder's ConvTranspose2d(4, s2, p1) as four sub-pixel phas
 fused ReLU / sigmoid.  Activations are NHWC inside; the flatten/view of the 256x4x4 map is
 folded into a column/row permutation of enc_fc / dec_fc at pack time.
 The reparameterisation noise and the training-time condition dropout draw from torch's RNG
-in the reference's order (vae.py:57-60, 65-67); those [B, z]/[B, 8] elementwise steps are host
-plumbing.  Backward is not implemented this round (forward/encode/decode only).
+in the reference's order (vae.py:57-60, 65-67); the one-hot/concat condition vector, the
+keep mask and the reparameterisation run in libtcx kernels (tcx_vae_yvec, tcx_reparam).
+
+Training: with autograd on (grad enabled and parameters requiring grad) the same forward runs
+as a chain of libtcx autograd Functions (functional.py): Conv2d(4,2,1)+ReLU encoder, the NCHW
+flatten as an explicit [16][256] -> [256][16] transpose, FCs on the fp32-MFMA GEMM,
+ConvTranspose2d phases, Sigmoid; `kl_stats` (train_vae.py:17-36) is functional.kl_stats.
 """
 from __future__ import annotations
 
@@ -16,6 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import functional as TF
 from .._lib import check, lib, ptr, require_gpu_tensor, stream_ptr
 
 
@@ -121,10 +127,44 @@ class _VAEBase(nn.Module):
             h, H, W = y, 2 * H, 2 * W
         return h.reshape(B, 1, H, W)  # C == 1: NHWC == NCHW
 
-    def reparameterise(self, mu: torch.Tensor, logvar: torch.Tensor) -> torch.Tensor:
-        std = torch.exp(0.5 * logvar)
-        eps = torch.randn_like(std)
-        return mu + std * eps
+    def _grad_mode(self) -> bool:
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+
+    def reparameterise(self, mu: torch.Tensor, logvar: torch.Tensor, eps: torch.Tensor = None) -> torch.Tensor:
+        """mu + exp(0.5 logvar) * eps, eps = randn_like(std) (vae.py:57-60)."""
+        mu, logvar = mu.float().contiguous(), logvar.float().contiguous()
+        if eps is None:
+            eps = torch.randn_like(mu)
+        eps = eps.to(device=mu.device, dtype=torch.float32).contiguous()
+        if torch.is_grad_enabled() and (mu.requires_grad or logvar.requires_grad):
+            return TF.ReparamFn.apply(mu, logvar, eps)
+        z = torch.empty_like(mu)
+        check(lib().tcx_reparam(ptr(mu), ptr(logvar), ptr(eps), mu.numel(), ptr(z), stream_ptr(mu.device)),
+              "tcx_reparam")
+        return z
+
+    # ---------------------------------------------------------------- training path (autograd)
+    def _enc_train(self, x: torch.Tensor, y: torch.Tensor = None):
+        require_gpu_tensor(x, "x")
+        B = x.shape[0]
+        h = x.float().contiguous().view(B, x.shape[2], x.shape[3], 1)
+        for i in (0, 2, 4, 6):
+            h = TF.act(TF.conv2d(h, None, self.enc[i]), TF.ACT_RELU)
+        _, Hh, Wh, Ch = h.shape
+        hf = TF.TransposeBHCFn.apply(h.view(B, Hh * Wh, Ch)).view(B, Ch * Hh * Wh)  # h.flatten(1) of NCHW
+        if y is not None:
+            hf = TF.cat_cols(hf, y)
+        h = TF.act(TF.linear(hf, self.enc_fc), TF.ACT_RELU)
+        return TF.linear(h, self.mu), TF.linear(h, self.logvar)
+
+    def _dec_train(self, zc: torch.Tensor):
+        B = zc.shape[0]
+        hd = TF.linear(zc, self.dec_fc)  # [B, 256*4*4] in the reference's .view(-1, 256, 4, 4) order
+        hd = TF.TransposeBHCFn.apply(hd.view(B, 256, 16)).view(B, 4, 4, 256)
+        for j, i in enumerate((0, 2, 4, 6)):
+            ct = self.dec[i]
+            hd = TF.act(TF.ConvTranspose2xFn.apply(hd, ct.weight, ct.bias), TF.ACT_SIGMOID if j == 3 else TF.ACT_RELU)
+        return hd.view(B, 1, hd.shape[1], hd.shape[2])
 
 
 class CondVAE(_VAEBase):
@@ -152,33 +192,50 @@ class CondVAE(_VAEBase):
             nn.ConvTranspose2d(32, 1, kernel_size=4, stride=2, padding=1), nn.Sigmoid(),
         )
 
-    def _y_vec(self, y_cat: torch.Tensor, y_cont: torch.Tensor) -> torch.Tensor:
-        y_oh = F.one_hot(y_cat, num_classes=self.n_types).to(dtype=torch.float32)
-        return torch.cat([y_oh, y_cont.to(dtype=torch.float32)], dim=1).contiguous()
+    def _y_vec(self, y_cat: torch.Tensor, y_cont: torch.Tensor, keep_u: torch.Tensor = None) -> torch.Tensor:
+        """[one_hot(y_cat) | y_cont] (vae.py:45-48), optionally times the keep mask (vae.py:65-67)."""
+        y_cat = y_cat.to(torch.int64).contiguous()
+        y_cont = y_cont.to(device=y_cat.device, dtype=torch.float32).contiguous()
+        B = y_cat.shape[0]
+        out = torch.empty((B, self.y_dim), device=y_cat.device, dtype=torch.float32)
+        check(lib().tcx_vae_yvec(ptr(y_cat), ptr(y_cont), ptr(keep_u), float(self.cond_drop), B, self.n_types,
+                                 self.y_cont_dim, ptr(out), stream_ptr(y_cat.device)), "tcx_vae_yvec")
+        return out
 
-    @torch.no_grad()
-    def encode(self, x, y_cat, y_cont):
-        h = self._encode_img(x)
-        y = self._y_vec(y_cat, y_cont)
-        h = _linear(h, y, self._pk.enc_fc[0], self._pk.enc_fc[1], act=1)
-        ml = _linear(h, None, self._pk.heads[0], self._pk.heads[1], act=0)
-        return ml[:, :self.z_dim].contiguous(), ml[:, self.z_dim:].contiguous()
-
-    @torch.no_grad()
-    def decode(self, z, y_cat, y_cont):
-        require_gpu_tensor(z, "z")
-        pk = self._tcx(z.device)
-        y = self._y_vec(y_cat, y_cont)
+    def _keep_u(self, B: int, device, keep_u=None):
         if self.training and self.cond_drop > 0.0:
-            keep = (torch.rand((y.shape[0], 1), device=y.device) >= self.cond_drop).to(y.dtype)
-            y = (y * keep).contiguous()
-        h = _linear(z.float().contiguous(), y, pk.dec_fc[0], pk.dec_fc[1], act=0)
-        return self._decode_map(h)
+            if keep_u is None:
+                keep_u = torch.rand((B, 1), device=device)
+            return keep_u.to(device=device, dtype=torch.float32).contiguous()
+        return None
 
-    def forward(self, x, y_cat, y_cont):
+    def encode(self, x, y_cat, y_cont):
+        if self._grad_mode():
+            return self._enc_train(x, self._y_vec(y_cat, y_cont))
+        with torch.no_grad():
+            h = self._encode_img(x)
+            y = self._y_vec(y_cat, y_cont)
+            h = _linear(h, y, self._pk.enc_fc[0], self._pk.enc_fc[1], act=1)
+            ml = _linear(h, None, self._pk.heads[0], self._pk.heads[1], act=0)
+            return ml[:, :self.z_dim].contiguous(), ml[:, self.z_dim:].contiguous()
+
+    def decode(self, z, y_cat, y_cont, *, keep_u: torch.Tensor = None):
+        require_gpu_tensor(z, "z")
+        y = self._y_vec(y_cat, y_cont, self._keep_u(z.shape[0], z.device, keep_u))
+        if self._grad_mode():
+            return self._dec_train(TF.cat_cols(z.float(), y))
+        with torch.no_grad():
+            pk = self._tcx(z.device)
+            h = _linear(z.float().contiguous(), y, pk.dec_fc[0], pk.dec_fc[1], act=0)
+            return self._decode_map(h)
+
+    def forward(self, x, y_cat, y_cont, *, draws=None):
+        """x_hat, mu, logvar (vae.py:70-78).  draws = (reparam eps [B,z], keep_u [B,1]) injects the
+        reference's two RNG draws (randn_like then rand) for parity runs."""
+        eps, keep_u = draws if draws is not None else (None, None)
         mu, logvar = self.encode(x, y_cat, y_cont)
-        z = self.reparameterise(mu, logvar)
-        return self.decode(z, y_cat, y_cont), mu, logvar
+        z = self.reparameterise(mu, logvar, eps)
+        return self.decode(z, y_cat, y_cont, keep_u=keep_u), mu, logvar
 
 
 class VAE(_VAEBase):
@@ -204,21 +261,26 @@ class VAE(_VAEBase):
             nn.ConvTranspose2d(32, 1, kernel_size=4, stride=2, padding=1), nn.Sigmoid(),
         )
 
-    @torch.no_grad()
     def encode(self, x):
-        h = self._encode_img(x)
-        h = _linear(h, None, self._pk.enc_fc[0], self._pk.enc_fc[1], act=1)
-        ml = _linear(h, None, self._pk.heads[0], self._pk.heads[1], act=0)
-        return ml[:, :self.z_dim].contiguous(), ml[:, self.z_dim:].contiguous()
+        if self._grad_mode():
+            return self._enc_train(x)
+        with torch.no_grad():
+            h = self._encode_img(x)
+            h = _linear(h, None, self._pk.enc_fc[0], self._pk.enc_fc[1], act=1)
+            ml = _linear(h, None, self._pk.heads[0], self._pk.heads[1], act=0)
+            return ml[:, :self.z_dim].contiguous(), ml[:, self.z_dim:].contiguous()
 
-    @torch.no_grad()
     def decode(self, z):
         require_gpu_tensor(z, "z")
-        pk = self._tcx(z.device)
-        h = _linear(z.float().contiguous(), None, pk.dec_fc[0], pk.dec_fc[1], act=0)
-        return self._decode_map(h)
+        if self._grad_mode():
+            return self._dec_train(z.float())
+        with torch.no_grad():
+            pk = self._tcx(z.device)
+            h = _linear(z.float().contiguous(), None, pk.dec_fc[0], pk.dec_fc[1], act=0)
+            return self._decode_map(h)
 
-    def forward(self, x):
+    def forward(self, x, *, draws=None):
+        eps = draws[0] if draws is not None else None
         mu, logvar = self.encode(x)
-        z = self.reparameterise(mu, logvar)
+        z = self.reparameterise(mu, logvar, eps)
         return self.decode(z), mu, logvar
