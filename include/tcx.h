@@ -286,7 +286,8 @@ int tcx_ln_bwd(const float* x, const float* dh, int M, int Wd, const float* w, c
                int ld_gb, const float* mean, const float* rstd, float* dx, float* dwrow, float* dbrow, float* dgb,
                void* stream);
 
-/* Multi-tensor optimiser steps over a DEVICE table of tensors.
+/* Multi-tensor optimiser steps over a HOST array of tensor descriptors (copied into the kernel
+ * arguments, 48 tensors per launch: no device table, no host synchronisation).
  * tcx_adam: torch.optim.Adam (amsgrad off) step `step` (1-based) on every {p, g, m, v, n}.
  * tcx_ema:  p = p*decay + (1-decay)*g for every entry ({p_ema, p_model}; m/v unused)
  * (train_sde_score_model.py:233-240). */
@@ -346,6 +347,9 @@ int tcx_ddim_step(float* z, const float* eps, size_t n, float abar_t, float abar
 /* DiffusionSchedule.q_sample with given integer t (diffusion_prior.py:194-201). */
 int tcx_q_sample(const float* z0, const int64_t* t, const float* eps, const float* sqrt_ab, const float* sqrt_1mab,
                  int B, int Z, float* out, void* stream);
+
+/* Device-side batch of the disk dataset: out[b] = x_u8[idx[b]] / 255 (disk_data.py:27-31). */
+int tcx_u8_gather(const uint8_t* x_u8, const int64_t* idx, int B, int npix, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -376,6 +376,7 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int K
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const int k = (int)(i / Cout), co = (int)(i - (size_t)k * Cout);
         float s = 0.f;
+#pragma unroll 8
         for (int sp = 0; sp < nsplit; ++sp) s += part[(size_t)sp * n + i];
         const int tap = k / Cin, ci = k - tap * Cin;
         const size_t o = ((size_t)co * Cin + ci) * ks * ks + tap;
@@ -391,6 +392,7 @@ void wgrad_plan(int M, int K, int Cout, int* nt, int* nsplit, int* cps, int* nkb
     const int nch = cdiv(std::max(M, 1), 32);
     int ns = std::max(1, cdiv(2048, tiles));
     ns = std::min(ns, std::max(1, nch / 8));  // >= 8 chunks per split
+    ns = std::min(ns, 256);                   // the reduction folds ns partials per weight
     *cps = cdiv(nch, ns);
     *nsplit = cdiv(nch, *cps);
 }

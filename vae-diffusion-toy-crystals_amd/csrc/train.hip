@@ -184,17 +184,28 @@ __global__ __launch_bounds__(256) void k_gn_bwd_apply(const float* __restrict__ 
     }
 }
 
-// d gamma[c] = sum_b S2[b][c], d beta[c] = sum_b S1[b][c]
-__global__ void k_gn_bwd_affine(const double* __restrict__ s12, int Bt, int C, float* __restrict__ dgamma,
-                                float* __restrict__ dbeta) {
-    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+// d gamma[c] = sum_b S2[b][c], d beta[c] = sum_b S1[b][c]  (32-lane group per channel, fixed tree)
+__device__ __forceinline__ double group32_sum_d(double v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_gn_bwd_affine(const double* __restrict__ s12, int Bt, int C,
+                                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    const int lane = threadIdx.x & 31;
+    for (int c = blockIdx.x * 8 + (threadIdx.x >> 5); c < C; c += gridDim.x * 8) {
         double a = 0, q = 0;
-        for (int b = 0; b < Bt; ++b) {
+        for (int b = lane; b < Bt; b += 32) {
             a += s12[((size_t)b * C + c) * 2];
             q += s12[((size_t)b * C + c) * 2 + 1];
         }
-        if (dgamma) dgamma[c] = (float)q;
-        if (dbeta) dbeta[c] = (float)a;
+        a = group32_sum_d(a);
+        q = group32_sum_d(q);
+        if (lane == 0) {
+            if (dgamma) dgamma[c] = (float)q;
+            if (dbeta) dbeta[c] = (float)a;
+        }
     }
 }
 
@@ -248,29 +259,83 @@ __global__ __launch_bounds__(256) void k_upsample2x_bwd(const float* __restrict_
 }
 
 // ---------------------------------------------------------------- column sums (bias grads)
-// x [Bt][HW][C]: part[b][split][C] (fp64) -> per_batch[b][C] and total[C] (fixed order).
+// x [Bt][HW][C] -> part[b][split][C] (fp64).  Block = 256 threads as (channel quad, row lane):
+// float4 loads along C, rows strided by the lane count, then an LDS reduction over lanes.
+// Scalar variant (C % 4 != 0 or unaligned): (channel, row lane).
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_colsum_part(const float* __restrict__ x, int HW, int C, int nsplit,
                                                      double* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) double cs_red[];  // [lanes][cols]
     const int b = blockIdx.y, sp = blockIdx.x;
     const int p0 = (int)((long long)HW * sp / nsplit), p1 = (int)((long long)HW * (sp + 1) / nsplit);
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        double s = 0;
-        for (int pp = p0; pp < p1; ++pp) s += (double)x[((size_t)b * HW + pp) * C + c];
-        part[((size_t)b * nsplit + sp) * C + c] = s;
+    const int W = VEC ? 4 : 1;
+    const int ncol = C / W;                        // columns handled as units
+    const int cpb = ncol < 256 ? ncol : 256;       // columns per pass
+    const int lanes = 256 / cpb;
+    const int tid = threadIdx.x;
+    const int cu = tid % cpb, ln = tid / cpb;
+    for (int c0 = 0; c0 < ncol; c0 += cpb) {
+        const int col = c0 + cu;
+        double s[4] = {0, 0, 0, 0};
+        if (ln < lanes && col < ncol) {
+#pragma unroll 4
+            for (int pp = p0 + ln; pp < p1; pp += lanes) {
+                const float* r = x + ((size_t)b * HW + pp) * C + (size_t)col * W;
+                if (VEC) {
+                    const float4 v = *reinterpret_cast<const float4*>(r);
+                    s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+                } else {
+                    s[0] += r[0];
+                }
+            }
+        }
+        __syncthreads();
+        if (ln < lanes)
+            for (int e = 0; e < W; ++e) cs_red[(size_t)ln * cpb * W + cu * W + e] = s[e];
+        __syncthreads();
+        for (int j = tid; j < cpb * W; j += 256) {
+            const int c = c0 * W + j;
+            if (c >= C) continue;
+            double t = 0;
+            for (int l = 0; l < lanes; ++l) t += cs_red[(size_t)l * cpb * W + j];
+            part[((size_t)b * nsplit + sp) * C + c] = t;
+        }
     }
 }
 
-__global__ void k_colsum_fold(const double* __restrict__ part, int Bt, int nsplit, int C, float* __restrict__ per_b,
-                              float* __restrict__ total, float beta) {
-    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-        double t = 0;
-        for (int b = 0; b < Bt; ++b) {
-            double s = 0;
-            for (int sp = 0; sp < nsplit; ++sp) s += part[((size_t)b * nsplit + sp) * C + c];
-            if (per_b) per_b[(size_t)b * C + c] = (float)s;
-            t += s;
+// per (b, c): fold the splits -> per_b (float) and a double row for the total.  One 32-lane group
+// per output: lane l sums splits l, l+32, ... then a fixed xor-shuffle tree (deterministic).
+__device__ __forceinline__ double group32_sum(double v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_colsum_fold(const double* __restrict__ part, int Bt, int nsplit, int C,
+                                                     float* __restrict__ per_b, double* __restrict__ tot_b) {
+    const size_t n = (size_t)Bt * C;
+    const int lane = threadIdx.x & 31;
+    for (size_t i = blockIdx.x * (size_t)8 + (threadIdx.x >> 5); i < n; i += (size_t)gridDim.x * 8) {
+        const int b = (int)(i / C), c = (int)(i - (size_t)b * C);
+        const double* pp = part + (size_t)b * nsplit * C + c;
+        double s = 0;
+        for (int sp = lane; sp < nsplit; sp += 32) s += pp[(size_t)sp * C];
+        s = group32_sum(s);
+        if (lane == 0) {
+            if (per_b) per_b[i] = (float)s;
+            tot_b[i] = s;
         }
-        if (total) total[c] = beta != 0.f ? beta * total[c] + (float)t : (float)t;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_colsum_total(const double* __restrict__ tot_b, int Bt, int C,
+                                                      float* __restrict__ total, float beta) {
+    const int lane = threadIdx.x & 31;
+    for (int c = blockIdx.x * 8 + (threadIdx.x >> 5); c < C; c += gridDim.x * 8) {
+        double t = 0;
+        for (int b = lane; b < Bt; b += 32) t += tot_b[(size_t)b * C + c];
+        t = group32_sum(t);
+        if (lane == 0) total[c] = beta != 0.f ? beta * total[c] + (float)t : (float)t;
     }
 }
 
@@ -474,8 +539,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ x, con
 // ---------------------------------------------------------------- optimiser
 // torch.optim.Adam single-tensor step (torch/optim/adam.py, weight_decay folded into the grad):
 //   m.lerp_(g, 1-b1); v = v*b2 + (1-b2)*g*g; denom = sqrt(v)/bc2_sqrt + eps; p += (-step_size)*m/denom
+constexpr int kMaxAdamTensors = 48;  // tensors per launch, passed by value in the kernel arguments
 struct AdamArgs {
-    const tcx_adam_tensor* t;
+    tcx_adam_tensor t[kMaxAdamTensors];
     float w1, b2, w2, bc2s, eps, neg_step, wd;
 };
 
@@ -498,10 +564,15 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 }
 
 // p_ema = p_ema * d + (1-d) * p   (mul_(decay).add_(p, alpha=1-decay))
-__global__ __launch_bounds__(256) void k_ema(const tcx_adam_tensor* t, float d, float w) {
-    const tcx_adam_tensor T = t[blockIdx.y];
+struct EmaArgs {
+    tcx_adam_tensor t[kMaxAdamTensors];
+    float d, w;
+};
+
+__global__ __launch_bounds__(256) void k_ema(EmaArgs a) {
+    const tcx_adam_tensor T = a.t[blockIdx.y];
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < T.n; i += (long long)gridDim.x * blockDim.x)
-        T.p[i] = T.p[i] * d + w * T.g[i];
+        T.p[i] = T.p[i] * a.d + a.w * T.g[i];
 }
 
 // ---------------------------------------------------------------- conditioning inputs (score net)
@@ -779,6 +850,17 @@ __global__ void k_q_sample_t(const float* __restrict__ z0, const int64_t* __rest
     }
 }
 
+// Device-side data pipeline (ToyCrystalsDiskDataset.__getitem__, disk_data.py:27-31):
+// out[b][p] = x_u8[idx[b]][p] / 255.0 for a shuffled batch of indices.
+__global__ void k_u8_gather(const uint8_t* __restrict__ x, const int64_t* __restrict__ idx, int B, int npix,
+                            float* __restrict__ out) {
+    const size_t n = (size_t)B * npix;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int b = (int)(i / npix), p = (int)(i - (size_t)b * npix);
+        out[i] = (float)x[(size_t)idx[b] * npix + p] / 255.0f;
+    }
+}
+
 int grid1d(size_t n, int cap = 8192) { return (int)std::max<size_t>(1, std::min<size_t>((n + 255) / 256, cap)); }
 
 }  // namespace
@@ -831,7 +913,7 @@ extern "C" int tcx_gn_bwd(const float* x, const float* dy, const float* scale, c
                        HW, C, silu, dx);
     TCX_TRY(check_launch("tcx_gn_bwd apply"));
     if (dgamma || dbeta) {
-        hipLaunchKernelGGL(k_gn_bwd_affine, dim3(cdiv(C, 256)), dim3(256), 0, st, s12, Bt, C, dgamma, dbeta);
+        hipLaunchKernelGGL(k_gn_bwd_affine, dim3(cdiv(C, 8)), dim3(256), 0, st, s12, Bt, C, dgamma, dbeta);
         TCX_TRY(check_launch("tcx_gn_bwd affine"));
     }
     return TCX_OK;
@@ -845,26 +927,44 @@ extern "C" int tcx_upsample2x_bwd(const float* dy, float* dx, int Bt, int H, int
     return check_launch("tcx_upsample2x_bwd");
 }
 
+static int colsum_nsplit(int Bt, int HW) {
+    // ~>= 2048 blocks overall, >= 64 rows per block
+    int ns = std::max(1, cdiv(2048, std::max(Bt, 1)));
+    ns = std::min(ns, std::max(1, HW / 64));
+    return std::min(ns, 4096);
+}
+
 extern "C" size_t tcx_colsum_workspace(int Bt, int HW, int C) {
-    const int nsplit = std::max(1, std::min(128, HW / 32));
-    return (size_t)Bt * nsplit * C * sizeof(double) + 256;
+    const int nsplit = colsum_nsplit(Bt, HW);
+    return ((size_t)Bt * nsplit * C + (size_t)Bt * C) * sizeof(double) + 512;
 }
 
 extern "C" int tcx_colsum(const float* x, int Bt, int HW, int C, float* per_batch, float* total, float beta, void* ws,
                           size_t ws_bytes, void* stream) {
     TCX_REQUIRE(x && ws && Bt >= 0 && HW >= 0 && C > 0, "tcx_colsum: bad args");
     TCX_REQUIRE(ws_bytes >= tcx_colsum_workspace(Bt, HW, C), "tcx_colsum: workspace too small");
-    const int nsplit = std::max(1, std::min(128, HW / 32));
+    const int nsplit = colsum_nsplit(Bt, HW);
     double* part = reinterpret_cast<double*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
+    double* tot_b = part + (size_t)Bt * nsplit * C;
     hipStream_t st = (hipStream_t)stream;
     if (Bt > 0) {
-        hipLaunchKernelGGL(k_colsum_part, dim3(nsplit, Bt), dim3(std::min(256, ((C + 63) / 64) * 64)), 0, st, x, HW, C,
-                           nsplit, part);
+        const bool vec = C % 4 == 0 && aligned16(x);
+        const int ncol = vec ? C / 4 : C;
+        const int cpb = std::min(ncol, 256);
+        const size_t shm = (size_t)(256 / cpb) * cpb * (vec ? 4 : 1) * sizeof(double);
+        if (vec) hipLaunchKernelGGL(k_colsum_part<true>, dim3(nsplit, Bt), dim3(256), shm, st, x, HW, C, nsplit, part);
+        else hipLaunchKernelGGL(k_colsum_part<false>, dim3(nsplit, Bt), dim3(256), shm, st, x, HW, C, nsplit, part);
         TCX_TRY(check_launch("tcx_colsum part"));
+        const size_t n = (size_t)Bt * C;
+        hipLaunchKernelGGL(k_colsum_fold, dim3((unsigned)std::min<size_t>((n + 7) / 8, 16384)), dim3(256), 0, st, part,
+                           Bt, nsplit, C, per_batch, tot_b);
+        TCX_TRY(check_launch("tcx_colsum fold"));
     }
-    hipLaunchKernelGGL(k_colsum_fold, dim3(cdiv(C, 256)), dim3(256), 0, st, part, Bt, nsplit, C, per_batch, total,
-                       beta);
-    return check_launch("tcx_colsum fold");
+    if (total) {
+        hipLaunchKernelGGL(k_colsum_total, dim3(cdiv(C, 8)), dim3(256), 0, st, tot_b, Bt, C, total, beta);
+        TCX_TRY(check_launch("tcx_colsum total"));
+    }
+    return TCX_OK;
 }
 
 extern "C" int tcx_softmax_rows(const float* S, float* P, long long rows, int n, void* stream) {
@@ -945,10 +1045,8 @@ extern "C" int tcx_ln_bwd(const float* x, const float* dh, int M, int Wd, const 
 
 extern "C" int tcx_adam(const tcx_adam_tensor* table, int ntensors, long long max_n, float lr, float beta1,
                         float beta2, float eps, float weight_decay, long long step, void* stream) {
-    TCX_REQUIRE(table && ntensors >= 0 && step >= 1, "tcx_adam: bad args");
-    if (ntensors == 0) return TCX_OK;
+    TCX_REQUIRE((table || ntensors == 0) && ntensors >= 0 && step >= 1, "tcx_adam: bad args");
     AdamArgs a{};
-    a.t = table;
     // host scalars in double as torch's Python-side arithmetic, then cast to the tensor dtype
     const double b1 = beta1, b2 = beta2;
     const double bc1 = 1.0 - std::pow(b1, (double)step), bc2 = 1.0 - std::pow(b2, (double)step);
@@ -960,17 +1058,29 @@ extern "C" int tcx_adam(const tcx_adam_tensor* table, int ntensors, long long ma
     a.neg_step = (float)(-((double)lr / bc1));
     a.wd = weight_decay;
     const int gx = (int)std::max<long long>(1, std::min<long long>((max_n + 255) / 256, 1024));
-    hipLaunchKernelGGL(k_adam, dim3(gx, ntensors), dim3(256), 0, (hipStream_t)stream, a);
-    return check_launch("tcx_adam");
+    for (int t0 = 0; t0 < ntensors; t0 += kMaxAdamTensors) {
+        const int nt = std::min(kMaxAdamTensors, ntensors - t0);
+        for (int i = 0; i < nt; ++i) a.t[i] = table[t0 + i];
+        hipLaunchKernelGGL(k_adam, dim3(gx, nt), dim3(256), 0, (hipStream_t)stream, a);
+        TCX_TRY(check_launch("tcx_adam"));
+    }
+    return TCX_OK;
 }
 
 extern "C" int tcx_ema(const tcx_adam_tensor* table, int ntensors, long long max_n, float decay, void* stream) {
-    TCX_REQUIRE(table && ntensors >= 0, "tcx_ema: bad args");
-    if (ntensors == 0) return TCX_OK;
+    TCX_REQUIRE((table || ntensors == 0) && ntensors >= 0, "tcx_ema: bad args");
+    EmaArgs a{};
     const double d = decay;
+    a.d = (float)d;
+    a.w = (float)(1.0 - d);
     const int gx = (int)std::max<long long>(1, std::min<long long>((max_n + 255) / 256, 1024));
-    hipLaunchKernelGGL(k_ema, dim3(gx, ntensors), dim3(256), 0, (hipStream_t)stream, table, (float)d, (float)(1.0 - d));
-    return check_launch("tcx_ema");
+    for (int t0 = 0; t0 < ntensors; t0 += kMaxAdamTensors) {
+        const int nt = std::min(kMaxAdamTensors, ntensors - t0);
+        for (int i = 0; i < nt; ++i) a.t[i] = table[t0 + i];
+        hipLaunchKernelGGL(k_ema, dim3(gx, nt), dim3(256), 0, (hipStream_t)stream, a);
+        TCX_TRY(check_launch("tcx_ema"));
+    }
+    return TCX_OK;
 }
 
 extern "C" int tcx_cond_inputs(const float* t, const int64_t* y_cat, const float* y_cont, int B, int E, int n_types,
@@ -1116,4 +1226,12 @@ extern "C" int tcx_q_sample(const float* z0, const int64_t* t, const float* eps,
     hipLaunchKernelGGL(k_q_sample_t, dim3(grid1d(n)), dim3(256), 0, (hipStream_t)stream, z0, t, eps, sqrt_ab, sqrt_1mab,
                        B, Z, out);
     return check_launch("tcx_q_sample");
+}
+
+extern "C" int tcx_u8_gather(const uint8_t* x_u8, const int64_t* idx, int B, int npix, float* out, void* stream) {
+    TCX_REQUIRE(x_u8 && idx && out && B >= 0 && npix > 0, "tcx_u8_gather: bad args");
+    const size_t n = (size_t)B * npix;
+    if (n == 0) return TCX_OK;
+    hipLaunchKernelGGL(k_u8_gather, dim3(grid1d(n)), dim3(256), 0, (hipStream_t)stream, x_u8, idx, B, npix, out);
+    return check_launch("tcx_u8_gather");
 }

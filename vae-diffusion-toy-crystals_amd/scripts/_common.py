@@ -1,0 +1,47 @@
+"""Shared plumbing of the CLI mirrors: package path, device choice, optional torchrun batch-DP."""
+from __future__ import annotations
+
+import os
+import sys
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _PKG_ROOT not in sys.path:
+    sys.path.insert(0, _PKG_ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def pick_device(name: str) -> torch.device:
+    """The reference falls back to CPU without CUDA; this build has no CPU path, so it refuses."""
+    if name == "cpu":
+        raise SystemExit("this MI355X build has no CPU path: use --device cuda (the MI355X under PyTorch-ROCm)")
+    if not torch.cuda.is_available():
+        raise SystemExit("no GPU visible: this build runs on the MI355X only")
+    return torch.device(name)
+
+
+def init_dp():
+    """One process per GPU under torchrun (backend nccl = RCCL over xGMI); (rank, world, device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return 0, 1, None
+    rank = int(os.environ["RANK"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    return rank, world, torch.device("cuda", local)
+
+
+def shutdown_dp(world: int) -> None:
+    if world > 1 and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def allreduce_scalar_mean(v: float, world: int, device) -> float:
+    if world <= 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    return float(t.item()) / world

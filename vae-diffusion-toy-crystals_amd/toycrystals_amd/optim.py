@@ -11,7 +11,6 @@ p_ema = p_ema * decay + (1 - decay) * p.
 """
 from __future__ import annotations
 
-import ctypes
 from typing import Iterable
 
 import torch
@@ -19,10 +18,9 @@ import torch
 from ._lib import TcxAdamTensor, check, lib, stream_ptr
 
 
-def _device_table(entries, device) -> torch.Tensor:
-    arr = (TcxAdamTensor * len(entries))(*entries)
-    host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-    return host.to(device, non_blocking=False)
+def _host_table(entries):
+    """ctypes array of tcx_adam_tensor; libtcx copies it into the kernel arguments."""
+    return (TcxAdamTensor * len(entries))(*entries)
 
 
 class Adam(torch.optim.Optimizer):
@@ -34,8 +32,7 @@ class Adam(torch.optim.Optimizer):
             raise NotImplementedError("amsgrad / maximize are not supported by the fused MI355X Adam")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
                                       maximize=False, foreach=None, capturable=False, differentiable=False,
-                                      fused=None))
-        self._tables = []  # keep device tables alive until the launch is ordered
+                                      fused=None, decoupled_weight_decay=False))
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -44,7 +41,6 @@ class Adam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         L = lib()
-        self._tables = []
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
             by_step = {}
@@ -71,10 +67,9 @@ class Adam(torch.optim.Optimizer):
             for (step, device), items in by_step.items():
                 entries = [TcxAdamTensor(p.data_ptr(), g.data_ptr(), s["exp_avg"].data_ptr(),
                                          s["exp_avg_sq"].data_ptr(), p.numel()) for p, g, s in items]
-                table = _device_table(entries, device)
-                self._tables.append((table, [g for _, g, _ in items]))
+                table = _host_table(entries)
                 max_n = max(p.numel() for p, _, _ in items)
-                check(L.tcx_adam(table.data_ptr(), len(entries), max_n, float(group["lr"]), float(beta1),
+                check(L.tcx_adam(table, len(entries), max_n, float(group["lr"]), float(beta1),
                                  float(beta2), float(group["eps"]), float(group["weight_decay"]), step,
                                  stream_ptr(device)), "tcx_adam")
         return loss
@@ -88,10 +83,8 @@ def ema_update(ema_model: torch.nn.Module, model: torch.nn.Module, decay: float)
         return
     device = pairs[0][1].device
     entries = [TcxAdamTensor(pe.data_ptr(), p.data_ptr(), None, None, p.numel()) for pe, p in pairs]
-    table = _device_table(entries, device)
-    check(lib().tcx_ema(table.data_ptr(), len(entries), max(p.numel() for _, p in pairs), float(decay),
+    check(lib().tcx_ema(_host_table(entries), len(entries), max(p.numel() for _, p in pairs), float(decay),
                         stream_ptr(device)), "tcx_ema")
-    torch.cuda.current_stream(device).synchronize()  # the table is a temporary
 
 
 def params_to(params: Iterable[torch.nn.Parameter]):  # pragma: no cover - convenience
