@@ -15,9 +15,11 @@ samples its own 128 (weak scaling, no data-path collective); the only collective
 barrier and the max-over-ranks reduction of the elapsed time.
 
 Also reports, on one JSON line:
-  roofline     — the dominant kernel (the fp32-MFMA implicit-GEMM conv, k_conv) timed live with HIP
-                 events around every launch in the timed region: achieved algorithmic TFLOP/s vs the
-                 157.3 TFLOP/s fp32 MFMA peak (MI355X_MICROARCH.md).
+  roofline     — the dominant kernel (the implicit-GEMM conv, k_conv) timed live with HIP events around
+                 every launch in the timed region: achieved algorithmic (fp32-equivalent) TFLOP/s vs
+                 the peak of the MFMA it runs on — f16x3 split path (default): the 2.5 PFLOP/s dense
+                 f16 MFMA peak / 3 MFMA products per fp32 multiply-add = 833.3; fp32 path
+                 (--precision fp32): the 157.3 TFLOP/s fp32 MFMA peak (MI355X_MICROARCH.md).
   cpu_baseline — the numpy oracle (a port of the reference's arithmetic) timed on this host's cores on a
                  bounded sample (rank 0, N=1 only) and extrapolated per image to the 602-forward run.
 """
@@ -40,6 +42,8 @@ import torch  # noqa: E402
 GFLOP_PER_IMG_FWD = 7.142544384  # CondUNetTiny(96) forward at 64x64 (reference's 17-ch first conv)
 FWD_PER_IMG = 602                # 300 steps x 2 CFG evaluations + 2 for the final projection
 FP32_PEAK_TFLOPS = 157.3         # MI355X fp32 MFMA (= vector) peak, MI355X_MICROARCH.md
+F16_PEAK_TFLOPS = 2500.0         # MI355X dense f16/bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
+SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 multiply-add
 
 
 def cpu_baseline(state_dict, B: int, n_steps: int, cfg: float, t_end: float) -> dict:
@@ -81,6 +85,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--precision", choices=["f16x3", "fp32"], default="f16x3",
+                    help="conv arithmetic: f16x3 split MFMA (fp32-grade, default) or fp32 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -92,7 +98,8 @@ def main() -> int:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
 
-    from toycrystals_amd._lib import lib
+    from toycrystals_amd._lib import lib, set_conv_precision
+    set_conv_precision(args.precision)
     from toycrystals_amd.models.sde_score_model import CondUNetTiny, VPSDE, sample_reverse_sde_euler_maruyama
 
     torch.manual_seed(0)
@@ -134,13 +141,21 @@ def main() -> int:
     L.tcx_prof_enable(0)
     assert out is not None and bool(torch.isfinite(out).all()) and float(out.min()) >= 0.0 and float(out.max()) <= 1.0
 
+    if args.precision == "f16x3":
+        kname = "k_conv<SPL> (f16x3 split implicit-GEMM conv, 3x v_mfma_f32_32x32x16_f16 per fp32 MAC)"
+        peak = F16_PEAK_TFLOPS / SPLIT_PRODUCTS
+        peak_basis = "2500 TFLOP/s dense f16 MFMA / 3 products per fp32 MAC; achieved in fp32-equivalent FLOPs"
+    else:
+        kname = "k_conv (fp32-MFMA implicit-GEMM conv, v_mfma_f32_32x32x2_f32)"
+        peak = FP32_PEAK_TFLOPS
+        peak_basis = "157.3 TFLOP/s fp32 MFMA"
     images = world * B * args.steps
     value = images / elapsed
     conv_avg_ms = ms.value / max(1, n.value)
     conv_avg_flop = fl.value / max(1, n.value)
     achieved = conv_avg_flop / (conv_avg_ms * 1e-3) / 1e12 if n.value else 0.0
     result = {
-        "metric": "denoised images/sec (300-step reverse-SDE, CFG=1.5)",
+        "metric": "denoised images/sec (300-step reverse-SDE, CFG=1.5) at 1/2/4/8 MI355X",
         "value": round(value, 4),
         "unit": "images/s",
         "n_gpus": world,
@@ -150,16 +165,17 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32" if args.precision == "fp32" else "fp32 (f16x3 split MFMA, fp32-grade)",
         "data": "synthetic (y_cat=i%4, theta=linspace(0,pi/3,B); random-init weights seed 0; Philox noise)",
         "config": {"workload": f"reverse-SDE {args.n_steps} steps, CFG {args.cfg}, t_end {args.t_end}, "
                                f"CondUNetTiny(base_ch={args.base_ch}) 64x64, batch {B}/GPU",
                    "batch_per_gpu": B, "global_batch": world * B, "n_steps": args.n_steps, "cfg": args.cfg,
-                   "image": [1, 64, 64], "parallelism": "replicas" if world == 1 else f"dp{world} (independent shards)"},
+                   "image": [1, 64, 64], "conv_precision": args.precision,
+                   "parallelism": "replicas" if world == 1 else f"dp{world} (independent shards)"},
         "path_tflops": round(value / world * FWD_PER_IMG * GFLOP_PER_IMG_FWD / 1e3, 3),
-        "roofline": {"bound": "mfma", "kernel": "k_conv (fp32-MFMA implicit-GEMM conv)",
-                     "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+        "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": round(peak, 1),
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                     "peak_basis": peak_basis,
                      "avg_launch_ms": round(conv_avg_ms, 5), "avg_launch_gflop": round(conv_avg_flop / 1e9, 4),
                      "launches": n.value,
                      "conv_share_of_step": round(ms.value / 1e3 / elapsed, 4)},

@@ -109,6 +109,43 @@ int tcx_gn_apply_tab(const float* x, float* y, int Bt, int HW, int C, const floa
 int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, int C, const float* scale,
                    const float* shift, void* stream);
 
+/* ------------------------------------------------------------------ f16x3 split path
+ * "h2" storage (csrc/h2.hpp): an fp32 tensor [..][C] (C % 8 == 0) kept as [..][C/8][2][8] f16
+ * = per 8-channel group 8 hi halves then 8 lo halves (hi = f16(v), lo = f16(v - hi)), four bytes
+ * per element like fp32.  A conv over h2 operands forms every product as three f16 MFMAs
+ * (hi*hi + hi*lo + lo*hi, f32 accumulation): fp32-grade results at the f16 MFMA
+ * rate.  Values must stay below 65504 in magnitude: every h2 writer takes `ovf`, a device word
+ * that is OR-ed with 1 when a value does not fit (NULL = no check); the caller then recomputes
+ * in fp32.  Same nn.Conv2d sites as tcx_conv2d (sde_score_model.py:102,105,133-134,208,210,218,
+ * 222). */
+
+/* Split a packed fp32 conv weight (tcx_pack_conv_weight output, [cout_pad][kpad]) into h2 with a
+ * power-of-two scale chosen from max|w|; *wscale (device float) receives the inverse scale. */
+int tcx_pack_conv_weight_h2(const float* wpk, void* wh, float* wscale, int cout_pad, int kpad,
+                            void* stream);
+
+/* tcx_conv2d over h2 sources x1/x2 and h2 weights (MODE-3 geometry: C1 % 32 == 0, C2 in {0, C1},
+ * ks*ks <= 16, kpad == ks*ks*Cin, no upsample/prologue).  Output fp32 (out_h2 = 0) or h2 (1);
+ * the fused GroupNorm statistics are taken on the fp32 output value either way. */
+int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
+                  const void* wh, const float* wscale, const float* bias, const float* bias_b,
+                  const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
+                  int stride, int pad, int circular, int act, double* gn_stats, unsigned* ovf,
+                  void* stream);
+
+/* tcx_gn_apply_tab with the output written as h2 (x == y allowed: in place). */
+int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale,
+                        const float* shift, int silu, unsigned* ovf, void* stream);
+/* tcx_upsample2x with the output written as h2. */
+int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
+                      const float* shift, unsigned* ovf, void* stream);
+/* tcx_attention (MFMA kernel, N % 32 == 0) with the output written as h2. */
+int tcx_attention_h2(const float* qkv, void* out, int Bt, int N, int C, int heads, unsigned* ovf,
+                     void* stream);
+/* Conversions of n elements (n % 8 == 0, channel-fastest tensors with C % 8 == 0). */
+int tcx_f32_to_h2(const float* x, void* y, size_t n, unsigned* ovf, void* stream);
+int tcx_h2_to_f32(const void* x, float* y, size_t n, void* stream);
+
 /* Multi-head self-attention core of SelfAttention2d (sde_score_model.py:150-160):
  * qkv [Bt,N,3C] (1x1-conv output, channel order [q,k,v], head-major inside each),
  * out [Bt,N,C] = softmax(q k^T / sqrt(C/heads)) v. */
@@ -120,6 +157,8 @@ typedef struct tcx_conv {
     const float* w;  /* packed [cout_pad][kpad] */
     const float* b;  /* [cout] */
     int cin, cout, ks, kpad, cout_pad;
+    const void* wh;       /* h2 split of w (tcx_pack_conv_weight_h2), or NULL */
+    const float* wscale;  /* device float: inverse power-of-two scale of wh */
 } tcx_conv;
 
 /* Every pointer refers to device memory prepared by the host mirror of CondUNetTiny
@@ -140,6 +179,11 @@ typedef struct tcx_unet {
     /* GroupNorm affine, in forward order: down1 x2, down2 x2, mid x2, attn, up2 x2, up1 x2 */
     const float* gn_w[11];
     const float* gn_b[11];
+    /* 0: fp32 MFMA convs; 1: f16x3 split convs over h2 activations (needs base_ch % 32 == 0 and
+     * every conv's wh/wscale); h2_ovf: device word raised when an activation leaves the f16 range
+     * (the host re-runs the evaluation in fp32) */
+    int precision;
+    unsigned* h2_ovf;
 } tcx_unet;
 
 size_t tcx_unet_workspace_size(const tcx_unet* net, int Bt, int H, int W);

@@ -1,0 +1,219 @@
+"""GPU: the f16x3 split path (h2 storage, csrc/h2.hpp) through the C ABI.
+
+Every h2 conv is checked against the fp64 numpy oracle conv (oracle/nn_np.py) at the SAME gate
+as the fp32-MFMA conv in test_gpu_ops.py (2e-5 of the output scale), and its error is also
+required to stay within 2x the fp32-MFMA conv's error on the same inputs + 2e-7 of the scale
+(fp32-grade, not merely "within tolerance").  h2 writers are checked by decoding (hi + lo) against
+the fp32 value: |v - dec(v)| <= 2^-21 |v| + 2^-25 (f16 subnormal spacing / 2)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nn_np
+
+from test_gpu_ops import L, chk, close, dev, nchw, nhwc, pack, run_conv, rup, st
+
+pytestmark = pytest.mark.gpu
+
+rng = np.random.default_rng(7)
+
+
+def to_h2(t, ovf=None):
+    y = torch.empty_like(t)
+    chk(L().tcx_f32_to_h2(t.data_ptr(), y.data_ptr(), t.numel(), ovf.data_ptr() if ovf is not None else None, st()))
+    return y
+
+
+def from_h2(t):
+    y = torch.empty_like(t)
+    chk(L().tcx_h2_to_f32(t.data_ptr(), y.data_ptr(), t.numel(), st()))
+    return y
+
+
+def dec_ok(dec, v, fp32_ulps=0):
+    """fp32_ulps: allowance for a reference computed by a different fp32 kernel (FMA contraction)."""
+    bound = np.abs(v) * (2.0 ** -21 + fp32_ulps * 2.0 ** -23) + 2.0 ** -25
+    assert np.all(np.abs(dec - v) <= bound), float(np.max(np.abs(dec - v) - bound))
+
+
+def test_h2_roundtrip_and_range_flag():
+    v = np.concatenate([rng.standard_normal(4096) * 10.0 ** rng.uniform(-8, 4, 4096), [0.0, -0.0, 65503.0, -1e-30]])
+    v = np.resize(v, 4104).astype(np.float32)
+    t = dev(v)
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    d = from_h2(to_h2(t, ovf)).cpu().numpy()
+    dec_ok(d, v)
+    assert int(ovf.item()) == 0
+    big = t.clone()
+    big[5] = 70000.0
+    to_h2(big, ovf)
+    assert int(ovf.item()) == 1
+
+
+def pack_h2(w):
+    wpk, cpad, kpad = pack(w)
+    wh = torch.empty_like(wpk)
+    ws = torch.empty(4, device="cuda")
+    chk(L().tcx_pack_conv_weight_h2(wpk.data_ptr(), wh.data_ptr(), ws.data_ptr(), cpad, kpad, st()))
+    return wh, ws, cpad, kpad
+
+
+def run_conv_h2(x, w, b, stride, pad, circular, x2=None, act=0, resid=None, bmod=0, gn=False, Bt=None, out_h2=False):
+    B, C1, H, W = x.shape
+    C2 = 0 if x2 is None else x2.shape[1]
+    Bt = Bt or B
+    co, ci, ks, _ = w.shape
+    wh, ws, cpad, kpad = pack_h2(w)
+    Ho, Wo = (H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1
+    y = torch.empty((Bt, Ho, Wo, co), device="cuda")
+    xd = to_h2(dev(nhwc(x)))
+    x2d = to_h2(dev(nhwc(x2))) if x2 is not None else None
+    bd = dev(b) if b is not None else None
+    rd = dev(nhwc(resid)) if resid is not None else None
+    gnd = torch.zeros((Bt, -(-Ho * Wo // 128), co, 2), dtype=torch.float64, device="cuda") if gn else None
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    chk(L().tcx_conv2d_h2(xd.data_ptr(), x2d.data_ptr() if x2d is not None else None, Bt, bmod, H, W, C1, C2,
+                          wh.data_ptr(), ws.data_ptr(), bd.data_ptr() if bd is not None else None, None,
+                          rd.data_ptr() if rd is not None else None, y.data_ptr(), int(out_h2), co, cpad, kpad, ks,
+                          stride, pad, int(circular), act, gnd.data_ptr() if gnd is not None else None,
+                          ovf.data_ptr(), st()))
+    if out_h2:
+        y = from_h2(y)
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == 0
+    out = nchw(y.cpu().numpy())
+    return (out, gnd.cpu().numpy()) if gn else out
+
+
+def fp32_grade(got, fp32, ref):
+    scale = max(1.0, float(np.abs(ref).max()))
+    e_h2 = float(np.abs(got - ref).max())
+    e_32 = float(np.abs(fp32 - ref).max())
+    print(f"h2 err {e_h2 / scale:.2e}  fp32-mfma err {e_32 / scale:.2e} (of scale {scale:.2f})")
+    close(got, ref)
+    assert e_h2 <= 2.0 * e_32 + 2e-7 * scale
+
+
+@pytest.mark.parametrize("B,Ci,Co,H,ks,stride,circ", [
+    (2, 96, 96, 64, 3, 1, True), (3, 96, 192, 32, 3, 1, True), (2, 192, 192, 16, 3, 1, True),
+    (2, 96, 96, 64, 4, 2, True), (2, 192, 192, 32, 4, 2, True), (2, 192, 576, 16, 1, 1, True),
+    (2, 64, 40, 12, 3, 1, True),  # Cout not a multiple of 32, odd spatial size
+    (2, 32, 64, 16, 3, 1, False), (2, 64, 128, 16, 4, 2, False),  # zero padding
+])
+def test_conv_h2_vs_oracle(B, Ci, Co, H, ks, stride, circ):
+    x = rng.standard_normal((B, Ci, H, H))
+    w = rng.standard_normal((Co, Ci, ks, ks)) / np.sqrt(Ci * ks * ks)
+    b = rng.standard_normal(Co)
+    pad = 0 if ks == 1 else 1
+    ref = nn_np.conv2d(x, w, b, stride=stride, padding=pad, mode="circular" if circ else "zeros")
+    fp32_grade(run_conv_h2(x, w, b, stride, pad, circ), run_conv(x, w, b, stride, pad, circ), ref)
+
+
+def test_conv_h2_concat_out_h2_gn_stats():
+    """Two sources (the U-Net skip concat), h2 output, fused GroupNorm partials."""
+    x1 = rng.standard_normal((2, 96, 32, 32))
+    x2 = rng.standard_normal((2, 96, 32, 32)) * 3.0
+    w = rng.standard_normal((96, 192, 3, 3)) / 40
+    b = rng.standard_normal(96)
+    ref = nn_np.conv2d(np.concatenate([x1, x2], 1), w, b, padding=1, mode="circular")
+    got, part = run_conv_h2(x1, w, b, 1, 1, True, x2=x2, gn=True, out_h2=True)
+    fp32 = run_conv(x1, w, b, 1, 1, True, x2=x2)
+    fp32_grade(got, fp32, ref)
+    s = part.sum(axis=1)  # [B][C][2]
+    r = ref.reshape(2, 96, -1)
+    np.testing.assert_allclose(s[..., 0], r.sum(-1), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[..., 1], (r * r).sum(-1), rtol=1e-5, atol=1e-3)
+
+
+def test_conv_h2_bmod_resid_act():
+    """CFG batch aliasing (bmod), residual add and SiLU epilogue."""
+    x = rng.standard_normal((2, 64, 16, 16))
+    w = rng.standard_normal((64, 64, 3, 3)) / 24
+    b = rng.standard_normal(64)
+    resid = rng.standard_normal((4, 64, 16, 16))
+    xx = np.concatenate([x, x], 0)
+    ref = nn_np.conv2d(xx, w, b, padding=1, mode="circular") + resid
+    ref = ref / (1 + np.exp(-ref))
+    got = run_conv_h2(x, w, b, 1, 1, True, resid=resid, bmod=2, Bt=4, act=3)
+    fp32 = run_conv(x, w, b, 1, 1, True, resid=resid, bmod=2, Bt=4, act=3)
+    fp32_grade(got, fp32, ref)
+
+
+def test_weight_scale_extremes():
+    """Tiny and large weights: the power-of-two scale keeps lo halves normal either way."""
+    x = rng.standard_normal((1, 32, 16, 16))
+    for mag in (1e-7, 1e3):
+        w = rng.standard_normal((32, 32, 3, 3)) * mag
+        ref = nn_np.conv2d(x, w, None, padding=1, mode="circular")
+        got = run_conv_h2(x, w, None, 1, 1, True)
+        assert float(np.abs(got - ref).max()) <= 2e-6 * float(np.abs(ref).max())
+
+
+@pytest.mark.parametrize("inplace", [True, False])
+def test_gn_apply_h2(inplace):
+    B, HW, C = 2, 256, 96
+    x = rng.standard_normal((B, HW, C)).astype(np.float32)
+    sc = dev(rng.standard_normal((B, C)))
+    sh = dev(rng.standard_normal((B, C)))
+    t = dev(x)
+    out = t if inplace else torch.empty_like(t)
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    chk(L().tcx_gn_apply_tab_h2(t.data_ptr(), out.data_ptr(), B, HW, C, sc.data_ptr(), sh.data_ptr(), 1,
+                                ovf.data_ptr(), st()))
+    got = from_h2(out).cpu().numpy()
+    ref32 = torch.empty_like(t)
+    chk(L().tcx_gn_apply_tab(dev(x).data_ptr(), ref32.data_ptr(), B, HW, C, sc.data_ptr(), sh.data_ptr(), 1, st()))
+    r = ref32.cpu().numpy()
+    bad = np.argwhere(np.abs(got - r) > np.abs(r) * 2.0 ** -21 + 2.0 ** -25)
+    if len(bad):
+        print("mismatches", len(bad), bad[:8].tolist(), got[tuple(bad[0])], r[tuple(bad[0])])
+    dec_ok(got, r)
+    assert int(ovf.item()) == 0
+
+
+def test_upsample_h2():
+    B, H, W, C = 2, 8, 8, 96
+    x = dev(rng.standard_normal((B, H, W, C)))
+    y = torch.empty((B, 2 * H, 2 * W, C), device="cuda")
+    y32 = torch.empty_like(y)
+    chk(L().tcx_upsample2x_h2(x.data_ptr(), y.data_ptr(), B, H, W, C, None, None, None, st()))
+    chk(L().tcx_upsample2x(x.data_ptr(), y32.data_ptr(), B, H, W, C, None, None, st()))
+    dec_ok(from_h2(y).cpu().numpy(), y32.cpu().numpy(), fp32_ulps=2)
+
+
+def test_attention_h2():
+    Bt, N, C, heads = 2, 256, 192, 4
+    qkv = dev(rng.standard_normal((Bt, N, 3 * C)))
+    o = torch.empty((Bt, N, C), device="cuda")
+    o32 = torch.empty_like(o)
+    chk(L().tcx_attention_h2(qkv.data_ptr(), o.data_ptr(), Bt, N, C, heads, None, st()))
+    chk(L().tcx_attention(qkv.data_ptr(), o32.data_ptr(), Bt, N, C, heads, st()))
+    dec_ok(from_h2(o).cpu().numpy(), o32.cpu().numpy())
+
+
+def test_unet_range_fallback_to_fp32():
+    """An activation beyond the f16 range raises the flag and the evaluator recomputes in fp32."""
+    import warnings
+
+    from toycrystals_amd.models.sde_score_model import CondUNetTiny
+    torch.manual_seed(0)
+    m = CondUNetTiny(4, 4, 32).cuda().eval()
+    with torch.no_grad():
+        m.ds1.weight.mul_(1e5)  # ds1 output (written as h2, consumed by down2) far beyond 65504
+    x = torch.randn(2, 1, 64, 64, device="cuda")
+    t = torch.full((2,), 0.3, device="cuda")
+    yc = torch.tensor([0, 1], device="cuda")
+    yv = torch.zeros(2, 4, device="cuda")
+    with warnings.catch_warnings(record=True) as rec, torch.no_grad():
+        warnings.simplefilter("always")
+        e = m(x, t, yc, yv)
+    assert any("f16 range" in str(r.message) for r in rec)
+    from toycrystals_amd import _lib
+    old = _lib.conv_precision()
+    _lib.set_conv_precision("fp32")
+    try:
+        with torch.no_grad():
+            e32 = m(x, t, yc, yv)
+    finally:
+        _lib.set_conv_precision(old)
+    assert torch.equal(e, e32)

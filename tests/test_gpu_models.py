@@ -34,6 +34,17 @@ def unet(base, sd=None):
     return m.cuda().eval()
 
 
+@pytest.fixture(params=["f16x3", "fp32"])
+def prec(request):
+    """Run the score-U-Net evaluator with each conv precision (the split f16x3 path applies at
+    base_ch % 32 == 0; other nets fall back to fp32 inside either setting)."""
+    from toycrystals_amd import _lib
+    old = _lib.conv_precision()
+    _lib.set_conv_precision(request.param)
+    yield request.param
+    _lib.set_conv_precision(old)
+
+
 def rel_err(a, ref):
     return float(np.abs(a - ref).max()) / max(1.0, float(np.abs(ref).max()))
 
@@ -41,7 +52,7 @@ def rel_err(a, ref):
 @pytest.mark.parametrize("name,base,stored", [("unet16_b3", 16, True), ("unet96_b2", 96, False),
                                               ("unet32_b2_h32", 32, False)])
 @pytest.mark.parametrize("grad", [False, True], ids=["fused", "autograd"])
-def test_unet_forward_vs_reference(golden, name, base, stored, grad):
+def test_unet_forward_vs_reference(golden, name, base, stored, grad, prec):
     """The fused evaluator (no grad) and the autograd training chain (grad) against the reference."""
     g = golden(name)
     sd = {k[2:]: v for k, v in g.items() if k.startswith("w/")} if stored else None
@@ -65,7 +76,7 @@ def test_predict_eps_cfg_vs_reference(golden):
     assert rel_err(e0, g["eps0"]) < 2e-5
 
 
-def test_batch_independence_and_oracle_at_full_size():
+def test_batch_independence_and_oracle_at_full_size(prec):
     """B=128 (the metric's batch) with CFG doubling to 256: every sample equals the same sample
     evaluated alone, and a random subset matches the fp64 oracle."""
     from oracle.score_model import ScoreUNet, predict_eps_cfg as o_cfg
@@ -88,7 +99,7 @@ def test_batch_independence_and_oracle_at_full_size():
 
 
 @pytest.mark.parametrize("name", ["sde16_3step", "sde96_2step_b2"])
-def test_sde_sampler_vs_reference(golden, name):
+def test_sde_sampler_vs_reference(golden, name, prec):
     from toycrystals_amd.models.sde_score_model import VPSDE, sample_reverse_sde_euler_maruyama
     g = golden(name)
     m = unet(int(g["base_ch"]))
@@ -109,7 +120,7 @@ def test_ode_sampler_vs_reference(golden):
     assert np.abs(out - g["out"]).max() < 1e-4
 
 
-def test_trained_ode20_vs_reference(golden):
+def test_trained_ode20_vs_reference(golden, prec):
     from toycrystals_amd.models.sde_score_model import VPSDE, sample_probability_flow_ode
     g = golden("ode32_trained_20")
     m = unet(32, golden("trained32_state"))
@@ -121,7 +132,7 @@ def test_trained_ode20_vs_reference(golden):
     assert np.abs(out - g["out"]).max() < 1e-4
 
 
-def test_trained_sde300_vs_reference(golden):
+def test_trained_sde300_vs_reference(golden, prec):
     """The metric's sampler (300-step reverse SDE, CFG 1.5, t_end 0.005) end to end, with the
     reference's noise regenerated from its seed in the reference's draw order."""
     from toycrystals_amd.models.sde_score_model import VPSDE, host_noise, sample_reverse_sde_euler_maruyama
@@ -134,7 +145,7 @@ def test_trained_sde300_vs_reference(golden):
                                             n_steps=int(g["steps"]), guidance_scale=float(g["cfg"]),
                                             t_end=float(g["t_end"]), noise=noise.cuda()).cpu().numpy()
     err = float(np.abs(out - g["out"]).max())
-    print(f"300-step SDE clamped max-abs err {err:.3e}")
+    print(f"300-step SDE ({prec}) clamped max-abs err {err:.3e}")
     assert err < 1e-4
 
 

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-layer micro-benchmark of libtcx's implicit-GEMM conv at the U-Net's shapes (Bt=256).
-Prints µs and algorithmic TFLOP/s per layer (HIP events, median of N reps)."""
+Prints µs and algorithmic TFLOP/s per layer (HIP events, median of N reps).
+H2=1: the f16x3 split conv (tcx_conv2d_h2) over h2 operands instead of the fp32-MFMA conv."""
 import ctypes, os, sys, statistics
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "vae-diffusion-toy-crystals_amd"))
@@ -42,7 +43,25 @@ def bench(name, H, C1, C2, Co, ks, s, pad, ups, reps=20, gn=True):
     tabs = [torch.rand(Bt, C1, device="cuda") + 0.5, torch.randn(Bt, C1, device="cuda")] if use_pro else []
     pro = [t.data_ptr() for t in tabs] + [None, None] if use_pro else [None] * 4
     g = torch.empty(Bt, max(1, Ho * Ho // 128), Co, 2, dtype=torch.float64, device="cuda") if use_gn else None
-    def run():
+    if H2:
+        if ups or C1 % 32:
+            return None
+        def h2(t):
+            o = torch.empty_like(t)
+            check(L.tcx_f32_to_h2(t.data_ptr(), o.data_ptr(), t.numel(), None, st))
+            return o
+        x1 = h2(x1)
+        x2 = h2(x2) if x2 is not None else None
+        wh = torch.empty_like(wpk)
+        ws = torch.empty(4, device="cuda")
+        check(L.tcx_pack_conv_weight_h2(wpk.data_ptr(), wh.data_ptr(), ws.data_ptr(), cpad, kpad, st))
+
+        def run():
+            check(L.tcx_conv2d_h2(x1.data_ptr(), x2.data_ptr() if x2 is not None else None, Bt, 0, H, H, C1, C2,
+                                  wh.data_ptr(), ws.data_ptr(), b.data_ptr(), None, None, y.data_ptr(), 0, Co, cpad,
+                                  kpad, ks, s, pad, 1, 0, g.data_ptr() if g is not None else None, None, st))
+    else:
+      def run():
         check(L.tcx_conv2d(x1.data_ptr(), x2.data_ptr() if x2 is not None else None, Bt, 0, H, H, C1, C2,
                            wpk.data_ptr(), b.data_ptr(), None, None, y.data_ptr(), Co, cpad, kpad, ks, s, pad, 1,
                            ups, 0, g.data_ptr() if g is not None else None, *pro, st))
@@ -59,13 +78,17 @@ def bench(name, H, C1, C2, Co, ks, s, pad, ups, reps=20, gn=True):
     return us, fl
 
 
+H2 = os.environ.get("H2", "0") == "1"
 only = os.environ.get("LAYER")
 reps = int(os.environ.get("REPS", "20"))
 tot_us = tot_fl = 0
 for l in LAYERS:
     if only and l[0] != only:
         continue
-    us, fl = bench(*l, reps=reps)
+    r = bench(*l, reps=reps)
+    if r is None:
+        continue
+    us, fl = r
     if l[0] not in ("us2(pre)",):
         tot_us += us; tot_fl += fl
 print(f"TOTAL {tot_us:.1f} us  {tot_fl / tot_us / 1e6:.1f} TF (mid counted once)")

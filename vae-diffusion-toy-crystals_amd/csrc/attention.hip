@@ -5,6 +5,7 @@
 // row max / sum and the output by two xor-shuffles.  The q,k,v channel split and the head-major
 // channel order (view [B,heads,d,N] -> transpose) are folded into the addressing.
 #include "common.hpp"
+#include "h2.hpp"
 
 namespace tcx {
 namespace {
@@ -23,7 +24,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // ---------------------------------------------------------------------------------------------
 template <int D>
 __global__ __launch_bounds__(512) void k_attention_mfma(const float* __restrict__ qkv, float* __restrict__ out, int N,
-                                                        int C, float scale) {
+                                                        int C, float scale, int out_h2, unsigned* ovf) {
     constexpr int HD = D / 2;           // d per lane half
     constexpr int KS = D + 4;           // K row stride in LDS ((D+4)/4 odd: conflict-free b128)
     constexpr int DT = (D + 31) / 32;   // 32-row tiles of O^T
@@ -118,6 +119,23 @@ __global__ __launch_bounds__(512) void k_attention_mfma(const float* __restrict_
             }
         }
     const float inv = 1.f / l;
+    if (out_h2) {  // h2 split record of the query's pixel (h2.hpp): 4 consecutive d per register quad
+        bool bad = false;
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = t * 32 + 8 * i + 4 * lh;
+                if (d < D) {
+                    const float4 v = make_float4(oacc[t][4 * i] * inv, oacc[t][4 * i + 1] * inv, oacc[t][4 * i + 2] * inv,
+                                                 oacc[t][4 * i + 3] * inv);
+                    store4_h2(reinterpret_cast<char*>(out), ((size_t)b * N + q) * C * 4, (h * D + d) >> 2, v);
+                    bad = bad || h2_bad(v.x) || h2_bad(v.y) || h2_bad(v.z) || h2_bad(v.w);
+                }
+            }
+        h2_flag(ovf, bad);
+        return;
+    }
     float* dst = out + ((size_t)b * N + q) * C + h * D;
 #pragma unroll
     for (int t = 0; t < DT; ++t)
@@ -129,7 +147,8 @@ __global__ __launch_bounds__(512) void k_attention_mfma(const float* __restrict_
 }
 
 template <int D>
-int launch_attn_mfma(const float* qkv, float* out, int Bt, int N, int C, int heads, hipStream_t st) {
+int launch_attn_mfma(const float* qkv, float* out, int Bt, int N, int C, int heads, hipStream_t st, int out_h2 = 0,
+                     unsigned* ovf = nullptr) {
     const float scale = (float)(1.0 / std::sqrt((double)D));
     constexpr int KS = D + 4, VS = ((D + 31) / 32) * 32;
     const size_t shm = (size_t)N * (KS + VS) * sizeof(float);
@@ -142,7 +161,7 @@ int launch_attn_mfma(const float* qkv, float* out, int Bt, int N, int C, int hea
         }
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_attention_mfma<D>), dim3(heads, Bt), dim3(2 * N), shm, st, qkv, out, N, C, scale);
+    hipLaunchKernelGGL((k_attention_mfma<D>), dim3(heads, Bt), dim3(2 * N), shm, st, qkv, out, N, C, scale, out_h2, ovf);
     return check_launch("tcx_attention(mfma)");
 }
 
@@ -294,5 +313,24 @@ extern "C" int tcx_attention(const float* qkv, float* out, int Bt, int N, int C,
         case 48: return launch_attn<48>(qkv, out, Bt, N, C, heads, st);
         case 64: return launch_attn<64>(qkv, out, Bt, N, C, heads, st);
         default: set_error("tcx_attention: head dim %d unsupported", D); return TCX_EUNSUP;
+    }
+}
+
+extern "C" int tcx_attention_h2(const float* qkv, void* out, int Bt, int N, int C, int heads, unsigned* ovf,
+                                void* stream) {
+    TCX_REQUIRE(qkv && out && heads > 0 && C % heads == 0 && C % 8 == 0, "tcx_attention_h2: bad args");
+    TCX_REQUIRE(N > 0 && N <= 256 && N % 32 == 0, "tcx_attention_h2: needs N %% 32 == 0, N <= 256 (MFMA kernel)");
+    TCX_REQUIRE(aligned16(qkv) && aligned16(out), "tcx_attention_h2: pointers must be 16-B aligned");
+    if (Bt == 0) return TCX_OK;
+    float* o = (float*)out;
+    hipStream_t st = (hipStream_t)stream;
+    switch (C / heads) {
+        case 8: return launch_attn_mfma<8>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+        case 16: return launch_attn_mfma<16>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+        case 24: return launch_attn_mfma<24>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+        case 32: return launch_attn_mfma<32>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+        case 48: return launch_attn_mfma<48>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+        case 64: return launch_attn_mfma<64>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+        default: set_error("tcx_attention_h2: head dim %d unsupported", C / heads); return TCX_EUNSUP;
     }
 }

@@ -18,6 +18,7 @@
 // the A load, bias / per-batch bias / residual / activation epilogue, and GroupNorm partial
 // statistics of the output (fp64) for the following GroupNorm.
 #include "common.hpp"
+#include "h2.hpp"
 
 namespace tcx {
 namespace {
@@ -56,6 +57,11 @@ struct ConvParams {
     // when the staged chunk is written to LDS (tables from tcx_gn_finalize; null = raw source)
     const float *sc1, *sh1, *sc2, *sh2;
     unsigned bytes1, bytes2, bytesw;  // buffer extents for the MODE 3 raw-buffer loads
+    // f16x3 path (SPL): sources and weights in the h2 split format (h2.hpp), *wscale = 2^-e
+    // undoes the weights' power-of-two scale; out_h2 writes the output in h2 (ovf: range flag)
+    const float* wscale;
+    int out_h2;
+    unsigned* ovf;
 };
 
 constexpr int PRO_MAXC = 384;  // max channels per source for the fused GN prologue
@@ -99,8 +105,12 @@ __device__ __forceinline__ void bilin_axis(int d, int n, int& i0, int& i1, float
 //         the U-Net).  The byte offset of each (tap, tile pixel) is built once per workgroup in
 //         an LDS table; per chunk a thread reads its 4 pixels' offsets with one ds_read_b128 and
 //         the channel offset rides in the scalar soffset — no per-chunk im2col VALU.
-template <int NT, int MODE, bool CIRC, bool PRO>
+// SPL: the f16x3 split path (h2.hpp): MODE 3 staging unchanged (4 bytes per element either
+//      way); per 32-deep chunk two k16 steps, lane half h of step s owns the 8-channel group
+//      2s + h = one hi and one lo b128 read per operand; 3 MFMA 32x32x16 f16 per accumulator.
+template <int NT, int MODE, bool CIRC, bool PRO, bool SPL = false>
 __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
+    static_assert(!SPL || (MODE == 3 && !PRO), "split path: MODE 3 staging only, no prologue");
     constexpr int BN = 32 * NT;
     __shared__ __attribute__((aligned(16))) float As[2][BM * LDA];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDA];
@@ -371,6 +381,49 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
         for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[n].w, acc[n], 0, 0, 0);
     };
 
+    if constexpr (SPL) {
+        // fragments of both k16 steps of the chunk being computed (hi, lo per operand)
+        h8 ah0, al0, ah1, al1, bh0[NT], bl0[NT], bh1[NT], bl1[NT];
+        auto rd = [&](int buf, int s, h8& ah, h8& al, h8 (&bh)[NT], h8 (&bl)[NT]) {
+            const float* Ab = &As[buf][(wv * 32 + li) * LDA + (2 * s + lh) * 8];
+            ah = __builtin_bit_cast(h8, ld4(Ab));
+            al = __builtin_bit_cast(h8, ld4(Ab + 4));
+            const float* Bb = &Bs[buf][li * LDA + (2 * s + lh) * 8];
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                bh[n] = __builtin_bit_cast(h8, ld4(Bb + n * 32 * LDA));
+                bl[n] = __builtin_bit_cast(h8, ld4(Bb + n * 32 * LDA + 4));
+            }
+        };
+        auto mf = [&](const h8& ah, const h8& al, const h8 (&bh)[NT], const h8 (&bl)[NT]) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[n], acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[n], acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[n], acc[n], 0, 0, 0);
+        };
+        rd(0, 0, ah0, al0, bh0, bl0);
+        for (int c = 0; c < p.nchunks; ++c) {
+            const int cur = c & 1;
+            const int cn = c + 1 < p.nchunks ? c + 1 : c;
+            const Dec d = decode(cn);
+            read_poff(d);
+            rd(cur, 1, ah1, al1, bh1, bl1);
+            load_a(d, cn, 0);
+            load_a(d, cn, 1);
+            load_a(d, cn, 2);
+            load_a(d, cn, 3);
+            load_b(cn);
+            __builtin_amdgcn_sched_barrier(0);
+            mf(ah0, al0, bh0, bl0);
+            __builtin_amdgcn_sched_barrier(0);
+            mf(ah1, al1, bh1, bl1);
+            store_chunk(cur ^ 1);
+            __syncthreads();
+            rd(cur ^ 1, 0, ah0, al0, bh0, bl0);
+        }
+    } else {
     Dec dc = decode(0);  // decode of the chunk being computed
     read_frags(0, 0, dc, fa0, fb0);
     for (int c = 0; c < p.nchunks; ++c) {
@@ -404,6 +457,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
         dc = d;
         read_frags(cur ^ 1, 0, dc, fa0, fb0);
     }
+    }  // !SPL
 
     // ---- epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
     const bool gn = p.gn != nullptr;
@@ -444,18 +498,36 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
             for (int r = 0; r < 16; ++r) add[r] += p.resid[oidx[r]];
         }
         double s = 0.0, ss = 0.0;
+        const float wsc = SPL ? *p.wscale : 1.f;
+        bool bad = false;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            float v = acc[n][r] + add[r];
+            float v = (SPL ? acc[n][r] * wsc : acc[n][r]) + add[r];
             if (p.act == 1) v = fmaxf(v, 0.f);
             else if (p.act == 2) v = 1.f / (1.f + expf(-v));
             else if (p.act == 3) v = silu_f(v);
-            if (ok[r]) {
+            if (p.out_h2) {
+                // h2 record of the pixel: lane pairs (2j, 2j+1) of an 8-channel group swap halves so
+                // the even lane stores the hi pair and the odd lane the lo pair (one dword each)
+                const unsigned sp = split1(v);
+                const bool odd = (li & 1) != 0;
+                const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
+                const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
+                const size_t pe = oidx[r] - (size_t)coc;  // pixel's first element
+                const int c8 = coc & ~7, j = (coc & 7) & ~1;
+                if (ok[r]) {
+                    *reinterpret_cast<unsigned*>(reinterpret_cast<char*>(p.y) + pe * 4 + (size_t)c8 * 4 + (odd ? 16 : 0) + 2 * j) = word;
+                    bad = bad || h2_bad(v);
+                }
+            } else if (ok[r]) {
                 p.y[oidx[r]] = v;
+            }
+            if (ok[r]) {
                 s += (double)v;
                 ss += (double)v * (double)v;
             }
         }
+        h2_flag(p.ovf, bad);
         if (gn) {
             s += __shfl_xor(s, 32);
             ss += __shfl_xor(ss, 32);
@@ -495,6 +567,11 @@ int launch_nt(const ConvParams& p, int mode, hipStream_t st) {
                      p.ks * p.ks <= MAXTAP && p.kpad == p.ks * p.ks * p.Cin && p.Hi == p.H && p.Wi == p.W &&
                      p.bytes1 && (p.C2 == 0 || p.bytes2) && p.bytesw;
     const bool pro = p.sc1 || p.sc2;
+    if (p.wscale) {  // f16x3 split path, validated by the caller: uni
+        if (p.circular) hipLaunchKernelGGL((k_conv<NT, 3, true, false, true>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((k_conv<NT, 3, false, false, true>), grid, block, 0, st, p);
+        return check_launch("tcx_conv2d_h2");
+    }
     if (pro) {  // validated by the caller: uni && circular
         hipLaunchKernelGGL((k_conv<NT, 3, true, true>), grid, block, 0, st, p);
     } else if (p.circular) {
@@ -584,10 +661,90 @@ __global__ void k_pack_conv_dgrad(const float* __restrict__ w, float* __restrict
     }
 }
 
+// fp32 packed weight [cout_pad][kpad] -> h2 split [cout_pad][kpad/8][2][8] f16 of w * 2^e, with
+// e chosen from max|w| so the largest scaled weight lies in [2^13, 2^14) (lo halves normal);
+// *wscale = 2^-e.  One workgroup: max-reduce, then split.
+__global__ __launch_bounds__(1024) void k_pack_h2(const float* __restrict__ wpk, char* __restrict__ wh,
+                                                  float* __restrict__ wscale, size_t n) {
+    __shared__ float red[16];
+    const int tid = threadIdx.x;
+    float m = 0.f;
+    for (size_t i = tid; i < n; i += 1024) m = fmaxf(m, fabsf(wpk[i]));
+    for (int off = 32; off; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) {
+        float mx = 0.f;
+        for (int w = 0; w < 16; ++w) mx = fmaxf(mx, red[w]);
+        int k = 0;
+        if (mx > 0.f && mx < INFINITY) (void)frexpf(mx, &k);  // mx < 2^k
+        int e = 14 - k;
+        e = e < -100 ? -100 : (e > 100 ? 100 : e);
+        red[0] = ldexpf(1.f, e);
+        wscale[0] = ldexpf(1.f, -e);
+    }
+    __syncthreads();
+    const float sc = red[0];
+    for (size_t g = tid; g < n / 4; g += 1024) {
+        float4 v = reinterpret_cast<const float4*>(wpk)[g];
+        v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+        store4_h2(wh, (g >> 1) * 32, (int)(g & 1), v);
+    }
+}
+
 }  // namespace
 }  // namespace tcx
 
 using namespace tcx;
+
+extern "C" int tcx_pack_conv_weight_h2(const float* wpk, void* wh, float* wscale, int cout_pad, int kpad,
+                                       void* stream) {
+    TCX_REQUIRE(wpk && wh && wscale && cout_pad > 0 && kpad > 0 && kpad % BK == 0 && aligned16(wpk) && aligned16(wh),
+                "tcx_pack_conv_weight_h2: bad args");
+    hipLaunchKernelGGL(k_pack_h2, dim3(1), dim3(1024), 0, (hipStream_t)stream, wpk, (char*)wh, wscale,
+                       (size_t)cout_pad * kpad);
+    return check_launch("tcx_pack_conv_weight_h2");
+}
+
+extern "C" int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
+                             const void* wh, const float* wscale, const float* bias, const float* bias_b,
+                             const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
+                             int stride, int pad, int circular, int act, double* gn_stats, unsigned* ovf,
+                             void* stream) {
+    TCX_REQUIRE(x1 && wh && wscale && y, "tcx_conv2d_h2: null pointer");
+    TCX_REQUIRE(Bt >= 0 && H > 0 && W > 0 && C1 > 0 && C2 >= 0 && Cout > 0, "tcx_conv2d_h2: bad shape");
+    TCX_REQUIRE((C2 == 0) == (x2 == nullptr), "tcx_conv2d_h2: x2/C2 mismatch");
+    TCX_REQUIRE(cout_pad >= Cout && cout_pad % 32 == 0, "tcx_conv2d_h2: cout_pad must be a multiple of 32 >= Cout");
+    TCX_REQUIRE(act >= 0 && act <= 3 && ks >= 1 && stride >= 1 && pad >= 0, "tcx_conv2d_h2: bad geometry/act");
+    const int Cin = C1 + C2;
+    TCX_REQUIRE(C1 % BK == 0 && (C2 == 0 || C2 == C1) && ks * ks <= MAXTAP && kpad == ks * ks * Cin,
+                "tcx_conv2d_h2: needs C1 %% 32 == 0, C2 in {0, C1}, ks*ks <= 16 and kpad == ks*ks*Cin");
+    TCX_REQUIRE(!out_h2 || Cout % 8 == 0, "tcx_conv2d_h2: h2 output needs Cout %% 8 == 0");
+    TCX_REQUIRE(aligned16(x1) && (!x2 || aligned16(x2)) && aligned16(wh) && aligned16(y),
+                "tcx_conv2d_h2: pointers must be 16-B aligned");
+    ConvParams p{};
+    p.x1 = (const float*)x1; p.x2 = (const float*)x2; p.C1 = C1; p.C2 = C2; p.Cin = Cin;
+    p.bmod = bmod; p.H = H; p.W = W; p.Hi = H; p.Wi = W;
+    p.Ho = (H + 2 * pad - ks) / stride + 1;
+    p.Wo = (W + 2 * pad - ks) / stride + 1;
+    TCX_REQUIRE(p.Ho > 0 && p.Wo > 0, "tcx_conv2d_h2: empty output");
+    p.HoWo = p.Ho * p.Wo;
+    p.M = Bt * p.HoWo;
+    p.w = (const float*)wh; p.bias = bias; p.bias_b = bias_b; p.resid = resid; p.y = (float*)y;
+    p.Cout = Cout; p.kpad = kpad; p.nchunks = kpad / BK;
+    p.ks = ks; p.stride = stride; p.pad_y = pad; p.pad_x = pad; p.circular = circular;
+    p.Hy = p.Ho; p.Wy = p.Wo; p.osy = 1; p.ooy = 0; p.osx = 1; p.oox = 0; p.act = act;
+    p.gn = gn_stats;
+    p.nsplit = cdiv(p.HoWo, BM);
+    if (gn_stats) TCX_REQUIRE(p.HoWo % BM == 0, "tcx_conv2d_h2: fused GN stats need Ho*Wo %% 128 == 0");
+    const size_t bsrc = bmod > 0 ? (size_t)bmod : (size_t)Bt;
+    const size_t lim = (size_t)1 << 31;
+    const size_t b1 = bsrc * H * W * C1 * 4, b2 = bsrc * H * W * C2 * 4, bw = (size_t)cout_pad * kpad * 4;
+    TCX_REQUIRE(b1 < lim && b2 < lim && bw < lim, "tcx_conv2d_h2: operands must be < 2 GiB (32-bit buffer offsets)");
+    p.bytes1 = (unsigned)b1; p.bytes2 = (unsigned)b2; p.bytesw = (unsigned)bw;
+    p.wscale = wscale; p.out_h2 = out_h2; p.ovf = ovf;
+    return launch_conv(p, cout_pad, 0, (hipStream_t)stream);
+}
 
 extern "C" int tcx_conv2d(const float* x1, const float* x2, int Bt, int bmod, int H, int W, int C1, int C2,
                           const float* wpk, const float* bias, const float* bias_b, const float* resid,

@@ -1,0 +1,72 @@
+// "h2" split-f16 storage of an fp32 tensor, the operand format of the f16x3 conv path.
+//
+// A tensor [..][C] (C % 8 == 0) is stored as [..][C/8][2][8] f16: for every 8-channel group,
+// 8 "hi" halves then 8 "lo" halves, hi = f16(v), lo = f16(v - hi) (both round-to-nearest-even).
+// Four bytes per element, so every byte offset of the fp32 layout that is a multiple of 32
+// (a pixel, an 8-channel group) is unchanged and the im2col gather of the conv is the same code.
+// hi + lo carries 22 significant bits (f16 subnormals are kept by the gfx950 converts and MFMA,
+// measured: tools/probe/mfma_f16_probe.hip), and a product a*b is formed on MFMA as
+// hi_a*hi_b + hi_a*lo_b + lo_a*hi_b (three v_mfma_f32_32x32x16_f16, f32 accumulate): the dropped
+// lo*lo term and the split residuals are below 2^-21 relative, within the fp32 rounding of the
+// K-long accumulation.  Weights are scaled by an exact power of two before the
+// split so that their lo halves stay normal; the epilogue multiplies by the inverse.
+// Range: |v| must stay below 65504 (f16 max); writers raise a flag word otherwise (the host
+// re-runs in fp32: toycrystals_amd/models/sde_score_model.py).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace tcx {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+constexpr float kH2Max = 65504.f;
+
+__device__ __forceinline__ unsigned short f16_bits(_Float16 h) { return __builtin_bit_cast(unsigned short, h); }
+
+// split one value: returns (lo << 16) | hi
+__device__ __forceinline__ unsigned split1(float v) {
+    const _Float16 h = (_Float16)v;
+    const _Float16 l = (_Float16)(v - (float)h);
+    return (unsigned)f16_bits(h) | ((unsigned)f16_bits(l) << 16);
+}
+
+// 4 consecutive channels -> 4 hi halves (uint2) and 4 lo halves (uint2)
+__device__ __forceinline__ void split4(const float4 v, uint2& hi, uint2& lo) {
+    const unsigned a = split1(v.x), b = split1(v.y), c = split1(v.z), d = split1(v.w);
+    hi.x = (a & 0xffffu) | (b << 16);
+    hi.y = (c & 0xffffu) | (d << 16);
+    lo.x = (a >> 16) | (b & 0xffff0000u);
+    lo.y = (c >> 16) | (d & 0xffff0000u);
+}
+
+__device__ __forceinline__ bool h2_bad(float v) { return !(fabsf(v) < kH2Max); }
+
+// Store channels [4q, 4q+4) of one pixel whose h2 record starts at byte `pix` (= pixel * C * 4).
+__device__ __forceinline__ void store4_h2(char* base, size_t pix, int q, const float4 v) {
+    uint2 hi, lo;
+    split4(v, hi, lo);
+    char* g = base + pix + 32 * (size_t)(q >> 1) + 8 * (q & 1);
+    *reinterpret_cast<uint2*>(g) = hi;
+    *reinterpret_cast<uint2*>(g + 16) = lo;
+}
+
+// Raise the overflow flag (rare: a plain per-lane atomic on the taken branch only).
+__device__ __forceinline__ void h2_flag(unsigned* ovf, bool bad) {
+    if (bad && ovf) atomicOr(ovf, 1u);
+}
+
+// Decode 4 channels [4q, 4q+4) of one pixel record (tests / conversions).
+__device__ __forceinline__ float4 load4_h2(const char* base, size_t pix, int q) {
+    const char* g = base + pix + 32 * (size_t)(q >> 1) + 8 * (q & 1);
+    const uint2 hi = *reinterpret_cast<const uint2*>(g);
+    const uint2 lo = *reinterpret_cast<const uint2*>(g + 16);
+    auto f = [](unsigned h, unsigned l) {
+        return (float)__builtin_bit_cast(_Float16, (unsigned short)h) + (float)__builtin_bit_cast(_Float16, (unsigned short)l);
+    };
+    return make_float4(f(hi.x & 0xffffu, lo.x & 0xffffu), f(hi.x >> 16, lo.x >> 16), f(hi.y & 0xffffu, lo.y & 0xffffu),
+                       f(hi.y >> 16, lo.y >> 16));
+}
+
+}  // namespace tcx

@@ -6,6 +6,7 @@
 // (tcx_conv2d gn_stats): partial {sum, sumsq} per (batch, split, channel) in fp64, then an
 // apply pass that folds mean/rstd/gamma/beta into one per-channel scale/shift and fuses SiLU.
 #include "common.hpp"
+#include "h2.hpp"
 
 namespace tcx {
 namespace {
@@ -157,9 +158,11 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const double* __restrict__ 
     }
 }
 
+template <bool OUTH2>
 __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ x, float* __restrict__ y, int Bt, int H,
                                                     int W, int C, const float* __restrict__ tsc,
-                                                    const float* __restrict__ tsh) {
+                                                    const float* __restrict__ tsh, unsigned* ovf) {
+    bool bad = false;
     const int C4 = C / 4;
     const size_t n = (size_t)Bt * 4 * H * W * C4;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -196,8 +199,14 @@ __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ x,
         o.y = ly0 * (lx0 * a.y + lx1 * bq.y) + ly1 * (lx0 * c.y + lx1 * d.y);
         o.z = ly0 * (lx0 * a.z + lx1 * bq.z) + ly1 * (lx0 * c.z + lx1 * d.z);
         o.w = ly0 * (lx0 * a.w + lx1 * bq.w) + ly1 * (lx0 * c.w + lx1 * d.w);
-        *reinterpret_cast<float4*>(y + i * 4) = o;
+        if constexpr (OUTH2) {
+            store4_h2(reinterpret_cast<char*>(y), (i / C4) * (size_t)C * 4, c4, o);
+            bad = bad || h2_bad(o.x) || h2_bad(o.y) || h2_bad(o.z) || h2_bad(o.w);
+        } else {
+            *reinterpret_cast<float4*>(y + i * 4) = o;
+        }
     }
+    h2_flag(ovf, bad);
 }
 
 // LayerNorm over rows of width Wd (+ optional FiLM h*(1+gamma)+beta), one wave per row.
@@ -235,6 +244,67 @@ __global__ __launch_bounds__(256) void k_layernorm_film(const float* __restrict_
         }
         yr[i] = h;
     }
+}
+
+// GroupNorm apply from tables with the output in the h2 split format (h2.hpp): one thread per
+// (pixel, 8-channel group) reads 32 B and writes the same 32 B (hi[8], lo[8]), so x == y is safe.
+__global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y, int HW, int C,
+                                                         const float* __restrict__ tsc, const float* __restrict__ tsh,
+                                                         int silu, int ppb, unsigned* ovf) {
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    float* sc = lsm;
+    float* sh = lsm + ((C + 3) & ~3);
+    const int b = blockIdx.y;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        sc[c] = tsc[(size_t)b * C + c];
+        sh[c] = tsh[(size_t)b * C + c];
+    }
+    __syncthreads();
+    const int p0 = blockIdx.x * ppb;
+    const int p1 = min(HW, p0 + ppb);
+    const size_t base = ((size_t)b * HW + p0) * C;
+    const int C8 = C / 8;
+    const int n8 = (p1 - p0) * C8;
+    bool bad = false;
+    for (int i = threadIdx.x; i < n8; i += 256) {
+        const int c0 = (i % C8) * 8;
+        const float* src = x + base + (size_t)i * 8;
+        float4 v0 = *reinterpret_cast<const float4*>(src);
+        float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+        v0.x = fmaf(v0.x, sc[c0], sh[c0]); v0.y = fmaf(v0.y, sc[c0 + 1], sh[c0 + 1]);
+        v0.z = fmaf(v0.z, sc[c0 + 2], sh[c0 + 2]); v0.w = fmaf(v0.w, sc[c0 + 3], sh[c0 + 3]);
+        v1.x = fmaf(v1.x, sc[c0 + 4], sh[c0 + 4]); v1.y = fmaf(v1.y, sc[c0 + 5], sh[c0 + 5]);
+        v1.z = fmaf(v1.z, sc[c0 + 6], sh[c0 + 6]); v1.w = fmaf(v1.w, sc[c0 + 7], sh[c0 + 7]);
+        if (silu) {
+            v0.x = silu_f(v0.x); v0.y = silu_f(v0.y); v0.z = silu_f(v0.z); v0.w = silu_f(v0.w);
+            v1.x = silu_f(v1.x); v1.y = silu_f(v1.y); v1.z = silu_f(v1.z); v1.w = silu_f(v1.w);
+        }
+        uint2 h0, l0, h1, l1;
+        split4(v0, h0, l0);
+        split4(v1, h1, l1);
+        char* g = y + (base + (size_t)i * 8) * 4;
+        *reinterpret_cast<uint4*>(g) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+        *reinterpret_cast<uint4*>(g + 16) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+        bad = bad || h2_bad(v0.x) || h2_bad(v0.y) || h2_bad(v0.z) || h2_bad(v0.w) || h2_bad(v1.x) || h2_bad(v1.y) ||
+              h2_bad(v1.z) || h2_bad(v1.w);
+    }
+    h2_flag(ovf, bad);
+}
+
+__global__ __launch_bounds__(256) void k_f32_to_h2(const float* __restrict__ x, char* __restrict__ y, size_t n4,
+                                                   unsigned* ovf) {
+    bool bad = false;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        const float4 v = reinterpret_cast<const float4*>(x)[i];
+        store4_h2(y, (i >> 1) * 32, (int)(i & 1), v);
+        bad = bad || h2_bad(v.x) || h2_bad(v.y) || h2_bad(v.z) || h2_bad(v.w);
+    }
+    h2_flag(ovf, bad);
+}
+
+__global__ __launch_bounds__(256) void k_h2_to_f32(const char* __restrict__ x, float* __restrict__ y, size_t n4) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
+        reinterpret_cast<float4*>(y)[i] = load4_h2(x, (i >> 1) * 32, (int)(i & 1));
 }
 
 }  // namespace
@@ -295,8 +365,51 @@ extern "C" int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, in
     const size_t n = (size_t)Bt * 4 * H * W * (C / 4);
     if (n == 0) return TCX_OK;
     const int blocks = (int)std::min<size_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_upsample2x, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, y, Bt, H, W, C, scale, shift);
+    hipLaunchKernelGGL(k_upsample2x<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, y, Bt, H, W, C, scale,
+                       shift, nullptr);
     return check_launch("tcx_upsample2x");
+}
+
+extern "C" int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
+                                 const float* shift, unsigned* ovf, void* stream) {
+    TCX_REQUIRE(x && y && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_upsample2x_h2: bad args");
+    TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x_h2: scale/shift pair");
+    const size_t n = (size_t)Bt * 4 * H * W * (C / 4);
+    if (n == 0) return TCX_OK;
+    const int blocks = (int)std::min<size_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_upsample2x<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (float*)y, Bt, H, W, C,
+                       scale, shift, ovf);
+    return check_launch("tcx_upsample2x_h2");
+}
+
+extern "C" int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale,
+                                   const float* shift, int silu, unsigned* ovf, void* stream) {
+    TCX_REQUIRE(x && y && scale && shift && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_gn_apply_tab_h2: bad args");
+    TCX_REQUIRE((const void*)x == y || (const char*)y + (size_t)Bt * HW * C * 4 <= (const char*)x ||
+                (const char*)x + (size_t)Bt * HW * C * 4 <= (const char*)y, "tcx_gn_apply_tab_h2: partial overlap");
+    if (Bt == 0) return TCX_OK;
+    const int ppb = std::max(1, 32768 / C);
+    const dim3 grid(cdiv(HW, ppb), Bt);
+    const size_t shm = (size_t)2 * ((C + 3) & ~3) * sizeof(float);
+    hipLaunchKernelGGL(k_gn_apply_tab_h2, grid, dim3(256), shm, (hipStream_t)stream, x, (char*)y, HW, C, scale, shift,
+                       silu, ppb, ovf);
+    return check_launch("tcx_gn_apply_tab_h2");
+}
+
+extern "C" int tcx_f32_to_h2(const float* x, void* y, size_t n, unsigned* ovf, void* stream) {
+    TCX_REQUIRE(x && y && n % 8 == 0 && aligned16(x) && aligned16(y), "tcx_f32_to_h2: n %% 8 and 16-B alignment");
+    if (n == 0) return TCX_OK;
+    const int blocks = (int)std::min<size_t>((n / 4 + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_f32_to_h2, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (char*)y, n / 4, ovf);
+    return check_launch("tcx_f32_to_h2");
+}
+
+extern "C" int tcx_h2_to_f32(const void* x, float* y, size_t n, void* stream) {
+    TCX_REQUIRE(x && y && n % 8 == 0 && aligned16(x) && aligned16(y), "tcx_h2_to_f32: n %% 8 and 16-B alignment");
+    if (n == 0) return TCX_OK;
+    const int blocks = (int)std::min<size_t>((n / 4 + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_h2_to_f32, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const char*)x, y, n / 4);
+    return check_launch("tcx_h2_to_f32");
 }
 
 extern "C" int tcx_layernorm_film(const float* x, float* y, int M, int Wd, const float* ln_w, const float* ln_b,

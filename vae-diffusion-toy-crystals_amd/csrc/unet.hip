@@ -414,15 +414,28 @@ struct GnRef {
 
 // conv helper: writes GN partials in the epilogue when the tile geometry allows it, else runs
 // the partials kernel afterwards; sc/sh{1,2}: fused GN+SiLU prologue tables of the sources.
+// H2: split-path context of one evaluation (on: sources are h2 and the f16x3 conv runs)
+struct H2Ctx {
+    bool on;
+    unsigned* ovf;
+};
+
 int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2, int Bt, int bmod, int H, int W,
             int stride, int pad, const float* bias_b, const float* resid, float* y, double* gn, int* nsplit,
             hipStream_t st, const float* sc1 = nullptr, const float* sh1 = nullptr, const float* sc2 = nullptr,
-            const float* sh2 = nullptr) {
+            const float* sh2 = nullptr, H2Ctx h2 = {false, nullptr}, int out_h2 = 0) {
     const int Ho = (H + 2 * pad - cv.ks) / stride + 1, Wo = (W + 2 * pad - cv.ks) / stride + 1;
     const int HoWo = Ho * Wo;
     const bool fused = gn && HoWo % 128 == 0;
-    TCX_TRY(tcx_conv2d(x1, x2, Bt, bmod, H, W, C1, C2, cv.w, cv.b, bias_b, resid, y, cv.cout, cv.cout_pad, cv.kpad,
-                       cv.ks, stride, pad, 1, 0, 0, fused ? gn : nullptr, sc1, sh1, sc2, sh2, st));
+    if (h2.on) {
+        TCX_REQUIRE(cv.wh && cv.wscale && !sc1 && !sc2, "tcx_unet: split path needs packed h2 weights");
+        TCX_TRY(tcx_conv2d_h2(x1, x2, Bt, bmod, H, W, C1, C2, cv.wh, cv.wscale, cv.b, bias_b, resid, y, out_h2,
+                              cv.cout, cv.cout_pad, cv.kpad, cv.ks, stride, pad, 1, 0, fused ? gn : nullptr, h2.ovf,
+                              st));
+    } else {
+        TCX_TRY(tcx_conv2d(x1, x2, Bt, bmod, H, W, C1, C2, cv.w, cv.b, bias_b, resid, y, cv.cout, cv.cout_pad,
+                           cv.kpad, cv.ks, stride, pad, 1, 0, 0, fused ? gn : nullptr, sc1, sh1, sc2, sh2, st));
+    }
     if (gn && !fused) {
         const int ns = std::max(1, HoWo / 512);
         TCX_TRY(tcx_gn_partials(y, Bt, HoWo, cv.cout, ns, gn, st));
@@ -491,9 +504,13 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     auto SC = [&](int i) -> const float* { return pro[i] ? P.sc(i) : nullptr; };
     auto SH = [&](int i) -> const float* { return pro[i] ? P.sh(i) : nullptr; };
     // finalize the table of norm i, or normalise `y` in place when no prologue can consume it
-    auto norm = [&](int i, float* y, int HW, int Cn) -> int {
+    // split path: every conv source is h2 (h2.hpp) — GroupNorm applies feeding a conv write h2
+    // in place, convs feeding only convs (ds1, ds2, us2, us1) write h2, the rest stay fp32
+    const H2Ctx h2{net->precision == 1, net->h2_ovf};
+    auto norm = [&](int i, float* y, int HW, int Cn, bool to_h2 = true) -> int {
         TCX_TRY(gn_tab(net, P, i, HW, Cn, gn, ns, st));
         if (pro[i]) return TCX_OK;
+        if (h2.on && to_h2) return tcx_gn_apply_tab_h2(y, y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, h2.ovf, st);
         return tcx_gn_apply_tab(y, y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, st);
     };
     // down1 (first conv: x_t channel only, maps folded into bias0; the conv bias is inside bias0)
@@ -514,26 +531,28 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     }
     TCX_TRY(norm(0, P.a64, P.P0, C));
     TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.h1, gn, &ns, st,
-                    SC(0), SH(0)));
+                    SC(0), SH(0), nullptr, nullptr, h2));
     TCX_TRY(norm(1, P.h1, P.P0, C));  // h1 stays raw; its two consumers apply table 1
     // ds1: 4x4/s2 circular on silu(gn(h1))
     TCX_TRY(conv_gn(net->ds1, P.h1, nullptr, C, 0, Bt, 0, H, W, 2, 1, nullptr, nullptr, P.a32, nullptr, &ns, st,
-                    SC(1), SH(1)));
+                    SC(1), SH(1), nullptr, nullptr, h2, 1));
     // down2
-    TCX_TRY(conv_gn(net->down2_0, P.a32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st));
+    TCX_TRY(conv_gn(net->down2_0, P.a32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st,
+                    nullptr, nullptr, nullptr, nullptr, h2));
     TCX_TRY(norm(2, P.b32, P.P1, C2));
     TCX_TRY(conv_gn(net->down2_1, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.h2, gn, &ns, st,
-                    SC(2), SH(2)));
+                    SC(2), SH(2), nullptr, nullptr, h2));
     TCX_TRY(norm(3, P.h2, P.P1, C2));  // h2 raw; consumers apply table 3
     // ds2
     TCX_TRY(conv_gn(net->ds2, P.h2, nullptr, C2, 0, Bt, 0, H1, W1, 2, 1, nullptr, nullptr, P.a16, nullptr, &ns, st,
-                    SC(3), SH(3)));
+                    SC(3), SH(3), nullptr, nullptr, h2, 1));
     // mid
-    TCX_TRY(conv_gn(net->mid_0, P.a16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, nullptr, nullptr, P.b16, gn, &ns, st));
+    TCX_TRY(conv_gn(net->mid_0, P.a16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, nullptr, nullptr, P.b16, gn, &ns, st,
+                    nullptr, nullptr, nullptr, nullptr, h2));
     TCX_TRY(norm(4, P.b16, P.P2, C2));
     TCX_TRY(conv_gn(net->mid_1, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, nullptr, nullptr, P.a16, gn, &ns, st,
-                    SC(4), SH(4)));
-    // the attention block needs the normalised tensor itself (input of attn.norm and residual)
+                    SC(4), SH(4), nullptr, nullptr, h2));
+    // the attention block needs the normalised tensor itself (input of attn.norm and residual): fp32
     TCX_TRY(gn_tab(net, P, 5, P.P2, C2, gn, ns, st));
     TCX_TRY(tcx_gn_apply_tab(P.a16, P.a16, Bt, P.P2, C2, P.sc(5), P.sh(5), 1, st));
     // attention: x_in = a16; b16 = GN(x_in); qkv = 1x1; b16 = attn; a16 = x_in + proj(b16)
@@ -541,37 +560,44 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         const int ns_a = std::max(1, P.P2 / 256);
         TCX_TRY(tcx_gn_partials(P.a16, Bt, P.P2, C2, ns_a, gn, st));
         TCX_TRY(gn_tab(net, P, 6, P.P2, C2, gn, ns_a, st));
-        TCX_TRY(tcx_gn_apply_tab(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, st));
+        if (h2.on) TCX_TRY(tcx_gn_apply_tab_h2(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, h2.ovf, st));
+        else TCX_TRY(tcx_gn_apply_tab(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, st));
         const tcx_conv& q = net->qkv;
-        TCX_TRY(tcx_conv2d(P.b16, nullptr, Bt, 0, H2, W2, C2, 0, q.w, q.b, nullptr, nullptr, P.qkv, q.cout, q.cout_pad,
-                           q.kpad, 1, 1, 0, 1, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, st));
-        TCX_TRY(tcx_attention(P.qkv, P.b16, Bt, P.P2, C2, net->heads, st));
+        int dummy = 0;
+        TCX_TRY(conv_gn(q, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 0, nullptr, nullptr, P.qkv, nullptr, &dummy, st,
+                        nullptr, nullptr, nullptr, nullptr, h2));
+        if (h2.on) TCX_TRY(tcx_attention_h2(P.qkv, P.b16, Bt, P.P2, C2, net->heads, h2.ovf, st));
+        else TCX_TRY(tcx_attention(P.qkv, P.b16, Bt, P.P2, C2, net->heads, st));
         const tcx_conv& pr = net->proj;
-        TCX_TRY(tcx_conv2d(P.b16, nullptr, Bt, 0, H2, W2, C2, 0, pr.w, pr.b, nullptr, P.a16, P.a16, pr.cout,
-                           pr.cout_pad, pr.kpad, 1, 1, 0, 1, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, st));
+        TCX_TRY(conv_gn(pr, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 0, nullptr, P.a16, P.a16, nullptr, &dummy, st,
+                        nullptr, nullptr, nullptr, nullptr, h2));
     }
     // us2: bilinear x2 (edge-clamped) into the free b32 buffer, then the circular 3x3 conv -> a32.
     // (The upsample-on-load conv variant re-reads 4 source taps per im2col element and measured
     // slower than this separate 250 MB pass.)
-    TCX_TRY(tcx_upsample2x(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, st));
-    TCX_TRY(conv_gn(net->us2, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, nullptr, &ns, st));
+    if (h2.on) TCX_TRY(tcx_upsample2x_h2(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, h2.ovf, st));
+    else TCX_TRY(tcx_upsample2x(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, st));
+    TCX_TRY(conv_gn(net->us2, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, nullptr, &ns, st,
+                    nullptr, nullptr, nullptr, nullptr, h2, 1));
     // up2 on cat[a32, silu(gn(h2))]
     TCX_TRY(conv_gn(net->up2_0, P.a32, P.h2, C2, C2, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st,
-                    nullptr, nullptr, SC(3), SH(3)));
+                    nullptr, nullptr, SC(3), SH(3), h2));
     TCX_TRY(norm(7, P.b32, P.P1, C));
     TCX_TRY(conv_gn(net->up2_1, P.b32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, gn, &ns, st,
-                    SC(7), SH(7)));
+                    SC(7), SH(7), nullptr, nullptr, h2));
     // us1: GN+SiLU of up2's output in place (1x per element; the upsample-side transform
     // recomputed it for 4 taps per output and measured 3x slower), upsample into the free b64, conv
-    TCX_TRY(norm(8, P.a32, P.P1, C));
-    TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, st));
-    TCX_TRY(conv_gn(net->us1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, nullptr, &ns, st));
+    TCX_TRY(norm(8, P.a32, P.P1, C, false));
+    if (h2.on) TCX_TRY(tcx_upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, h2.ovf, st));
+    else TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, st));
+    TCX_TRY(conv_gn(net->us1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, nullptr, &ns, st,
+                    nullptr, nullptr, nullptr, nullptr, h2, 1));
     // up1 on cat[a64, silu(gn(h1))]
     TCX_TRY(conv_gn(net->up1_0, P.a64, P.h1, C, C, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.b64, gn, &ns, st, nullptr,
-                    nullptr, SC(1), SH(1)));
+                    nullptr, SC(1), SH(1), h2));
     TCX_TRY(norm(9, P.b64, P.P0, C));
     TCX_TRY(conv_gn(net->up1_1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, gn, &ns, st,
-                    SC(9), SH(9)));
+                    SC(9), SH(9), nullptr, nullptr, h2));
     // head: GN(up1.net.4)+SiLU fused with the out conv's channel reduction
     {
         TCX_TRY(gn_tab(net, P, 10, P.P0, C, gn, ns, st));
@@ -591,6 +617,9 @@ int validate(const tcx_unet* net, int B, int H, int W) {
     TCX_REQUIRE(net->emb_dim <= 256 && net->emb_dim % 2 == 0, "tcx_unet: emb_dim must be even and <= 256");
     TCX_REQUIRE(net->time_ch + net->cond_ch <= 64 && net->y_cont_dim >= 3 && net->y_cont_dim <= 16, "tcx_unet: bad cond dims");
     TCX_REQUIRE((H / 4) * (W / 4) <= 256, "tcx_unet: bottleneck attention supports N <= 256 tokens");
+    TCX_REQUIRE(net->precision == 0 || net->precision == 1, "tcx_unet: precision must be 0 (fp32) or 1 (f16x3)");
+    TCX_REQUIRE(net->precision == 0 || (net->base_ch % 32 == 0 && ((H / 4) * (W / 4)) % 32 == 0),
+                "tcx_unet: the f16x3 split path needs base_ch %% 32 == 0 and (H/4)*(W/4) %% 32 == 0");
     return TCX_OK;
 }
 

@@ -28,7 +28,7 @@ TCX_SCAL = 8
 
 class TcxConv(ctypes.Structure):
     _fields_ = [("w", c_fp), ("b", c_fp), ("cin", c_int), ("cout", c_int), ("ks", c_int), ("kpad", c_int),
-                ("cout_pad", c_int)]
+                ("cout_pad", c_int), ("wh", c_fp), ("wscale", c_fp)]
 
 
 _CONV_NAMES = ["down1_0", "down1_1", "ds1", "down2_0", "down2_1", "ds2", "mid_0", "mid_1", "qkv", "proj", "us2",
@@ -41,7 +41,8 @@ class TcxUnet(ctypes.Structure):
                                        "tcm_b", "cat_emb", "cmlp_w1t", "cmlp_b1", "cmlp_w2t", "cmlp_b2", "cout_wt",
                                        "cout_b", "map_wsum")]
                 + [(n, TcxConv) for n in _CONV_NAMES]
-                + [("out_w", c_fp), ("out_b", c_float), ("gn_w", c_fp * 11), ("gn_b", c_fp * 11)])
+                + [("out_w", c_fp), ("out_b", c_float), ("gn_w", c_fp * 11), ("gn_b", c_fp * 11)]
+                + [("precision", c_int), ("h2_ovf", c_fp)])
 
 
 class TcxAdamTensor(ctypes.Structure):
@@ -67,6 +68,15 @@ _SIGS = {
     "tcx_gn_finalize": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_float, c_fp, c_fp, c_fp]),
     "tcx_upsample2x": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
     "tcx_attention": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
+    # f16x3 split path (h2 storage)
+    "tcx_pack_conv_weight_h2": (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_fp]),
+    "tcx_conv2d_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp, c_fp,
+                              c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
+    "tcx_gn_apply_tab_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp, c_fp]),
+    "tcx_upsample2x_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
+    "tcx_attention_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),
+    "tcx_f32_to_h2": (c_int, [c_fp, c_fp, c_size, c_fp, c_fp]),
+    "tcx_h2_to_f32": (c_int, [c_fp, c_fp, c_size, c_fp]),
     "tcx_unet_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int]),
     "tcx_unet_eval": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_fp, c_fp, c_int, c_int, c_int,
                               c_float, c_int, c_fp, c_fp, c_u64, c_u64, c_fp, c_fp, c_fp, c_size, c_fp]),
@@ -127,6 +137,26 @@ _SIGS = {
 }
 
 _lib = None
+
+# Conv arithmetic of the score U-Net evaluator: "f16x3" (split-f16 MFMA over h2 activations,
+# fp32-grade: DESIGN.md §3c) or "fp32" (v_mfma_f32_32x32x2_f32).  Env TCX_CONV_PRECISION or
+# set_conv_precision(); the U-Net falls back to fp32 per call where the split path does not apply
+# (base_ch % 32 != 0) or when an activation leaves the f16 range.
+_PRECISIONS = ("f16x3", "fp32")
+_conv_precision = os.environ.get("TCX_CONV_PRECISION", "f16x3")
+if _conv_precision not in _PRECISIONS:
+    raise ValueError(f"TCX_CONV_PRECISION must be one of {_PRECISIONS}, got {_conv_precision!r}")
+
+
+def set_conv_precision(name: str) -> None:
+    global _conv_precision
+    if name not in _PRECISIONS:
+        raise ValueError(f"conv precision must be one of {_PRECISIONS}, got {name!r}")
+    _conv_precision = name
+
+
+def conv_precision() -> str:
+    return _conv_precision
 
 
 class TcxError(RuntimeError):

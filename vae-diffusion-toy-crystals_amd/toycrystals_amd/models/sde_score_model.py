@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import warnings
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -119,6 +120,11 @@ class _UNetPack:
         net.n_types = model.n_types
         net.y_cont_dim = model.y_cont_dim
         net.heads = model.attn.num_heads
+        # the f16x3 split convs need every conv source channel count % 32 (base_ch % 32 == 0)
+        self.split_ok = model.base_ch % 32 == 0
+        self.ovf = torch.zeros(4, device=device, dtype=torch.int32)
+        net.h2_ovf = self.ovf.data_ptr()
+        net.precision = 0
 
         def dev(t: torch.Tensor) -> int:
             t = t.detach().to(device=device, dtype=torch.float32).contiguous()
@@ -147,7 +153,14 @@ class _UNetPack:
             check(L.tcx_pack_conv_weight(w.data_ptr(), wpk.data_ptr(), cout, cin, ks, cpad, kpad, st),
                   "pack conv weight")
             self.keep.extend([w, wpk])
-            return TcxConv(wpk.data_ptr(), dev(m.bias), cin, cout, ks, kpad, cpad)
+            wh = whs = None
+            if self.split_ok:
+                wh = torch.empty((cpad, kpad), device=device, dtype=torch.float32)  # h2: 4 B per element
+                whs = torch.empty(4, device=device, dtype=torch.float32)
+                check(L.tcx_pack_conv_weight_h2(wpk.data_ptr(), wh.data_ptr(), whs.data_ptr(), cpad, kpad, st),
+                      "pack conv weight h2")
+                self.keep.extend([wh, whs])
+            return TcxConv(wpk.data_ptr(), dev(m.bias), cin, cout, ks, kpad, cpad, ptr(wh), ptr(whs))
 
         w0 = model.down1.net[0].weight.detach()
         net.down1_0 = conv(model.down1.net[0], w0[:, :1])
@@ -178,6 +191,20 @@ class _UNetPack:
             net.gn_b[i] = dev(gnm.bias)
         self.net = net
         self.ws = None
+
+    def run(self, H: int, W: int, launch) -> None:
+        """Run `launch()` (which must (re)initialise its outputs) with the configured conv
+        precision; if an f16x3 run raised the range flag, re-run it in fp32 (one host sync)."""
+        split = (_lib.conv_precision() == "f16x3" and self.split_ok and ((H // 4) * (W // 4)) % 32 == 0)
+        self.net.precision = 1 if split else 0
+        if split:
+            self.ovf.zero_()
+        launch()
+        if split and int(self.ovf[0].item()) != 0:
+            warnings.warn("libtcx: an activation left the f16 range of the split path; recomputed in fp32")
+            self.net.precision = 0
+            launch()
+        self.net.precision = 0
 
     def workspace(self, Bt: int, H: int, W: int, extra: int = 0) -> Tuple[torch.Tensor, int]:
         need = int(lib().tcx_unet_workspace_size(ctypes.byref(self.net), Bt, H, W)) + extra
@@ -306,9 +333,9 @@ def _eval_eps(model: CondUNetTiny, x, t, t_per_sample, y_cat, y_cont, guidance: 
     Bt = 2 * B if guidance > 0.0 else B
     ws, nbytes = pk.workspace(Bt, H, W)
     eps = torch.empty_like(x)
-    check(lib().tcx_unet_eval(ctypes.byref(pk.net), ptr(x), None, ptr(t), t_per_sample, ptr(y_cat), ptr(y_cont), B, H,
-                              W, float(guidance), 0, None, None, 0, 0, None, ptr(eps), ptr(ws), nbytes,
-                              stream_ptr(x.device)), "tcx_unet_eval")
+    pk.run(H, W, lambda: check(lib().tcx_unet_eval(ctypes.byref(pk.net), ptr(x), None, ptr(t), t_per_sample, ptr(y_cat),
+                                                   ptr(y_cont), B, H, W, float(guidance), 0, None, None, 0, 0, None,
+                                                   ptr(eps), ptr(ws), nbytes, stream_ptr(x.device)), "tcx_unet_eval"))
     return eps
 
 
@@ -484,19 +511,24 @@ def sample_reverse_sde_euler_maruyama(model: CondUNetTiny, sde: VPSDE, y_cat: to
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
     x = torch.empty((B, 1, H, W), device=device, dtype=torch.float32)
+    zs = None
     if noise is not None:
         noise = noise.to(device=device, dtype=torch.float32).contiguous()
         if noise.shape[0] != n_steps + 1 or noise[0].numel() != x.numel():
             raise ValueError(f"noise must be [n_steps+1, B, 1, H, W], got {tuple(noise.shape)}")
-        x.copy_(noise[0].view_as(x))
         zs = noise[1:]
-    else:
-        check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
-        zs = None
     g = float(guidance_scale) if guidance_scale > 0.0 else 0.0
     ws, nbytes = pk.workspace(2 * B if g > 0 else B, H, W)
-    check(L.tcx_sde_sample(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g, ptr(tab),
-                           ptr(zs) if zs is not None else None, seed, ptr(ws), nbytes, st), "tcx_sde_sample")
+
+    def launch():
+        if noise is not None:
+            x.copy_(noise[0].view_as(x))
+        else:
+            check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
+        check(L.tcx_sde_sample(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g,
+                               ptr(tab), ptr(zs) if zs is not None else None, seed, ptr(ws), nbytes, st),
+              "tcx_sde_sample")
+    pk.run(H, W, launch)
     return x
 
 
@@ -513,15 +545,18 @@ def sample_probability_flow_ode(model: CondUNetTiny, sde: VPSDE, y_cat: torch.Te
     L = lib()
     st = stream_ptr(device)
     x = torch.empty((B, 1, H, W), device=device, dtype=torch.float32)
-    if x_init is not None:
-        x.copy_(x_init.to(device=device, dtype=torch.float32).view_as(x))
-    else:
-        if seed is None:
-            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
+    if x_init is None and seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
     g = float(guidance_scale) if guidance_scale > 0.0 else 0.0
     img_bytes = B * H * W * 4
     ws, nbytes = pk.workspace(2 * B if g > 0 else B, H, W, extra=2 * img_bytes + 1024)
-    check(L.tcx_ode_sample(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g, ptr(tab),
-                           ptr(ws), nbytes, st), "tcx_ode_sample")
+
+    def launch():
+        if x_init is not None:
+            x.copy_(x_init.to(device=device, dtype=torch.float32).view_as(x))
+        else:
+            check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
+        check(L.tcx_ode_sample(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g,
+                               ptr(tab), ptr(ws), nbytes, st), "tcx_ode_sample")
+    pk.run(H, W, launch)
     return x
