@@ -17,85 +17,10 @@
 // Fusions: channel concat (two sources), CFG batch aliasing (bmod), bilinear x2 upsample on
 // the A load, bias / per-batch bias / residual / activation epilogue, and GroupNorm partial
 // statistics of the output (fp64) for the following GroupNorm.
-#include "common.hpp"
-#include "h2.hpp"
+#include "conv_common.hpp"
 
 namespace tcx {
 namespace {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-// 16 zero bytes: masked-out im2col elements load from here (an address select, not a value
-// select after the load, which hipcc lowers through scratch memory).
-__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
-
-constexpr int BM = 128;
-constexpr int BK = 32;
-constexpr int LDA = 36;  // padded LDS row (floats)
-
-struct ConvParams {
-    const float* x1;
-    const float* x2;
-    int C1, C2, Cin;
-    int bmod, H, W;    // source image dims (pre-upsample)
-    int Hi, Wi;        // im2col input dims (2H,2W when upsampling)
-    int Ho, Wo, HoWo, M;
-    const float* w;
-    const float* bias;
-    const float* bias_b;
-    const float* resid;
-    float* y;
-    int Cout, kpad, nchunks;
-    int ks, stride, pad_y, pad_x, circular;
-    // output placement (sub-pixel phases of a transposed conv): row = oy*osy + ooy
-    int Hy, Wy, osy, ooy, osx, oox;
-    int act;       // 0 none, 1 relu, 2 sigmoid, 3 silu
-    double* gn;    // [Bt][nsplit][Cout][2] or null
-    int nsplit;
-    int n_nblk;
-    // GroupNorm+SiLU prologue of each source: x -> silu(x * scale[b][c] + shift[b][c]) applied
-    // when the staged chunk is written to LDS (tables from tcx_gn_finalize; null = raw source)
-    const float *sc1, *sh1, *sc2, *sh2;
-    unsigned bytes1, bytes2, bytesw;  // buffer extents for the MODE 3 raw-buffer loads
-    // f16x3 path (SPL): sources and weights in the h2 split format (h2.hpp), *wscale = 2^-e
-    // undoes the weights' power-of-two scale; out_h2 writes the output in h2 (ovf: range flag)
-    const float* wscale;
-    int out_h2;
-    unsigned* ovf;
-};
-
-constexpr int PRO_MAXC = 384;  // max channels per source for the fused GN prologue
-
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-// Raw buffer load (32-bit byte offset, hardware range check: an offset past num_records reads 0)
-__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const float* p, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)bytes, 0x00020000);
-}
-// 0x80000000: beyond every num_records (extents are < 2^31) with or without the SGPR offset
-// added, and no 32-bit wrap -> the load returns zeros
-constexpr int kOOB = (int)0x80000000u;
-constexpr int MAXTAP = 16;  // MODE 3 offset table: up to 4x4 kernels
-
-__device__ __forceinline__ float4 f4_fma(float s, float4 a, float4 acc) {
-    return make_float4(fmaf(s, a.x, acc.x), fmaf(s, a.y, acc.y), fmaf(s, a.z, acc.z), fmaf(s, a.w, acc.w));
-}
-
-// Bilinear x2 (align_corners=False) tap: mirrors ATen's upsample_bilinear2d CPU kernel:
-// src = 0.5*(d+0.5)-0.5 clamped at 0, i1 = i0 + (i0 < n-1), l1 = src - i0, l0 = 1 - l1,
-// out = l0y*(l0x*a00 + l1x*a01) + l1y*(l0x*a10 + l1x*a11).
-__device__ __forceinline__ void bilin_axis(int d, int n, int& i0, int& i1, float& l0, float& l1) {
-    float s = 0.5f * ((float)d + 0.5f) - 0.5f;
-    s = s < 0.f ? 0.f : s;
-    i0 = (int)s;
-    i1 = i0 + (i0 < n - 1 ? 1 : 0);
-    l1 = s - (float)i0;
-    l0 = 1.f - l1;
-}
 
 // MODE 0: float4 loads, per-lane (tap, ci) decode (Cin % 4 == 0)
 // MODE 1: scalar loads, any Cin (the Cin = 1 first convs)
@@ -403,26 +328,65 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[n], acc[n], 0, 0, 0);
         };
+        // Two register staging sets, prefetch distance 2: chunk c+2 is loaded while chunk c computes
+        // and chunk c+1 (loaded one iteration earlier, so its latency is covered by a whole chunk)
+        // goes to LDS at the end of the iteration.  One f16x3 chunk is only 18 MFMAs per wave,
+        // too short to hide an L2 round trip at distance 1.  MODE 3 staging: A = 4 pixel rows of
+        // 16 B at the tap's byte offset, B = NT weight rows of 16 B.
+        float4 sa1[4], sb1[NT];
+        // running (tap, channel) of the load stream (wave-uniform, SGPRs): chunks are loaded in
+        // order, so advance by 32 channels per chunk instead of dividing; past the last chunk the
+        // state stays put (the last chunk is re-loaded into a set nothing stores)
+        int ld_c = 1, ld_tap = BK / p.Cin, ld_ci = BK % p.Cin;
+        auto ld_set = [&](float4 (&xa)[4], float4 (&xb)[NT]) {
+            const bool s1 = ld_ci < p.C1;
+            const int cc = (s1 ? ld_ci : ld_ci - p.C1) * 4;
+            const int4 po = *reinterpret_cast<const int4*>(&Ptab[ld_tap * BM + prow * 4]);
+            const __amdgpu_buffer_rsrc_t rs = s1 ? r1 : r2;
+            xa[0] = bld4(rs, po.x + k4 * 16, cc);
+            xa[1] = bld4(rs, po.y + k4 * 16, cc);
+            xa[2] = bld4(rs, po.z + k4 * 16, cc);
+            xa[3] = bld4(rs, po.w + k4 * 16, cc);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) xb[j] = bld4(rw, boffw[j], ld_c * BK * 4);
+            if (ld_c + 1 < p.nchunks) {
+                ++ld_c;
+                ld_ci += BK;
+                if (ld_ci == p.Cin) {
+                    ld_ci = 0;
+                    ++ld_tap;
+                }
+            }
+        };
+        auto st_set = [&](const float4 (&xa)[4], const float4 (&xb)[NT], int buf) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&As[buf][(prow + 32 * i) * LDA + k4 * 4]) = xa[i];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) *reinterpret_cast<float4*>(&Bs[buf][(prow + 32 * j) * LDA + k4 * 4]) = xb[j];
+        };
+        // chunk 0 is in LDS buffer 0 (common prologue); chunk 1 -> set 1
+        ld_set(sa1, sb1);
         rd(0, 0, ah0, al0, bh0, bl0);
-        for (int c = 0; c < p.nchunks; ++c) {
+        auto iter = [&](int c, float4 (&la)[4], float4 (&lb)[NT], const float4 (&sa)[4], const float4 (&sb)[NT]) {
             const int cur = c & 1;
-            const int cn = c + 1 < p.nchunks ? c + 1 : c;
-            const Dec d = decode(cn);
-            read_poff(d);
+            ld_set(la, lb);  // chunk c + 2
             rd(cur, 1, ah1, al1, bh1, bl1);
-            load_a(d, cn, 0);
-            load_a(d, cn, 1);
-            load_a(d, cn, 2);
-            load_a(d, cn, 3);
-            load_b(cn);
             __builtin_amdgcn_sched_barrier(0);
             mf(ah0, al0, bh0, bl0);
-            __builtin_amdgcn_sched_barrier(0);
             mf(ah1, al1, bh1, bl1);
-            store_chunk(cur ^ 1);
+            __builtin_amdgcn_sched_barrier(0);
+            st_set(sa, sb, cur ^ 1);
             __syncthreads();
             rd(cur ^ 1, 0, ah0, al0, bh0, bl0);
+        };
+        // pairs of iterations with the staging sets swapped (static registers, no branch inside the
+        // loop body, so the waitcnt state at the back edge is exact); an odd last chunk is peeled
+        int c = 0;
+        for (; c + 1 < p.nchunks; c += 2) {
+            iter(c, ra, rb, sa1, sb1);
+            iter(c + 1, sa1, sb1, ra, rb);
         }
+        if (c < p.nchunks) iter(c, ra, rb, sa1, sb1);
     } else {
     Dec dc = decode(0);  // decode of the chunk being computed
     read_frags(0, 0, dc, fa0, fb0);
@@ -459,103 +423,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     }
     }  // !SPL
 
-    // ---- epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-    const bool gn = p.gn != nullptr;
-    double* red = reinterpret_cast<double*>(&As[0][0]);  // [4 waves][BN][2] (LDS free after the loop)
-    const bool dense_out = p.osy == 1 && p.osx == 1;
-    const bool one_img = p.HoWo % BM == 0;  // the whole 128-pixel tile belongs to image m0 / HoWo
-    const int btile = m0 / p.HoWo;
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-        const int co = n0 + n * 32 + li;
-        const bool cv = co < p.Cout;
-        const int coc = cv ? co : 0;
-        const float bco = p.bias ? p.bias[coc] : 0.f;
-        const float bbt = (p.bias_b && one_img) ? p.bias_b[(size_t)btile * p.Cout + coc] : 0.f;
-        size_t oidx[16];
-        bool ok[16];
-        float add[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
-            const int m = m0 + wv * 32 + row;
-            ok[r] = m < p.M && cv;
-            const int mm = m < p.M ? m : p.M - 1;
-            add[r] = bco + bbt;
-            if (dense_out) {
-                oidx[r] = (size_t)mm * p.Cout + coc;
-                if (p.bias_b && !one_img) add[r] += p.bias_b[(size_t)(mm / p.HoWo) * p.Cout + coc];
-            } else {
-                const int b = mm / p.HoWo;
-                const int rr = mm - b * p.HoWo;
-                const int oy = rr / p.Wo, ox = rr - (rr / p.Wo) * p.Wo;
-                oidx[r] = ((size_t)b * p.Hy * p.Wy + (size_t)(oy * p.osy + p.ooy) * p.Wy + (ox * p.osx + p.oox)) * p.Cout + coc;
-                if (p.bias_b) add[r] += p.bias_b[(size_t)b * p.Cout + coc] - bbt;
-            }
-        }
-        if (p.resid) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) add[r] += p.resid[oidx[r]];
-        }
-        double s = 0.0, ss = 0.0;
-        const float wsc = SPL ? *p.wscale : 1.f;
-        bool bad = false;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            float v = (SPL ? acc[n][r] * wsc : acc[n][r]) + add[r];
-            if (p.act == 1) v = fmaxf(v, 0.f);
-            else if (p.act == 2) v = 1.f / (1.f + expf(-v));
-            else if (p.act == 3) v = silu_f(v);
-            if (p.out_h2) {
-                // h2 record of the pixel: lane pairs (2j, 2j+1) of an 8-channel group swap halves so
-                // the even lane stores the hi pair and the odd lane the lo pair (one dword each)
-                const unsigned sp = split1(v);
-                const bool odd = (li & 1) != 0;
-                const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
-                const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
-                const size_t pe = oidx[r] - (size_t)coc;  // pixel's first element
-                const int c8 = coc & ~7, j = (coc & 7) & ~1;
-                if (ok[r]) {
-                    *reinterpret_cast<unsigned*>(reinterpret_cast<char*>(p.y) + pe * 4 + (size_t)c8 * 4 + (odd ? 16 : 0) + 2 * j) = word;
-                    bad = bad || h2_bad(v);
-                }
-            } else if (ok[r]) {
-                p.y[oidx[r]] = v;
-            }
-            if (ok[r]) {
-                s += (double)v;
-                ss += (double)v * (double)v;
-            }
-        }
-        h2_flag(p.ovf, bad);
-        if (gn) {
-            s += __shfl_xor(s, 32);
-            ss += __shfl_xor(ss, 32);
-            if (lh == 0) {
-                red[(wv * BN + n * 32 + li) * 2 + 0] = s;
-                red[(wv * BN + n * 32 + li) * 2 + 1] = ss;
-            }
-        }
-    }
-    if (gn) {
-        __syncthreads();
-        if (tid < BN) {
-            const int co = n0 + tid;
-            if (co < p.Cout) {
-                double s = 0.0, ss = 0.0;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    s += red[(w * BN + tid) * 2 + 0];
-                    ss += red[(w * BN + tid) * 2 + 1];
-                }
-                const int b = m0 / p.HoWo;
-                const int split = (m0 - b * p.HoWo) / BM;
-                double* dst = p.gn + (((size_t)b * p.nsplit + split) * p.Cout + co) * 2;
-                dst[0] = s;
-                dst[1] = ss;
-            }
-        }
-    }
+    conv_epilogue<NT, SPL, 4>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(&As[0][0]));
 }
 
 template <int NT>
@@ -743,6 +611,7 @@ extern "C" int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, i
     TCX_REQUIRE(b1 < lim && b2 < lim && bw < lim, "tcx_conv2d_h2: operands must be < 2 GiB (32-bit buffer offsets)");
     p.bytes1 = (unsigned)b1; p.bytes2 = (unsigned)b2; p.bytesw = (unsigned)bw;
     p.wscale = wscale; p.out_h2 = out_h2; p.ovf = ovf;
+    if (conv3h_applies(p, cout_pad)) return launch_conv3h(p, cout_pad, (hipStream_t)stream);
     return launch_conv(p, cout_pad, 0, (hipStream_t)stream);
 }
 

@@ -1,0 +1,279 @@
+// Halo-staged 3x3 stride-1 conv over h2 (split-f16) operands: the hot layer shape of
+// CondUNetTiny (every _ConvBlock conv and us*_conv, /root/reference/src/toycrystals/models/
+// sde_score_model.py:102,105,218,222 — 3x3, padding 1, circular).
+//
+// The implicit-GEMM kernel of conv.hip (k_conv SPL) gathers every im2col element from L1/L2 and
+// writes it to LDS once per tap: 9 LDS writes per input element, and at the f16x3 MFMA rate
+// (18 MFMA per wave per 32-deep chunk) those ds_write_b128 (13 LDS cycles each) and the global
+// loads behind them, not the MFMA, set the pace.  Here a workgroup owns 256 output pixels = whole
+// image rows (TR = 256/W rows) x 96 output channels, and per 32-channel input chunk stages the
+// (TR+2) x (W+2) halo of those rows ONCE in LDS (circular wrap or zero padding applied while
+// staging); the 9 taps then read their A fragments from the same halo at a constant
+// (dy*(W+2) + dx)*144-byte offset, an immediate of the ds_read.  Per tap only the weight chunk
+// (96 x 32 x h2) is staged.  K order: input-channel chunk outer, tap inner.
+//
+// Tile: 8 waves (512 threads, 2 per SIMD), wave w = output pixels [32w, 32w+32) of the tile x
+// NT = 3 accumulator tiles of 32 channels; per tap and 16-deep step 3 x v_mfma_f32_32x32x16_f16
+// per accumulator (hi*lo, lo*hi, hi*hi; h2.hpp).  LDS: halo x2 (next chunk staged during taps
+// 0-4 of the current one) + weight chunk x2 = 141.7 KB at W = 64.  Epilogue shared with k_conv
+// (conv_common.hpp), GroupNorm partials per 128-pixel half so the stats layout is unchanged.
+#include "conv_common.hpp"
+
+namespace tcx {
+namespace {
+
+constexpr int HROW = 36;     // floats per staged pixel: 32 (h2 of 32 channels, 128 B) + 16 B pad
+
+// NW waves per workgroup, tile = 32*NW output pixels = whole rows
+__host__ __device__ constexpr int halo_px(int W, int NW) { return (32 * NW / W + 2) * (W + 2); }
+// halo buffers: two at NW = 8 (one workgroup per CU), one at NW = 4 (two workgroups per CU)
+__host__ __device__ constexpr int halo_bufs(int NW) { return NW == 8 ? 2 : 1; }
+
+constexpr size_t conv3h_lds_bytes(int NT, int W, int NW) {
+    return (size_t)(halo_bufs(NW) * halo_px(W, NW) + 2 * 32 * NT) * HROW * sizeof(float);
+}
+
+template <int NT, int W, bool CIRC, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void k_conv3h(ConvParams p) {
+    constexpr int HB = 32 * NW;
+    constexpr int NTHR = 64 * NW;
+    constexpr int HBUFS = halo_bufs(NW);
+    constexpr int BN = 32 * NT;
+    constexpr int W2 = W + 2;
+    constexpr int NPX = halo_px(W, NW);
+    constexpr int HPI = (NPX * 8 + NTHR - 1) / NTHR;  // halo pieces (16 B) per thread
+    constexpr int HBUF = NPX * HROW;            // floats per halo buffer
+    constexpr int BBUF = BN * HROW;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* const Hs = sm;                 // [HBUFS][NPX][HROW]
+    float* const Bs = sm + HBUFS * HBUF;  // [2][BN][HROW]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mblk = tile / p.n_nblk;
+    const int nblk = tile - mblk * p.n_nblk;
+    const int m0 = mblk * HB, n0 = nblk * BN;
+    const int b = m0 / p.HoWo;
+    const int r0 = (m0 - b * p.HoWo) / W;  // first output row of the tile
+    const int bs = p.bmod > 0 ? b % p.bmod : b;
+    const int H = p.H;
+    const int cpt = p.Cin / BK;  // 32-channel input chunks
+    const int nchunks = 9 * cpt;
+
+    const __amdgpu_buffer_rsrc_t r1 = mk_rsrc(p.x1, p.bytes1);
+    const __amdgpu_buffer_rsrc_t r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
+    const __amdgpu_buffer_rsrc_t rw = mk_rsrc(p.w, p.bytesw);
+
+    // ---- halo staging plan: piece e = tid + NTHR i -> halo pixel e >> 3, 16-B piece e & 7
+    const int rowb = p.C1 * 4;  // bytes per source pixel (C2 == C1 when there are two sources)
+    int hoff[HPI];              // source byte offset (kOOB: zero padding -> the buffer unit reads 0)
+    int hdst[HPI];              // LDS float index, -1: past the halo (no store)
+#pragma unroll
+    for (int i = 0; i < HPI; ++i) {
+        const int e = tid + NTHR * i;
+        const int hp = e >> 3;
+        hoff[i] = kOOB;
+        hdst[i] = -1;
+        if (hp < NPX) {
+            const int hr = hp / W2, hc = hp - hr * W2;
+            int y = r0 + hr - 1, x = hc - 1;
+            bool ok = true;
+            if (CIRC) {
+                y = wrap_idx(y, H);
+                x = wrap_idx(x, W);
+            } else {
+                ok = y >= 0 && y < H && x >= 0 && x < W;
+            }
+            hoff[i] = ok ? ((bs * H + y) * W + x) * rowb + (e & 7) * 16 : kOOB;
+            hdst[i] = hp * HROW + (e & 7) * 4;
+        }
+    }
+    float4 hv[HPI];
+    auto halo_load = [&](int j) {  // input-channel chunk j (uniform)
+        const int ci0 = j * BK;
+        const bool s1 = ci0 < p.C1;
+        const int cc = (s1 ? ci0 : ci0 - p.C1) * 4;
+        const __amdgpu_buffer_rsrc_t rs = s1 ? r1 : r2;
+#pragma unroll
+        for (int i = 0; i < HPI; ++i) hv[i] = bld4(rs, hoff[i], cc);
+    };
+    auto halo_store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < HPI; ++i)
+            if ((i + 1) * NTHR <= NPX * 8 || hdst[i] >= 0)  // only the last piece can fall past the halo
+                *reinterpret_cast<float4*>(&Hs[buf * HBUF + hdst[i]]) = hv[i];
+    };
+    // ---- weight chunk staging: BN rows x 8 pieces
+    constexpr int BPI = (BN * 8 + NTHR - 1) / NTHR;
+    float4 bv[BPI];
+    int boff[BPI];
+#pragma unroll
+    for (int i = 0; i < BPI; ++i) {
+        const int e = tid + NTHR * i;
+        boff[i] = ((n0 + (e >> 3)) * p.kpad) * 4 + (e & 7) * 16;
+    }
+    auto w_load = [&](int c) {  // chunk c = 9 j + t -> packed k = t * Cin + 32 j
+        const int j = c / 9, t = c - 9 * j;
+        const int kb = (t * p.Cin + j * BK) * 4;
+#pragma unroll
+        for (int i = 0; i < BPI; ++i)
+            if ((BN * 8) % NTHR == 0 || tid + NTHR * i < BN * 8) bv[i] = bld4(rw, boff[i], kb);
+    };
+    auto w_store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < BPI; ++i) {
+            const int e = tid + NTHR * i;
+            if ((BN * 8) % NTHR == 0 || e < BN * 8) *reinterpret_cast<float4*>(&Bs[buf * BBUF + (e >> 3) * HROW + (e & 7) * 4]) = bv[i];
+        }
+    };
+
+    // ---- fragments
+    const int mloc = wv * 32 + li;                                 // this lane's A row = tile pixel
+    const int abase = ((mloc / W) * W2 + (mloc % W)) * HROW + lh * 8;  // float index in a halo buffer
+    const int bbase = li * HROW + lh * 8;
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
+    h8 a_h[2], a_l[2], b_h[2][NT], b_l[2][NT];
+    auto rd_a = [&](int hbuf, int t) {  // tap t: both 16-deep steps
+        const int dy = t / 3, dx = t - 3 * (t / 3);
+        const float* A = &Hs[hbuf * HBUF + abase + (dy * W2 + dx) * HROW];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            a_h[s] = __builtin_bit_cast(h8, ld4(A + 16 * s));
+            a_l[s] = __builtin_bit_cast(h8, ld4(A + 16 * s + 4));
+        }
+    };
+    auto rd_b = [&](int bb) {
+        const float* B = &Bs[bb * BBUF + bbase];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                b_h[s][n] = __builtin_bit_cast(h8, ld4(B + n * 32 * HROW + 16 * s));
+                b_l[s][n] = __builtin_bit_cast(h8, ld4(B + n * 32 * HROW + 16 * s + 4));
+            }
+    };
+    auto mf = [&](int s) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[s], b_l[s][n], acc[n], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_l[s], b_h[s][n], acc[n], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[s], b_h[s][n], acc[n], 0, 0, 0);
+    };
+
+    // ---- prologue: halo 0 and weight chunk 0 in LDS; halo 1 and weight chunk 1 in flight
+    halo_load(0);
+    w_load(0);
+    halo_store(0);
+    w_store(0);
+    if (cpt > 1) halo_load(1);
+    w_load(nchunks > 1 ? 1 : 0);
+    __syncthreads();
+    rd_a(0, 0);
+
+    for (int j = 0; j < cpt; ++j) {
+        const int hb = HBUFS == 2 ? (j & 1) : 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int c = 9 * j + t;
+            const int cur = c & 1;
+            rd_b(cur);
+            __builtin_amdgcn_sched_barrier(0);
+            mf(0);
+            mf(1);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (HBUFS == 2) {
+                // halo j+1 (loaded since tap 4 of chunk j-1) into the other buffer; the next tap's
+                // A fragments come from the same halo (no barrier needed) or, after tap 8, the other
+                if (t == 4 && j + 1 < cpt) halo_store(hb ^ 1);
+                w_store(cur ^ 1);  // weight chunk c + 1
+                __syncthreads();
+                if (t == 4 && j + 2 < cpt) halo_load(j + 2);
+                if (c + 2 < nchunks) w_load(c + 2);
+                if (t < 8) rd_a(hb, t + 1);
+                else rd_a(hb ^ 1, 0);
+            } else {
+                // one halo buffer: after the last tap every wave is past its reads of halo j, so
+                // halo j+1 (loaded during chunk j) is stored behind one extra barrier
+                w_store(cur ^ 1);
+                __syncthreads();
+                if (c + 2 < nchunks) w_load(c + 2);
+                if (t < 8) {
+                    rd_a(0, t + 1);
+                } else {
+                    if (j + 1 < cpt) {
+                        halo_store(0);
+                        __syncthreads();
+                        if (j + 2 < cpt) halo_load(j + 2);
+                    }
+                    rd_a(0, 0);
+                }
+            }
+        }
+    }
+    __syncthreads();  // the halo buffers become the epilogue's reduction scratch
+    conv_epilogue<NT, true, NW>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
+}
+
+template <int NT, int W, int NW>
+int launch3h_w(const ConvParams& p, hipStream_t st) {
+    constexpr size_t shm = conv3h_lds_bytes(NT, W, NW);
+    static bool attr[2] = {false, false};
+    auto kc = p.circular ? &k_conv3h<NT, W, true, NW> : &k_conv3h<NT, W, false, NW>;
+    if (!attr[p.circular ? 1 : 0]) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)shm) != hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", shm);
+            return TCX_EHIP;
+        }
+        attr[p.circular ? 1 : 0] = true;
+    }
+    const int grid = (p.M / (32 * NW)) * p.n_nblk;
+    hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * NW), shm, st, p);
+    return check_launch("tcx_conv2d_h2(halo)");
+}
+
+// waves per workgroup: TCX_HALO_NW=8 (256-pixel tiles, one workgroup per CU) or 4 (default:
+// 128-pixel tiles, two workgroups per CU so one's prologue/epilogue overlaps the other's MFMAs)
+int halo_nw() {
+    static const int nw = [] {
+        const char* e = getenv("TCX_HALO_NW");
+        return (e && atoi(e) == 8) ? 8 : 4;
+    }();
+    return nw;
+}
+
+}  // namespace
+
+// Host dispatch (conv.hip): true when the halo kernel covers this conv.
+bool conv3h_applies(const ConvParams& p, int cout_pad) {
+    static const bool off = getenv("TCX_NO_HALO") != nullptr;
+    return !off && p.ks == 3 && p.stride == 1 && p.pad_y == 1 && p.pad_x == 1 && p.Hi == p.H && p.Wi == p.W &&
+           (p.W == 16 || p.W == 32 || p.W == 64) && p.H % (32 * halo_nw() / p.W) == 0 &&
+           p.HoWo % (32 * halo_nw()) == 0 &&
+           cout_pad % 96 == 0 && p.Cin % BK == 0 && p.C1 % BK == 0 && (p.C2 == 0 || p.C2 == p.C1) &&
+           p.kpad == 9 * p.Cin && p.osy == 1 && p.osx == 1;
+}
+
+int launch_conv3h(ConvParams& p, int cout_pad, hipStream_t st) {
+    p.n_nblk = cout_pad / 96;
+    if (p.M == 0) return TCX_OK;
+    prof_begin(st);
+    int rc;
+    if (halo_nw() == 8) {
+        if (p.W == 64) rc = launch3h_w<3, 64, 8>(p, st);
+        else if (p.W == 32) rc = launch3h_w<3, 32, 8>(p, st);
+        else rc = launch3h_w<3, 16, 8>(p, st);
+    } else {
+        if (p.W == 64) rc = launch3h_w<3, 64, 4>(p, st);
+        else if (p.W == 32) rc = launch3h_w<3, 32, 4>(p, st);
+        else rc = launch3h_w<3, 16, 4>(p, st);
+    }
+    prof_end(st, 2.0 * (double)p.M * p.Cout * 9 * p.Cin);
+    return rc;
+}
+
+}  // namespace tcx

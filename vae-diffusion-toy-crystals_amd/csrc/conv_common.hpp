@@ -1,0 +1,255 @@
+// Shared pieces of the implicit-GEMM conv kernels (conv.hip: k_conv, conv3h.hip: k_conv3h):
+// parameters, raw-buffer helpers and the fused epilogue.
+#pragma once
+#include "common.hpp"
+#include "h2.hpp"
+
+namespace tcx {
+
+struct ConvParams {
+    const float* x1;
+    const float* x2;
+    int C1, C2, Cin;
+    int bmod, H, W;    // source image dims (pre-upsample)
+    int Hi, Wi;        // im2col input dims (2H,2W when upsampling)
+    int Ho, Wo, HoWo, M;
+    const float* w;
+    const float* bias;
+    const float* bias_b;
+    const float* resid;
+    float* y;
+    int Cout, kpad, nchunks;
+    int ks, stride, pad_y, pad_x, circular;
+    // output placement (sub-pixel phases of a transposed conv): row = oy*osy + ooy
+    int Hy, Wy, osy, ooy, osx, oox;
+    int act;       // 0 none, 1 relu, 2 sigmoid, 3 silu
+    double* gn;    // [Bt][nsplit][Cout][2] or null
+    int nsplit;
+    int n_nblk;
+    // GroupNorm+SiLU prologue of each source: x -> silu(x * scale[b][c] + shift[b][c]) applied
+    // when the staged chunk is written to LDS (tables from tcx_gn_finalize; null = raw source)
+    const float *sc1, *sh1, *sc2, *sh2;
+    unsigned bytes1, bytes2, bytesw;  // buffer extents for the MODE 3 raw-buffer loads
+    // f16x3 path (SPL): sources and weights in the h2 split format (h2.hpp), *wscale = 2^-e
+    // undoes the weights' power-of-two scale; out_h2 writes the output in h2 (ovf: range flag)
+    const float* wscale;
+    int out_h2;
+    unsigned* ovf;
+};
+
+// Halo-staged 3x3 kernel (conv3h.hip): applicability test and launcher for tcx_conv2d_h2.
+bool conv3h_applies(const ConvParams& p, int cout_pad);
+int launch_conv3h(ConvParams& p, int cout_pad, hipStream_t st);
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// 16 zero bytes: masked-out im2col elements load from here (an address select, not a value
+// select after the load, which hipcc lowers through scratch memory).
+__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
+
+constexpr int BM = 128;
+constexpr int BK = 32;
+constexpr int LDA = 36;  // padded LDS row (floats)
+
+
+
+constexpr int PRO_MAXC = 384;  // max channels per source for the fused GN prologue
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Raw buffer load (32-bit byte offset, hardware range check: an offset past num_records reads 0)
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const float* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)bytes, 0x00020000);
+}
+// 0x80000000: beyond every num_records (extents are < 2^31) with or without the SGPR offset
+// added, and no 32-bit wrap -> the load returns zeros
+constexpr int kOOB = (int)0x80000000u;
+constexpr int MAXTAP = 16;  // MODE 3 offset table: up to 4x4 kernels
+
+__device__ __forceinline__ float4 f4_fma(float s, float4 a, float4 acc) {
+    return make_float4(fmaf(s, a.x, acc.x), fmaf(s, a.y, acc.y), fmaf(s, a.z, acc.z), fmaf(s, a.w, acc.w));
+}
+
+// Bilinear x2 (align_corners=False) tap: mirrors ATen's upsample_bilinear2d CPU kernel:
+// src = 0.5*(d+0.5)-0.5 clamped at 0, i1 = i0 + (i0 < n-1), l1 = src - i0, l0 = 1 - l1,
+// out = l0y*(l0x*a00 + l1x*a01) + l1y*(l0x*a10 + l1x*a11).
+__device__ __forceinline__ void bilin_axis(int d, int n, int& i0, int& i1, float& l0, float& l1) {
+    float s = 0.5f * ((float)d + 0.5f) - 0.5f;
+    s = s < 0.f ? 0.f : s;
+    i0 = (int)s;
+    i1 = i0 + (i0 < n - 1 ? 1 : 0);
+    l1 = s - (float)i0;
+    l0 = 1.f - l1;
+}
+
+// Fused epilogue of a conv tile: wave wv owns output rows m0 + 32*wv + [0, 32) and columns
+// n0 + [0, 32*NT).  C/D map of the 32x32 MFMAs: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+// bias / per-batch bias / residual / activation, fp32 or h2 store, and the fp64 GroupNorm partials
+// of every 128-pixel group of waves (4 waves each; red: LDS scratch [NW][32*NT][2] doubles).
+template <int NT, bool SPL, int NW>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x16 (&acc)[NT], int m0, int n0, int wv,
+                                              int tid, double* red) {
+    constexpr int BN = 32 * NT;
+    const int lane = tid & 63;
+    const int li = lane & 31;
+    const int lh = lane >> 5;
+    const bool gn = p.gn != nullptr;
+    // Fast path (every U-Net conv): dense NHWC output, whole tiles inside one image, no per-batch
+    // bias, output columns all valid, 32-bit element offsets; no per-row index arithmetic beyond
+    // one scalar multiple of Cout per accumulator row, GroupNorm partials summed per lane in fp32
+    // over its 16 rows (then fp64 across lanes and waves).
+    const bool fast = p.osy == 1 && p.osx == 1 && p.bias_b == nullptr && p.M % (32 * NW) == 0 &&
+                      p.HoWo % (32 * NW) == 0 && p.Cout % BN == 0 && (long long)p.M * p.Cout < (1ll << 29);
+    if (fast) {
+        const float wsc = SPL ? *p.wscale : 1.f;
+        const int obase = (m0 + wv * 32 + 4 * lh) * p.Cout;
+        char* const yb = reinterpret_cast<char*>(p.y);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int co = n0 + n * 32 + li;
+            const float bco = p.bias ? p.bias[co] : 0.f;
+            float s = 0.f, ss = 0.f;
+            bool bad = false;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int e = obase + ((r & 3) + 8 * (r >> 2)) * p.Cout + co;
+                float v = (SPL ? acc[n][r] * wsc : acc[n][r]) + bco;
+                if (p.resid) v += p.resid[e];
+                if (p.act == 1) v = fmaxf(v, 0.f);
+                else if (p.act == 2) v = 1.f / (1.f + expf(-v));
+                else if (p.act == 3) v = silu_f(v);
+                if (p.out_h2) {
+                    // lane pairs (2j, 2j+1) of an 8-channel group swap halves: the even lane
+                    // stores the hi pair, the odd lane the lo pair (one dword each)
+                    const unsigned sp = split1(v);
+                    const bool odd = (li & 1) != 0;
+                    const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
+                    const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
+                    const int pe = e - co + (co & ~7);  // the 8-channel group's first element
+                    *reinterpret_cast<unsigned*>(yb + (size_t)pe * 4 + (odd ? 16 : 0) + 2 * ((co & 7) & ~1)) = word;
+                    bad = bad || h2_bad(v);
+                } else {
+                    p.y[e] = v;
+                }
+                s += v;
+                ss = fmaf(v, v, ss);
+            }
+            h2_flag(p.ovf, bad);
+            if (gn) {
+                double ds = (double)s, dss = (double)ss;
+                ds += __shfl_xor(ds, 32);
+                dss += __shfl_xor(dss, 32);
+                if (lh == 0) {
+                    red[(wv * BN + n * 32 + li) * 2 + 0] = ds;
+                    red[(wv * BN + n * 32 + li) * 2 + 1] = dss;
+                }
+            }
+        }
+    } else {
+    const bool dense_out = p.osy == 1 && p.osx == 1;
+    const bool one_img = p.HoWo % (32 * NW) == 0;  // the whole tile belongs to image m0 / HoWo
+    const int btile = m0 / p.HoWo;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int co = n0 + n * 32 + li;
+        const bool cv = co < p.Cout;
+        const int coc = cv ? co : 0;
+        const float bco = p.bias ? p.bias[coc] : 0.f;
+        const float bbt = (p.bias_b && one_img) ? p.bias_b[(size_t)btile * p.Cout + coc] : 0.f;
+        size_t oidx[16];
+        bool ok[16];
+        float add[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const int m = m0 + wv * 32 + row;
+            ok[r] = m < p.M && cv;
+            const int mm = m < p.M ? m : p.M - 1;
+            add[r] = bco + bbt;
+            if (dense_out) {
+                oidx[r] = (size_t)mm * p.Cout + coc;
+                if (p.bias_b && !one_img) add[r] += p.bias_b[(size_t)(mm / p.HoWo) * p.Cout + coc];
+            } else {
+                const int b = mm / p.HoWo;
+                const int rr = mm - b * p.HoWo;
+                const int oy = rr / p.Wo, ox = rr - (rr / p.Wo) * p.Wo;
+                oidx[r] = ((size_t)b * p.Hy * p.Wy + (size_t)(oy * p.osy + p.ooy) * p.Wy + (ox * p.osx + p.oox)) * p.Cout + coc;
+                if (p.bias_b) add[r] += p.bias_b[(size_t)b * p.Cout + coc] - bbt;
+            }
+        }
+        if (p.resid) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) add[r] += p.resid[oidx[r]];
+        }
+        double s = 0.0, ss = 0.0;
+        const float wsc = SPL ? *p.wscale : 1.f;
+        bool bad = false;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float v = (SPL ? acc[n][r] * wsc : acc[n][r]) + add[r];
+            if (p.act == 1) v = fmaxf(v, 0.f);
+            else if (p.act == 2) v = 1.f / (1.f + expf(-v));
+            else if (p.act == 3) v = silu_f(v);
+            if (p.out_h2) {
+                // h2 record of the pixel: lane pairs (2j, 2j+1) of an 8-channel group swap halves so
+                // the even lane stores the hi pair and the odd lane the lo pair (one dword each)
+                const unsigned sp = split1(v);
+                const bool odd = (li & 1) != 0;
+                const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
+                const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
+                const size_t pe = oidx[r] - (size_t)coc;  // pixel's first element
+                const int c8 = coc & ~7, j = (coc & 7) & ~1;
+                if (ok[r]) {
+                    *reinterpret_cast<unsigned*>(reinterpret_cast<char*>(p.y) + pe * 4 + (size_t)c8 * 4 + (odd ? 16 : 0) + 2 * j) = word;
+                    bad = bad || h2_bad(v);
+                }
+            } else if (ok[r]) {
+                p.y[oidx[r]] = v;
+            }
+            if (ok[r]) {
+                s += (double)v;
+                ss += (double)v * (double)v;
+            }
+        }
+        h2_flag(p.ovf, bad);
+        if (gn) {
+            s += __shfl_xor(s, 32);
+            ss += __shfl_xor(ss, 32);
+            if (lh == 0) {
+                red[(wv * BN + n * 32 + li) * 2 + 0] = s;
+                red[(wv * BN + n * 32 + li) * 2 + 1] = ss;
+            }
+        }
+    }
+    }
+    if (gn) {
+        __syncthreads();
+        for (int e = tid; e < (NW / 4) * BN; e += NW * 64) {
+            const int g = e / BN, cl = e - g * BN;  // 128-pixel group g of the tile, tile column cl
+            const int co = n0 + cl;
+            if (co < p.Cout) {
+                double s = 0.0, ss = 0.0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    s += red[((4 * g + w) * BN + cl) * 2 + 0];
+                    ss += red[((4 * g + w) * BN + cl) * 2 + 1];
+                }
+                const int mg = m0 + 128 * g;
+                const int b = mg / p.HoWo;
+                const int split = (mg - b * p.HoWo) / 128;
+                double* dst = p.gn + (((size_t)b * p.nsplit + split) * p.Cout + co) * 2;
+                dst[0] = s;
+                dst[1] = ss;
+            }
+        }
+    }
+}
+
+}  // namespace
+}  // namespace tcx

@@ -194,11 +194,15 @@ __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ x,
             };
             tr(a); tr(bq); tr(c); tr(d);
         }
+        // explicit fmaf: the same rounding in every instantiation (fp32 and h2 outputs)
+        auto bl = [&](float va, float vb, float vc, float vd) {
+            return fmaf(ly1, fmaf(lx1, vd, lx0 * vc), ly0 * fmaf(lx1, vb, lx0 * va));
+        };
         float4 o;
-        o.x = ly0 * (lx0 * a.x + lx1 * bq.x) + ly1 * (lx0 * c.x + lx1 * d.x);
-        o.y = ly0 * (lx0 * a.y + lx1 * bq.y) + ly1 * (lx0 * c.y + lx1 * d.y);
-        o.z = ly0 * (lx0 * a.z + lx1 * bq.z) + ly1 * (lx0 * c.z + lx1 * d.z);
-        o.w = ly0 * (lx0 * a.w + lx1 * bq.w) + ly1 * (lx0 * c.w + lx1 * d.w);
+        o.x = bl(a.x, bq.x, c.x, d.x);
+        o.y = bl(a.y, bq.y, c.y, d.y);
+        o.z = bl(a.z, bq.z, c.z, d.z);
+        o.w = bl(a.w, bq.w, c.w, d.w);
         if constexpr (OUTH2) {
             store4_h2(reinterpret_cast<char*>(y), (i / C4) * (size_t)C * 4, c4, o);
             bad = bad || h2_bad(o.x) || h2_bad(o.y) || h2_bad(o.z) || h2_bad(o.w);
