@@ -19,6 +19,8 @@
 // (conv_common.hpp), GroupNorm partials per 128-pixel half so the stats layout is unchanged.
 #include "conv_common.hpp"
 
+#include <type_traits>
+
 namespace tcx {
 namespace {
 
@@ -218,6 +220,226 @@ __global__ __launch_bounds__(64 * NW, 2) void k_conv3h(ConvParams p) {
     conv_epilogue<NT, true, NW>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_conv3w: the same halo scheme with one wave per SIMD and 64 x 96 outputs per wave (two 32-row
+// blocks x three 32-column blocks: 36 MFMAs per 32-deep chunk, B fragments re-used by both row
+// blocks, so half the LDS fragment reads per MFMA of k_conv3h).  Tile = 256 pixels x 96 channels,
+// 4 waves, one workgroup per CU (halo x2 + weight chunk x2 = 141.7 KB at W = 64).  The fragments
+// of chunk c+1 are read from LDS into a second register set while chunk c's MFMAs run, so after
+// each barrier the MFMAs start from registers.  Per iteration c: global loads of weight chunk c+2
+// (and at tap 0 of input chunk j the halo of j+1), 36 MFMAs interleaved with the reads of chunk
+// c+1's fragments, weight chunk c+2 -> LDS (and at tap 4 halo j+1 -> LDS), one barrier.
+// ---------------------------------------------------------------------------------------------
+template <int W, bool CIRC>
+__global__ __launch_bounds__(256, 1) void k_conv3w(ConvParams p) {
+    constexpr int NT = 3, BN = 96, RT = 2, NW = 4, NTHR = 256;
+    constexpr int HB = 32 * RT * NW;  // 256 output pixels
+    constexpr int W2 = W + 2;
+    constexpr int NPX = (HB / W + 2) * W2;
+    constexpr int HPI = (NPX * 8 + NTHR - 1) / NTHR;
+    constexpr int HBUF = NPX * HROW, BBUF = BN * HROW;
+    constexpr int BPI = BN * 8 / NTHR;  // 3
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* const Hs = sm;             // [2][NPX][HROW]
+    float* const Bs = sm + 2 * HBUF;  // [2][BN][HROW]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mblk = tile / p.n_nblk;
+    const int nblk = tile - mblk * p.n_nblk;
+    const int m0 = mblk * HB, n0 = nblk * BN;
+    const int b = m0 / p.HoWo;
+    const int r0 = (m0 - b * p.HoWo) / W;
+    const int bs = p.bmod > 0 ? b % p.bmod : b;
+    const int H = p.H;
+    const int cpt = p.Cin / BK;
+    const int nchunks = 9 * cpt;
+
+    const __amdgpu_buffer_rsrc_t r1 = mk_rsrc(p.x1, p.bytes1);
+    const __amdgpu_buffer_rsrc_t r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
+    const __amdgpu_buffer_rsrc_t rw = mk_rsrc(p.w, p.bytesw);
+
+    const int rowb = p.C1 * 4;
+    int hoff[HPI], hdst[HPI];
+#pragma unroll
+    for (int i = 0; i < HPI; ++i) {
+        const int e = tid + NTHR * i;
+        const int hp = e >> 3;
+        hoff[i] = kOOB;
+        hdst[i] = -1;
+        if (hp < NPX) {
+            const int hr = hp / W2, hc = hp - hr * W2;
+            int y = r0 + hr - 1, x = hc - 1;
+            bool ok = true;
+            if (CIRC) {
+                y = wrap_idx(y, H);
+                x = wrap_idx(x, W);
+            } else {
+                ok = y >= 0 && y < H && x >= 0 && x < W;
+            }
+            hoff[i] = ok ? ((bs * H + y) * W + x) * rowb + (e & 7) * 16 : kOOB;
+            hdst[i] = hp * HROW + (e & 7) * 4;
+        }
+    }
+    float4 hv[HPI];
+    auto halo_load = [&](int j) {
+        const int ci0 = j * BK;
+        const bool s1 = ci0 < p.C1;
+        const int cc = (s1 ? ci0 : ci0 - p.C1) * 4;
+        const __amdgpu_buffer_rsrc_t rs = s1 ? r1 : r2;
+#pragma unroll
+        for (int i = 0; i < HPI; ++i) hv[i] = bld4(rs, hoff[i], cc);
+    };
+    auto halo_store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < HPI; ++i)
+            if ((i + 1) * NTHR <= NPX * 8 || hdst[i] >= 0)
+                *reinterpret_cast<float4*>(&Hs[buf * HBUF + hdst[i]]) = hv[i];
+    };
+    float4 bv[BPI];
+    int boff[BPI];
+#pragma unroll
+    for (int i = 0; i < BPI; ++i) {
+        const int e = tid + NTHR * i;
+        boff[i] = ((n0 + (e >> 3)) * p.kpad) * 4 + (e & 7) * 16;
+    }
+    auto w_load = [&](int c) {
+        const int j = c / 9, t = c - 9 * j;
+        const int kb = (t * p.Cin + j * BK) * 4;
+#pragma unroll
+        for (int i = 0; i < BPI; ++i) bv[i] = bld4(rw, boff[i], kb);
+    };
+    auto w_store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < BPI; ++i) {
+            const int e = tid + NTHR * i;
+            *reinterpret_cast<float4*>(&Bs[buf * BBUF + (e >> 3) * HROW + (e & 7) * 4]) = bv[i];
+        }
+    };
+
+    // fragments: lane's A rows = tile pixels 64*wv + 32*rt + li
+    int abase[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int mloc = wv * 64 + rt * 32 + li;
+        abase[rt] = ((mloc / W) * W2 + (mloc % W)) * HROW + lh * 8;
+    }
+    const int bbase = li * HROW + lh * 8;
+    f32x16 acc[RT][NT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[rt][n] = (f32x16){};
+    // two register sets of fragments [set][rt or n][step]
+    h8 ah[2][RT][2], al[2][RT][2], bh[2][NT][2], bl[2][NT][2];
+    auto rd = [&](auto SET, int hbuf, int tap, int bbuf) {
+        constexpr int st = decltype(SET)::value;
+        const int dy = tap / 3, dx = tap - 3 * (tap / 3);
+        const int toff = hbuf * HBUF + (dy * W2 + dx) * HROW;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const float* A = &Hs[toff + abase[rt] + 16 * s];
+                ah[st][rt][s] = __builtin_bit_cast(h8, ld4(A));
+                al[st][rt][s] = __builtin_bit_cast(h8, ld4(A + 4));
+            }
+            const float* B = &Bs[bbuf * BBUF + bbase + 16 * s];
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                bh[st][n][s] = __builtin_bit_cast(h8, ld4(B + n * 32 * HROW));
+                bl[st][n][s] = __builtin_bit_cast(h8, ld4(B + n * 32 * HROW + 4));
+            }
+        }
+    };
+    auto mf = [&](auto SET) {
+        constexpr int st = decltype(SET)::value;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int n = 0; n < NT; ++n) {
+                    acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[st][rt][s], bl[st][n][s], acc[rt][n], 0, 0, 0);
+                    acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[st][rt][s], bh[st][n][s], acc[rt][n], 0, 0, 0);
+                    acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[st][rt][s], bh[st][n][s], acc[rt][n], 0, 0, 0);
+                }
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    // one iteration: chunk c = 9 j + t computed from register set CS; chunk c+1 read into CS ^ 1
+    auto iter = [&](int j, auto T, auto CS) {
+        constexpr int t = decltype(T)::value;
+        constexpr int cs = decltype(CS)::value;
+        using NS = std::integral_constant<int, cs ^ 1>;
+        const int c = 9 * j + t;
+        if (c + 2 < nchunks) w_load(c + 2);
+        if (t == 0 && j + 1 < cpt) halo_load(j + 1);
+        mf(CS);
+        if (t < 8) rd(NS{}, j & 1, t + 1, (c + 1) & 1);
+        else rd(NS{}, (j + 1) & 1, 0, (c + 1) & 1);
+        if (t == 4 && j + 1 < cpt) halo_store((j + 1) & 1);
+        w_store(c & 1);  // weight chunk c + 2 (its slot held chunk c, read during iteration c - 1)
+        __syncthreads();
+    };
+    auto nine = [&](int j, auto E) {  // E: register set of the even taps
+        using O = std::integral_constant<int, decltype(E)::value ^ 1>;
+        iter(j, std::integral_constant<int, 0>{}, E);
+        iter(j, std::integral_constant<int, 1>{}, O{});
+        iter(j, std::integral_constant<int, 2>{}, E);
+        iter(j, std::integral_constant<int, 3>{}, O{});
+        iter(j, std::integral_constant<int, 4>{}, E);
+        iter(j, std::integral_constant<int, 5>{}, O{});
+        iter(j, std::integral_constant<int, 6>{}, E);
+        iter(j, std::integral_constant<int, 7>{}, O{});
+        iter(j, std::integral_constant<int, 8>{}, E);
+    };
+
+    // prologue: halo 0, weight chunks 0 and 1 in LDS; chunk 0's fragments in set 0
+    halo_load(0);
+    w_load(0);
+    halo_store(0);
+    w_store(0);
+    w_load(nchunks > 1 ? 1 : 0);
+    w_store(1);
+    __syncthreads();
+    rd(S0{}, 0, 0, 0);
+    int j = 0;
+    for (; j + 1 < cpt; j += 2) {
+        nine(j, S0{});
+        nine(j + 1, S1{});
+    }
+    if (j < cpt) nine(j, S0{});
+
+    __syncthreads();  // halo buffers -> epilogue scratch
+    double* red = reinterpret_cast<double*>(sm);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) conv_epi_store<NT, true, 2 * NW>(p, acc[rt], m0, n0, 2 * wv + rt, lane, red);
+    if (p.gn) {
+        __syncthreads();
+        conv_epi_gn<NT, 2 * NW>(p, m0, n0, tid, NTHR, red);
+    }
+}
+
+template <int W>
+int launch3w(const ConvParams& p, hipStream_t st) {
+    constexpr size_t shm = (size_t)(2 * ((256 / W + 2) * (W + 2)) + 2 * 96) * HROW * sizeof(float);
+    static bool attr[2] = {false, false};
+    auto kc = p.circular ? &k_conv3w<W, true> : &k_conv3w<W, false>;
+    if (!attr[p.circular ? 1 : 0]) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)shm) != hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", shm);
+            return TCX_EHIP;
+        }
+        attr[p.circular ? 1 : 0] = true;
+    }
+    const int grid = (p.M / 256) * p.n_nblk;
+    hipLaunchKernelGGL(kc, dim3(grid), dim3(256), shm, st, p);
+    return check_launch("tcx_conv2d_h2(halo, wide)");
+}
+
 template <int NT, int W, int NW>
 int launch3h_w(const ConvParams& p, hipStream_t st) {
     constexpr size_t shm = conv3h_lds_bytes(NT, W, NW);
@@ -236,12 +458,13 @@ int launch3h_w(const ConvParams& p, hipStream_t st) {
     return check_launch("tcx_conv2d_h2(halo)");
 }
 
-// waves per workgroup: TCX_HALO_NW=8 (256-pixel tiles, one workgroup per CU) or 4 (default:
-// 128-pixel tiles, two workgroups per CU so one's prologue/epilogue overlaps the other's MFMAs)
+// variant: TCX_HALO_NW=8 (k_conv3h, 256-pixel tiles of 8 waves, one workgroup per CU), 4 (k_conv3h,
+// 128-pixel tiles, two workgroups per CU) or 0 (default: k_conv3w, 256-pixel tiles of 4 wide waves)
 int halo_nw() {
     static const int nw = [] {
         const char* e = getenv("TCX_HALO_NW");
-        return (e && atoi(e) == 8) ? 8 : 4;
+        const int v = e ? atoi(e) : 0;
+        return v == 8 ? 8 : (v == 4 ? 4 : 0);
     }();
     return nw;
 }
@@ -252,8 +475,8 @@ int halo_nw() {
 bool conv3h_applies(const ConvParams& p, int cout_pad) {
     static const bool off = getenv("TCX_NO_HALO") != nullptr;
     return !off && p.ks == 3 && p.stride == 1 && p.pad_y == 1 && p.pad_x == 1 && p.Hi == p.H && p.Wi == p.W &&
-           (p.W == 16 || p.W == 32 || p.W == 64) && p.H % (32 * halo_nw() / p.W) == 0 &&
-           p.HoWo % (32 * halo_nw()) == 0 &&
+           (p.W == 16 || p.W == 32 || p.W == 64) && p.H % ((halo_nw() ? 32 * halo_nw() : 256) / p.W) == 0 &&
+           p.HoWo % (halo_nw() ? 32 * halo_nw() : 256) == 0 &&
            cout_pad % 96 == 0 && p.Cin % BK == 0 && p.C1 % BK == 0 && (p.C2 == 0 || p.C2 == p.C1) &&
            p.kpad == 9 * p.Cin && p.osy == 1 && p.osx == 1;
 }
@@ -263,7 +486,11 @@ int launch_conv3h(ConvParams& p, int cout_pad, hipStream_t st) {
     if (p.M == 0) return TCX_OK;
     prof_begin(st);
     int rc;
-    if (halo_nw() == 8) {
+    if (halo_nw() == 0) {
+        if (p.W == 64) rc = launch3w<64>(p, st);
+        else if (p.W == 32) rc = launch3w<32>(p, st);
+        else rc = launch3w<16>(p, st);
+    } else if (halo_nw() == 8) {
         if (p.W == 64) rc = launch3h_w<3, 64, 8>(p, st);
         else if (p.W == 32) rc = launch3h_w<3, 32, 8>(p, st);
         else rc = launch3h_w<3, 16, 8>(p, st);

@@ -92,11 +92,13 @@ __device__ __forceinline__ void bilin_axis(int d, int n, int& i0, int& i1, float
 // n0 + [0, 32*NT).  C/D map of the 32x32 MFMAs: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
 // bias / per-batch bias / residual / activation, fp32 or h2 store, and the fp64 GroupNorm partials
 // of every 128-pixel group of waves (4 waves each; red: LDS scratch [NW][32*NT][2] doubles).
+// conv_epi_store: one wave's 32 x 32*NT block (NW = waves of 32 rows in the tile, virtual waves
+// when a wave owns several row blocks); conv_epi_gn: the per-128-pixel-group reduction of the
+// partials in `red`, after a barrier.
 template <int NT, bool SPL, int NW>
-__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x16 (&acc)[NT], int m0, int n0, int wv,
-                                              int tid, double* red) {
+__device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc)[NT], int m0, int n0, int wv,
+                                               int lane, double* red) {
     constexpr int BN = 32 * NT;
-    const int lane = tid & 63;
     const int li = lane & 31;
     const int lh = lane >> 5;
     const bool gn = p.gn != nullptr;
@@ -228,9 +230,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x16 (&acc)
         }
     }
     }
-    if (gn) {
-        __syncthreads();
-        for (int e = tid; e < (NW / 4) * BN; e += NW * 64) {
+}
+
+template <int NT, int NW>
+__device__ __forceinline__ void conv_epi_gn(const ConvParams& p, int m0, int n0, int tid, int nthr,
+                                            const double* red) {
+    constexpr int BN = 32 * NT;
+    {
+        for (int e = tid; e < (NW / 4) * BN; e += nthr) {
             const int g = e / BN, cl = e - g * BN;  // 128-pixel group g of the tile, tile column cl
             const int co = n0 + cl;
             if (co < p.Cout) {
@@ -248,6 +255,16 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x16 (&acc)
                 dst[1] = ss;
             }
         }
+    }
+}
+
+template <int NT, bool SPL, int NW>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x16 (&acc)[NT], int m0, int n0, int wv,
+                                              int tid, double* red) {
+    conv_epi_store<NT, SPL, NW>(p, acc, m0, n0, wv, tid & 63, red);
+    if (p.gn) {
+        __syncthreads();
+        conv_epi_gn<NT, NW>(p, m0, n0, tid, NW * 64, red);
     }
 }
 

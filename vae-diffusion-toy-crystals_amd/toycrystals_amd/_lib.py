@@ -13,6 +13,11 @@ import os
 
 import torch  # noqa: F401  (must be loaded before libtcx: shared HIP runtime)
 
+# 3x3 halo-conv variant (csrc/conv3h.hip halo_nw): 4 = k_conv3h with two 128-pixel workgroups per
+# CU (the measured fastest, profiles/r01_s); 0 = the wide-wave k_conv3w, still work in progress
+# (its register demand spills to scratch). Read by libtcx at first use; an explicit setting wins.
+os.environ.setdefault("TCX_HALO_NW", "4")
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtcx.so")
 
