@@ -109,6 +109,16 @@ int tcx_gn_apply_tab(const float* x, float* y, int Bt, int HW, int C, const floa
 int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, int C, const float* scale,
                    const float* shift, void* stream);
 
+/* ------------------------------------------------------------------ procedural dataset
+ * Toy-crystal renderer (ToyCrystalsDataset, /root/reference/src/toycrystals/data.py:132-153 +
+ * :204-206, and the uint8 quantisation of scripts/build_dataset.py:34): for each image b, atoms
+ * pts[offsets[b] .. offsets[b+1]) ([*][2] fp32 (x, y) pixel coordinates, from the host point
+ * generator), s2[b] = fp32(2 sigma^2):  v(y, x) = sum_atoms exp(-((x-ax)^2 + (y-ay)^2) / s2[b]),
+ * x = clamp(v / (max v + 1e-8), 0, 1) -> x_out [n_img][H][W] fp32 and/or
+ * u8_out [n_img][H][W] = (uint8)(x * 255).  H*W <= 16384. */
+int tcx_render_crystals(const float* pts, const int* offsets, const float* s2, int n_img, int H, int W,
+                        float* x_out, unsigned char* u8_out, void* stream);
+
 /* ------------------------------------------------------------------ f16x3 split path
  * "h2" storage (csrc/h2.hpp): an fp32 tensor [..][C] (C % 8 == 0) kept as [..][C/8][2][8] f16
  * = per 8-channel group 8 hi halves then 8 lo halves (hi = f16(v), lo = f16(v - hi)), four bytes

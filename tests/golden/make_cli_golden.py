@@ -13,7 +13,7 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SCRIPTS = ["train_sde_score_model", "sample_sde_score_model", "train_vae", "train_diffusion_prior"]
+SCRIPTS = ["train_sde_score_model", "sample_sde_score_model", "train_vae", "train_diffusion_prior", "build_dataset"]
 
 
 class _Captured(Exception):

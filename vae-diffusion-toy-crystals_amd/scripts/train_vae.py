@@ -3,8 +3,8 @@
 kl_stats (:17-36), loss (:309-312), outputs checkpoints/vae_last.pt (state_dict) and
 results/{vae_recon, vae_samples_prior, vae_samples_mop, vae_loss}.png.
 
-The in-memory renderer (`--data-path ""`, toycrystals.data.ToyCrystalsDataset) is outside this
-build's scope: a disk dataset from the reference's build_dataset.py is required.
+`--data-path ""` renders the reference's in-memory dataset (toycrystals.data.ToyCrystalsDataset,
+non-rot-only, seed --seed) on the GPU once (toycrystals_amd.data, csrc/render.hip) and keeps it in HBM.
 """
 from __future__ import annotations
 
@@ -17,6 +17,7 @@ import torch
 
 from toycrystals_amd import functional as TF
 from toycrystals_amd.dist import allreduce_grads_
+from toycrystals_amd.data import ToyCrystalsDataset
 from toycrystals_amd.disk_data import DeviceBatches, ToyCrystalsDiskDataset
 from toycrystals_amd.models.vae import CondVAE, VAE
 from toycrystals_amd.optim import Adam
@@ -158,10 +159,11 @@ def main() -> int:
     lead = rank == 0
     os.makedirs("results", exist_ok=True)
     os.makedirs("checkpoints", exist_ok=True)
-    if not args.data_path:
-        raise SystemExit("the procedural renderer (--data-path '') is not part of this build; build a dataset "
-                         "with the reference's scripts/build_dataset.py and pass --data-path")
-    ds = ToyCrystalsDiskDataset(args.data_path)
+    if args.data_path:
+        ds = ToyCrystalsDiskDataset(args.data_path)
+    else:  # the reference's in-memory renderer (:259-260): non-rot-only, generator seed --seed
+        ds = ToyCrystalsDataset(n_samples=args.n_samples, img_size=args.img_size, seed=args.seed,
+                                device=device).materialize()
     dl = DeviceBatches(ds, args.batch_size, device, shuffle=True, drop_last=True, rank=rank, world=world)
     if args.uncond:
         model = VAE(z_dim=args.z_dim).to(device)

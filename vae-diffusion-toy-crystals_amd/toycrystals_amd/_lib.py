@@ -139,6 +139,7 @@ _SIGS = {
     "tcx_ddim_step": (c_int, [c_fp, c_fp, c_size, c_float, c_float, c_int, c_fp]),
     "tcx_q_sample": (c_int, [c_fp, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_fp, c_fp]),
     "tcx_u8_gather": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp]),
+    "tcx_render_crystals": (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
 }
 
 _lib = None

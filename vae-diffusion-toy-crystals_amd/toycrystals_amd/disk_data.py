@@ -45,12 +45,16 @@ class DeviceBatches:
         if batch_size % world != 0:
             raise ValueError(f"global batch {batch_size} must be divisible by world size {world}")
         self.device = torch.device(device)
-        self.x_u8 = ds.x_u8.to(self.device).contiguous()
+        # float images (toycrystals_amd.data.RenderedSet, the in-memory renderer) or uint8 (disk)
+        xf = getattr(ds, "x_f32", None)
+        self.x_f32 = xf.to(self.device).contiguous() if xf is not None else None
+        self.x_u8 = ds.x_u8.to(self.device).contiguous() if xf is None else None
+        xs = self.x_f32 if xf is not None else self.x_u8
         self.y_cat = ds.y_cat.to(self.device, torch.int64).contiguous()
         self.y_cont = ds.y_cont.to(self.device, torch.float32).contiguous()
-        self.N = int(self.x_u8.shape[0])
-        self.shape = tuple(self.x_u8.shape[1:])
-        self.npix = int(self.x_u8[0].numel())
+        self.N = int(xs.shape[0])
+        self.shape = tuple(xs.shape[1:])
+        self.npix = int(xs[0].numel())
         self.batch_size, self.shuffle, self.drop_last = int(batch_size), shuffle, drop_last
         self.rank, self.world = rank, world
         self.generator = generator
@@ -70,6 +74,9 @@ class DeviceBatches:
             per = g.shape[0] // self.world
             idx = g[self.rank * per:(self.rank + 1) * per].contiguous() if self.world > 1 else g.contiguous()
             B = idx.shape[0]
-            x = torch.empty((B,) + self.shape, device=self.device, dtype=torch.float32)
-            check(L.tcx_u8_gather(ptr(self.x_u8), ptr(idx), B, self.npix, ptr(x), st), "tcx_u8_gather")
+            if self.x_f32 is not None:
+                x = self.x_f32.index_select(0, idx)
+            else:
+                x = torch.empty((B,) + self.shape, device=self.device, dtype=torch.float32)
+                check(L.tcx_u8_gather(ptr(self.x_u8), ptr(idx), B, self.npix, ptr(x), st), "tcx_u8_gather")
             yield x, self.y_cat.index_select(0, idx), self.y_cont.index_select(0, idx)
