@@ -298,6 +298,7 @@ struct StepArgs {
     float* eps_out;
     const float* z;
     uint64_t seed, step;
+    size_t e0;  // element offset of this batch chunk (Philox counter = e0 + i: chunking-invariant noise)
 };
 
 __device__ __forceinline__ float gather_eps(const float* __restrict__ rb, int HW, int W, int H, int y, int x,
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
             const float xv = a.x_inout[i];
             const float score = -eps / sigma;
             const float drift = ((-0.5f * beta) * xv) - (beta * score);
-            const float z = a.z ? a.z[i] : philox_normal(a.seed, a.step + 1, i);
+            const float z = a.z ? a.z[i] : philox_normal(a.seed, a.step + 1, a.e0 + i);
             a.x_inout[i] = (xv + drift * dt) + (g * sq) * z;
         } else if (a.mode == 2) {
             // final projection (sde_score_model.py:562-569)
@@ -630,6 +631,22 @@ int launch_step(const StepArgs& a, hipStream_t st) {
     return check_launch("k_step");
 }
 
+// Batch chunking: one evaluation of B images can run as ceil(B / Bc) passes of Bc images (2*Bc
+// U-Net rows with CFG; per-image arithmetic unchanged: GroupNorm is per sample, CFG pairs stay in
+// one pass, in-kernel noise is keyed by the global element index).  Meant to keep a pass's
+// producer -> consumer hand-offs inside the 256 MB Infinity Cache; measured at B = 128
+// (profiles/r01_w_chunk_ab.txt) it LOSES: 59.9 img/s unchunked vs 56.6 / 49.3 / 37.2 at
+// Bc = 64 / 32 / 16 (the smaller conv grids lose more than the memory-bound passes gain), so the
+// default is one pass.  TCX_BATCH_CHUNK=<images> selects chunking (e.g. to bound the workspace).
+int chunk_images(int B) {
+    static const int env = [] {
+        const char* e = getenv("TCX_BATCH_CHUNK");
+        return e ? atoi(e) : -1;
+    }();
+    const int c = env < 0 ? 0 : env;
+    return (c <= 0 || c >= B) ? B : c;
+}
+
 }  // namespace
 }  // namespace tcx
 
@@ -637,7 +654,9 @@ using namespace tcx;
 
 extern "C" size_t tcx_unet_workspace_size(const tcx_unet* net, int Bt, int H, int W) {
     if (!net) return 0;
-    return make_plan(net, Bt, H, W, nullptr).bytes + 256;
+    // Bt = B or 2B (CFG): size for the largest pass of either reading
+    const int Btc = std::min(Bt, 2 * chunk_images(Bt));
+    return make_plan(net, Btc, H, W, nullptr).bytes + 256;
 }
 
 extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, const float* t, int t_per_sample,
@@ -652,17 +671,29 @@ extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, con
     TCX_REQUIRE((mode != 1 && mode != 3 && mode != 4) || x_inout, "tcx_unet_eval: x_inout needed");
     TCX_REQUIRE(mode != 3 || x2, "tcx_unet_eval: Heun stage 1 needs x2");
     const int cfg = guidance > 0.f ? 1 : 0;
-    const int Bt = cfg ? 2 * B : B;
+    const int Bc = chunk_images(B);
+    const int Btc = cfg ? 2 * Bc : Bc;
     char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
-    Plan P = make_plan(net, Bt, H, W, base);
-    TCX_REQUIRE(P.bytes + (base - (char*)ws) <= ws_bytes, "tcx_unet_eval: workspace too small (%zu < %zu)", ws_bytes,
-                P.bytes + 256);
+    const size_t need = make_plan(net, Btc, H, W, nullptr).bytes;
+    TCX_REQUIRE(need + (base - (char*)ws) <= ws_bytes, "tcx_unet_eval: workspace too small (%zu < %zu)", ws_bytes,
+                need + 256);
     hipStream_t st = (hipStream_t)stream;
-    TCX_TRY(unet_body(net, P, x, B, t, t_per_sample, y_cat, y_cont, cfg, st));
-    StepArgs a{};
-    a.r = P.r; a.out_b = net->out_b; a.B = B; a.H = H; a.W = W; a.cfg = cfg; a.guidance = guidance; a.mode = mode;
-    a.scal = scal; a.x = x; a.x_inout = x_inout; a.x2 = x2; a.eps_out = eps_out; a.z = z; a.seed = seed; a.step = step;
-    return launch_step(a, st);
+    const size_t HW = (size_t)H * W;
+    for (int c0 = 0; c0 < B; c0 += Bc) {
+        const int bc = std::min(Bc, B - c0);
+        const int Bt = cfg ? 2 * bc : bc;
+        Plan P = make_plan(net, Bt, H, W, base);
+        const size_t e0 = (size_t)c0 * HW;
+        TCX_TRY(unet_body(net, P, x + e0, bc, t_per_sample ? t + c0 : t, t_per_sample, y_cat + c0,
+                          y_cont + (size_t)c0 * net->y_cont_dim, cfg, st));
+        StepArgs a{};
+        a.r = P.r; a.out_b = net->out_b; a.B = bc; a.H = H; a.W = W; a.cfg = cfg; a.guidance = guidance;
+        a.mode = mode; a.scal = scal; a.x = x + e0; a.x_inout = x_inout ? x_inout + e0 : nullptr;
+        a.x2 = x2 ? x2 + e0 : nullptr; a.eps_out = eps_out ? eps_out + e0 : nullptr; a.z = z ? z + e0 : nullptr;
+        a.seed = seed; a.step = step; a.e0 = e0;
+        TCX_TRY(launch_step(a, st));
+    }
+    return TCX_OK;
 }
 
 extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
