@@ -44,6 +44,13 @@ FWD_PER_IMG = 602                # 300 steps x 2 CFG evaluations + 2 for the fin
 FP32_PEAK_TFLOPS = 157.3         # MI355X fp32 MFMA (= vector) peak, MI355X_MICROARCH.md
 F16_PEAK_TFLOPS = 2500.0         # MI355X dense f16/bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 multiply-add
+# HBM bytes per conv launch (the launches the roofline times), measured by rocprofv3 PMC passes on
+# this sampler (tools/gpu/pmc_bench_traffic.sh -> tools/pmc_traffic.py, profiles/r01_x_pmc_traffic.txt):
+# FETCH_SIZE x 2 (gfx950 reports half of 16-B/lane reads) + WRITE_SIZE, averaged over the k_conv<>
+# and k_conv3h<> launches of an evaluation.  A counter pass cannot run inside this process, so the
+# measured value is carried here with its source; it applies to the f16x3 path it was taken on.
+TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 595.7e6}
+TRAFFIC_SOURCE = "rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE, profiles/r01_x_pmc_traffic.txt"
 
 
 def cpu_baseline(state_dict, B: int, n_steps: int, cfg: float, t_end: float) -> dict:
@@ -174,7 +181,9 @@ def main() -> int:
                    "parallelism": "replicas" if world == 1 else f"dp{world} (independent shards)"},
         "path_tflops": round(value / world * FWD_PER_IMG * GFLOP_PER_IMG_FWD / 1e3, 3),
         "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": round(peak, 1),
-                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                     "traffic": TRAFFIC_BYTES_PER_CONV_LAUNCH.get(args.precision),
+                     "traffic_unit": "HBM bytes per conv launch", "traffic_source": TRAFFIC_SOURCE,
                      "peak_basis": peak_basis,
                      "avg_launch_ms": round(conv_avg_ms, 5), "avg_launch_gflop": round(conv_avg_flop / 1e9, 4),
                      "launches": n.value,
