@@ -89,6 +89,8 @@ def main() -> int:
     ap.add_argument("--cfg", type=float, default=1.5)
     ap.add_argument("--t-end", type=float, default=0.005)
     ap.add_argument("--base-ch", type=int, default=96)
+    ap.add_argument("--img-size", type=int, default=64,
+                    help="64 (the metric's config 2); 256 with --batch 64 = config 5's per-GPU share (512 over 8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -116,7 +118,8 @@ def main() -> int:
     y_cat = (torch.arange(B) % 4).to(device)
     y_cont = torch.zeros(B, 4, device=device)
     y_cont[:, 1] = torch.linspace(0.0, math.pi / 3.0, B, device=device)
-    shape = (B, 1, 64, 64)
+    S = args.img_size
+    shape = (B, 1, S, S)
 
     def run(i: int) -> torch.Tensor:
         return sample_reverse_sde_euler_maruyama(model, sde, y_cat, y_cont, shape, n_steps=args.n_steps,
@@ -175,14 +178,14 @@ def main() -> int:
         "dtype": "fp32" if args.precision == "fp32" else "fp32 (f16x3 split MFMA, fp32-grade)",
         "data": "synthetic (y_cat=i%4, theta=linspace(0,pi/3,B); random-init weights seed 0; Philox noise)",
         "config": {"workload": f"reverse-SDE {args.n_steps} steps, CFG {args.cfg}, t_end {args.t_end}, "
-                               f"CondUNetTiny(base_ch={args.base_ch}) 64x64, batch {B}/GPU",
+                               f"CondUNetTiny(base_ch={args.base_ch}) {S}x{S}, batch {B}/GPU",
                    "batch_per_gpu": B, "global_batch": world * B, "n_steps": args.n_steps, "cfg": args.cfg,
-                   "image": [1, 64, 64], "conv_precision": args.precision,
+                   "image": [1, S, S], "conv_precision": args.precision,
                    "parallelism": "replicas" if world == 1 else f"dp{world} (independent shards)"},
-        "path_tflops": round(value / world * FWD_PER_IMG * GFLOP_PER_IMG_FWD / 1e3, 3),
+        "path_tflops": round(value / world * FWD_PER_IMG * GFLOP_PER_IMG_FWD / 1e3, 3) if S == 64 else None,
         "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": round(peak, 1),
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                     "traffic": TRAFFIC_BYTES_PER_CONV_LAUNCH.get(args.precision),
+                     "traffic": TRAFFIC_BYTES_PER_CONV_LAUNCH.get(args.precision) if S == 64 else None,
                      "traffic_unit": "HBM bytes per conv launch", "traffic_source": TRAFFIC_SOURCE,
                      "peak_basis": peak_basis,
                      "avg_launch_ms": round(conv_avg_ms, 5), "avg_launch_gflop": round(conv_avg_flop / 1e9, 4),

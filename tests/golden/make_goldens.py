@@ -461,6 +461,9 @@ def main() -> int:
         gen_unet(16, 3, "unet16_b3", store_weights=True)
         gen_unet(96, 2, "unet96_b2", store_weights=False)
         gen_unet(32, 2, "unet32_b2_h32", store_weights=False, H=32)
+    if want("unet256"):
+        # config 5's resolution: 64x64 = 4096 tokens at the attention level (key-tiled kernel)
+        gen_unet(96, 2, "unet96_b2_h256", store_weights=False, H=256)
     if want("cfg"):
         gen_cfg("cfg16_b3")
     if want("vpsde"):

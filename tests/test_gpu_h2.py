@@ -197,8 +197,8 @@ def test_upsample_h2():
     dec_ok(from_h2(y).cpu().numpy(), y32.cpu().numpy())
 
 
-def test_attention_h2():
-    Bt, N, C, heads = 2, 256, 192, 4
+@pytest.mark.parametrize("Bt,N,C,heads", [(2, 256, 192, 4), (1, 4096, 192, 4), (2, 1024, 64, 4)])
+def test_attention_h2(Bt, N, C, heads):
     qkv = dev(rng.standard_normal((Bt, N, 3 * C)))
     o = torch.empty((Bt, N, C), device="cuda")
     o32 = torch.empty_like(o)

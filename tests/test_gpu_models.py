@@ -50,7 +50,7 @@ def rel_err(a, ref):
 
 
 @pytest.mark.parametrize("name,base,stored", [("unet16_b3", 16, True), ("unet96_b2", 96, False),
-                                              ("unet32_b2_h32", 32, False)])
+                                              ("unet32_b2_h32", 32, False), ("unet96_b2_h256", 96, False)])
 @pytest.mark.parametrize("grad", [False, True], ids=["fused", "autograd"])
 def test_unet_forward_vs_reference(golden, name, base, stored, grad, prec):
     """The fused evaluator (no grad) and the autograd training chain (grad) against the reference."""
@@ -96,6 +96,25 @@ def test_batch_independence_and_oracle_at_full_size(prec):
     o = ScoreUNet({k: v.cpu().numpy() for k, v in m.state_dict().items()}, dt=np.float64)
     ref = o_cfg(o, x[idx].double().numpy(), t[idx].numpy(), y_cat[idx].numpy(), y_cont[idx].numpy(), 1.5)
     assert rel_err(e[idx].numpy(), ref) < 2e-5
+
+
+def test_256px_pass_chunking_is_batch_independent():
+    """256x256 (config 5) with CFG: B=48 doubles to 96 rows, above the 84-image cap that keeps every
+    activation under 2 GiB (32-bit buffer offsets), so the evaluator runs two passes (42 + 6
+    images).  Every sample must equal the same sample evaluated alone."""
+    from toycrystals_amd.models.sde_score_model import predict_eps_cfg
+    m = unet(96)
+    B = 48
+    gen = torch.Generator().manual_seed(9)
+    x = torch.randn(B, 1, 256, 256, generator=gen)
+    t = torch.rand(B, generator=gen) * 0.9 + 0.05
+    y_cat = torch.arange(B) % 5
+    y_cont = torch.rand(B, 4, generator=gen)
+    e = predict_eps_cfg(m, x.cuda(), t.cuda(), y_cat.cuda(), y_cont.cuda(), 1.5).cpu()
+    assert torch.isfinite(e).all()
+    for idx in ([0], [41, 42], [47]):
+        e1 = predict_eps_cfg(m, x[idx].cuda(), t[idx].cuda(), y_cat[idx].cuda(), y_cont[idx].cuda(), 1.5).cpu()
+        assert torch.allclose(e[idx], e1, atol=1e-5, rtol=0)
 
 
 @pytest.mark.parametrize("name", ["sde16_3step", "sde96_2step_b2"])

@@ -253,7 +253,9 @@ def test_gn_finalize_tables():
     close(got, nn_np.group_norm(x, groups, gm, bt))
 
 
-@pytest.mark.parametrize("B,C,N,heads", [(2, 192, 256, 4), (3, 32, 256, 4), (2, 64, 64, 4)])
+@pytest.mark.parametrize("B,C,N,heads", [(2, 192, 256, 4), (3, 32, 256, 4), (2, 64, 64, 4),
+                                          # N > 256: key-tiled online-softmax kernel (256x256 images)
+                                          (1, 192, 4096, 4), (2, 64, 512, 4), (1, 128, 1024, 2), (1, 96, 768, 2)])
 def test_attention(B, C, N, heads):
     qkv = rng.standard_normal((B, N, 3 * C))
     d = C // heads

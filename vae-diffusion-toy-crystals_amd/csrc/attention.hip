@@ -146,6 +146,147 @@ __global__ __launch_bounds__(512) void k_attention_mfma(const float* __restrict_
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Key-tiled (flash) form for long sequences (the 256x256 U-Net's bottleneck: N = 64*64 = 4096):
+// grid (N/256 query blocks, heads, Bt), 8 waves x 32 queries; K and V staged in LDS 128 keys at a
+// time; per query (on the lane) a running max m, sum l and O^T accumulators rescaled by
+// exp((m_old - m_new) * scale) when a tile raises the max.  Same fp32 MFMA products as
+// k_attention_mfma; exact softmax up to the rescaling roundings.
+// ---------------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(512) void k_attention_flash(const float* __restrict__ qkv, float* __restrict__ out, int N,
+                                                         int C, float scale, int out_h2, unsigned* ovf) {
+    constexpr int HD = D / 2;
+    constexpr int KS = D + 4;
+    constexpr int DT = (D + 31) / 32;
+    constexpr int VS = DT * 32;
+    constexpr int KT = 128;        // keys per staged tile
+    constexpr int NST = KT / 32;   // 32-key sub-tiles
+    __shared__ __attribute__((aligned(16))) float Ks[KT * KS];
+    __shared__ __attribute__((aligned(16))) float Vs[KT * VS];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int tid = threadIdx.x;
+    const size_t rs = 3 * (size_t)C;
+    const float* base = qkv + (size_t)b * N * rs;
+    constexpr int D4 = D / 4;
+    const int lane = tid & 63, w = tid >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    const int q = blockIdx.x * 256 + w * 32 + li;
+    float qf[HD];
+    {
+        const float* qs = base + (size_t)q * rs + h * D + HD * lh;
+#pragma unroll
+        for (int s4 = 0; s4 < HD / 4; ++s4) {
+            const float4 v = *reinterpret_cast<const float4*>(qs + 4 * s4);
+            qf[4 * s4 + 0] = v.x; qf[4 * s4 + 1] = v.y; qf[4 * s4 + 2] = v.z; qf[4 * s4 + 3] = v.w;
+        }
+    }
+    if (VS > D) {
+        for (int i = tid; i < KT * (VS - D); i += 512) {
+            const int j = i / (VS - D), e = i - (i / (VS - D)) * (VS - D);
+            Vs[j * VS + D + e] = 0.f;
+        }
+    }
+    f32x16 oacc[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) oacc[t] = (f32x16){};
+    float m = -INFINITY, l = 0.f;
+    for (int k0 = 0; k0 < N; k0 += KT) {
+        __syncthreads();  // previous tile fully consumed
+        for (int i = tid; i < KT * D4; i += 512) {
+            const int j = i / D4, d4 = i - (i / D4) * D4;
+            const float* src = base + (size_t)(k0 + j) * rs + h * D + d4 * 4;
+            *reinterpret_cast<float4*>(Ks + j * KS + d4 * 4) = *reinterpret_cast<const float4*>(src + C);
+            *reinterpret_cast<float4*>(Vs + j * VS + d4 * 4) = *reinterpret_cast<const float4*>(src + 2 * C);
+        }
+        __syncthreads();
+        f32x16 sacc[NST];
+#pragma unroll
+        for (int n = 0; n < NST; ++n) {
+            sacc[n] = (f32x16){};
+            const float* kr = Ks + (n * 32 + li) * KS + HD * lh;
+#pragma unroll
+            for (int s4 = 0; s4 < HD / 4; ++s4) {
+                const float4 kv = *reinterpret_cast<const float4*>(kr + 4 * s4);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qf[4 * s4 + 0], sacc[n], 0, 0, 0);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qf[4 * s4 + 1], sacc[n], 0, 0, 0);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qf[4 * s4 + 2], sacc[n], 0, 0, 0);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qf[4 * s4 + 3], sacc[n], 0, 0, 0);
+            }
+        }
+        float mt = -INFINITY;
+#pragma unroll
+        for (int n = 0; n < NST; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sacc[n][r]);
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float mn = fmaxf(m, mt);
+        const float alpha = expf((m - mn) * scale);  // 0 on the first tile (m = -inf)
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[t][r] *= alpha;
+        float lt = 0.f;
+#pragma unroll
+        for (int n = 0; n < NST; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float pv = expf((sacc[n][r] - mn) * scale);
+                sacc[n][r] = pv;
+                lt += pv;
+            }
+        lt += __shfl_xor(lt, 32);
+        l += lt;
+#pragma unroll
+        for (int n = 0; n < NST; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = n * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const float* vr = Vs + key * VS + li;
+#pragma unroll
+                for (int t = 0; t < DT; ++t)
+                    oacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr[t * 32], sacc[n][r], oacc[t], 0, 0, 0);
+            }
+    }
+    const float inv = 1.f / l;
+    if (out_h2) {
+        bool bad = false;
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int d = t * 32 + 8 * i + 4 * lh;
+                if (d < D) {
+                    const float4 v = make_float4(oacc[t][4 * i] * inv, oacc[t][4 * i + 1] * inv, oacc[t][4 * i + 2] * inv,
+                                                 oacc[t][4 * i + 3] * inv);
+                    store4_h2(reinterpret_cast<char*>(out), ((size_t)b * N + q) * C * 4, (h * D + d) >> 2, v);
+                    bad = bad || h2_bad(v.x) || h2_bad(v.y) || h2_bad(v.z) || h2_bad(v.w);
+                }
+            }
+        h2_flag(ovf, bad);
+        return;
+    }
+    float* dst = out + ((size_t)b * N + q) * C + h * D;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (d < D) dst[d] = oacc[t][r] * inv;
+        }
+}
+
+template <int D>
+int launch_attn_flash(const float* qkv, float* out, int Bt, int N, int C, int heads, hipStream_t st, int out_h2,
+                      unsigned* ovf) {
+    const float scale = (float)(1.0 / std::sqrt((double)D));
+    hipLaunchKernelGGL((k_attention_flash<D>), dim3(N / 256, heads, Bt), dim3(512), 0, st, qkv, out, N, C, scale,
+                       out_h2, ovf);
+    return check_launch("tcx_attention(flash)");
+}
+
 template <int D>
 int launch_attn_mfma(const float* qkv, float* out, int Bt, int N, int C, int heads, hipStream_t st, int out_h2 = 0,
                      unsigned* ovf = nullptr) {
@@ -289,11 +430,20 @@ using namespace tcx;
 
 extern "C" int tcx_attention(const float* qkv, float* out, int Bt, int N, int C, int heads, void* stream) {
     TCX_REQUIRE(qkv && out && heads > 0 && C % heads == 0, "tcx_attention: bad args");
-    TCX_REQUIRE(N > 0 && N <= 4 * MAXK, "tcx_attention: N must be <= 256 (single-tile kernel)");
+    TCX_REQUIRE(N > 0 && (N <= 4 * MAXK || N % 256 == 0), "tcx_attention: N must be <= 256 or a multiple of 256");
     TCX_REQUIRE(aligned16(qkv) && aligned16(out), "tcx_attention: pointers must be 16-B aligned");
     if (Bt == 0) return TCX_OK;
     const int D = C / heads;
     hipStream_t st = (hipStream_t)stream;
+    if (N > 256) {  // key-tiled flash form
+        switch (D) {
+            case 16: return launch_attn_flash<16>(qkv, out, Bt, N, C, heads, st, 0, nullptr);
+            case 32: return launch_attn_flash<32>(qkv, out, Bt, N, C, heads, st, 0, nullptr);
+            case 48: return launch_attn_flash<48>(qkv, out, Bt, N, C, heads, st, 0, nullptr);
+            case 64: return launch_attn_flash<64>(qkv, out, Bt, N, C, heads, st, 0, nullptr);
+            default: set_error("tcx_attention: head dim %d unsupported for N > 256", D); return TCX_EUNSUP;
+        }
+    }
     if (N % 32 == 0) {  // MFMA path (every U-Net bottleneck: N = (H/4)*(W/4))
         switch (D) {
             case 8: return launch_attn_mfma<8>(qkv, out, Bt, N, C, heads, st);
@@ -319,11 +469,21 @@ extern "C" int tcx_attention(const float* qkv, float* out, int Bt, int N, int C,
 extern "C" int tcx_attention_h2(const float* qkv, void* out, int Bt, int N, int C, int heads, unsigned* ovf,
                                 void* stream) {
     TCX_REQUIRE(qkv && out && heads > 0 && C % heads == 0 && C % 8 == 0, "tcx_attention_h2: bad args");
-    TCX_REQUIRE(N > 0 && N <= 256 && N % 32 == 0, "tcx_attention_h2: needs N %% 32 == 0, N <= 256 (MFMA kernel)");
+    TCX_REQUIRE(N > 0 && ((N <= 256 && N % 32 == 0) || N % 256 == 0),
+                "tcx_attention_h2: needs N %% 32 == 0 and N <= 256, or N %% 256 == 0");
     TCX_REQUIRE(aligned16(qkv) && aligned16(out), "tcx_attention_h2: pointers must be 16-B aligned");
     if (Bt == 0) return TCX_OK;
     float* o = (float*)out;
     hipStream_t st = (hipStream_t)stream;
+    if (N > 256) {
+        switch (C / heads) {
+            case 16: return launch_attn_flash<16>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+            case 32: return launch_attn_flash<32>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+            case 48: return launch_attn_flash<48>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+            case 64: return launch_attn_flash<64>(qkv, o, Bt, N, C, heads, st, 1, ovf);
+            default: set_error("tcx_attention_h2: head dim %d unsupported for N > 256", C / heads); return TCX_EUNSUP;
+        }
+    }
     switch (C / heads) {
         case 8: return launch_attn_mfma<8>(qkv, o, Bt, N, C, heads, st, 1, ovf);
         case 16: return launch_attn_mfma<16>(qkv, o, Bt, N, C, heads, st, 1, ovf);

@@ -617,7 +617,8 @@ int validate(const tcx_unet* net, int B, int H, int W) {
     TCX_REQUIRE(net->base_ch % 4 == 0 && net->base_ch >= 4, "tcx_unet: base_ch must be a multiple of 4");
     TCX_REQUIRE(net->emb_dim <= 256 && net->emb_dim % 2 == 0, "tcx_unet: emb_dim must be even and <= 256");
     TCX_REQUIRE(net->time_ch + net->cond_ch <= 64 && net->y_cont_dim >= 3 && net->y_cont_dim <= 16, "tcx_unet: bad cond dims");
-    TCX_REQUIRE((H / 4) * (W / 4) <= 256, "tcx_unet: bottleneck attention supports N <= 256 tokens");
+    TCX_REQUIRE((H / 4) * (W / 4) <= 256 || ((H / 4) * (W / 4)) % 256 == 0,
+                "tcx_unet: bottleneck attention needs N <= 256 or N %% 256 == 0 tokens");
     TCX_REQUIRE(net->precision == 0 || net->precision == 1, "tcx_unet: precision must be 0 (fp32) or 1 (f16x3)");
     TCX_REQUIRE(net->precision == 0 || (net->base_ch % 32 == 0 && ((H / 4) * (W / 4)) % 32 == 0),
                 "tcx_unet: the f16x3 split path needs base_ch %% 32 == 0 and (H/4)*(W/4) %% 32 == 0");
@@ -638,13 +639,23 @@ int launch_step(const StepArgs& a, hipStream_t st) {
 // (profiles/r01_w_chunk_ab.txt) it LOSES: 59.9 img/s unchunked vs 56.6 / 49.3 / 37.2 at
 // Bc = 64 / 32 / 16 (the smaller conv grids lose more than the memory-bound passes gain), so the
 // default is one pass.  TCX_BATCH_CHUNK=<images> selects chunking (e.g. to bound the workspace).
-int chunk_images(int B) {
+// Independently of that knob, a pass is capped so that its largest activation (2*Bc*H*W*C fp32)
+// stays below 2 GiB: the conv kernels address their operands with 32-bit buffer offsets (the
+// 256x256 configuration at base_ch 96: at most 84 images, i.e. 2*42 with CFG, per pass).
+int max_pass_rows(const tcx_unet* net, int H, int W) {
+    const long long per_row = (long long)H * W * net->base_ch * 4;
+    const long long rows = ((1ll << 31) - 1) / per_row;
+    return (int)std::max(2ll, rows & ~1ll);
+}
+
+int chunk_images(int B, int cap_images) {
     static const int env = [] {
         const char* e = getenv("TCX_BATCH_CHUNK");
         return e ? atoi(e) : -1;
     }();
-    const int c = env < 0 ? 0 : env;
-    return (c <= 0 || c >= B) ? B : c;
+    int c = env < 0 ? 0 : env;
+    c = (c <= 0 || c >= B) ? B : c;
+    return std::max(1, std::min(c, cap_images));
 }
 
 }  // namespace
@@ -655,7 +666,8 @@ using namespace tcx;
 extern "C" size_t tcx_unet_workspace_size(const tcx_unet* net, int Bt, int H, int W) {
     if (!net) return 0;
     // Bt = B or 2B (CFG): size for the largest pass of either reading
-    const int Btc = std::min(Bt, 2 * chunk_images(Bt));
+    const int cap = max_pass_rows(net, H, W);
+    const int Btc = std::min(std::min(Bt, 2 * chunk_images(Bt, cap)), cap);
     return make_plan(net, Btc, H, W, nullptr).bytes + 256;
 }
 
@@ -671,7 +683,7 @@ extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, con
     TCX_REQUIRE((mode != 1 && mode != 3 && mode != 4) || x_inout, "tcx_unet_eval: x_inout needed");
     TCX_REQUIRE(mode != 3 || x2, "tcx_unet_eval: Heun stage 1 needs x2");
     const int cfg = guidance > 0.f ? 1 : 0;
-    const int Bc = chunk_images(B);
+    const int Bc = chunk_images(B, max_pass_rows(net, H, W) / (cfg ? 2 : 1));
     const int Btc = cfg ? 2 * Bc : Bc;
     char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
     const size_t need = make_plan(net, Btc, H, W, nullptr).bytes;
