@@ -152,6 +152,10 @@ int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, cons
 /* tcx_attention (MFMA kernel, N % 32 == 0) with the output written as h2. */
 int tcx_attention_h2(const float* qkv, void* out, int Bt, int N, int C, int heads, unsigned* ovf,
                      void* stream);
+/* The same attention with qkv AND out in h2 storage, both products on f16x3 MFMA
+ * (attention_split.hip): N % 256 == 0, head dim 16, 32, 48 or 64.  Replaces the SDPA of
+ * SelfAttention2d (sde_score_model.py:150-160) in the split-precision evaluator. */
+int tcx_attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream);
 /* Conversions of n elements (n % 8 == 0, channel-fastest tensors with C % 8 == 0). */
 int tcx_f32_to_h2(const float* x, void* y, size_t n, unsigned* ovf, void* stream);
 int tcx_h2_to_f32(const void* x, float* y, size_t n, void* stream);

@@ -207,6 +207,33 @@ def test_attention_h2(Bt, N, C, heads):
     dec_ok(from_h2(o).cpu().numpy(), o32.cpu().numpy())
 
 
+@pytest.mark.parametrize("Bt,N,C,heads,amp", [(2, 256, 192, 4, 1.0), (2, 256, 192, 4, 3.0), (1, 4096, 192, 4, 1.0),
+                                              (2, 512, 64, 4, 2.0), (1, 256, 128, 2, 1.0), (2, 256, 64, 2, 1.0)])
+def test_attention_split_vs_oracle(Bt, N, C, heads, amp):
+    """f16x3 attention (qkv and output h2, attention_split.hip) against the fp64 oracle on the same
+    (h2-representable) inputs, at the fp32 attention's gate and within 2x its error.  amp scales
+    q, k, v (amp 3: peaked softmax rows)."""
+    from test_gpu_ops import close as close_ops
+    qkv32 = dev(rng.standard_normal((Bt, N, 3 * C)) * amp)
+    qh = to_h2(qkv32)
+    qd = from_h2(qh)  # the values the h2 tensor represents
+    o = torch.empty((Bt, N, C), device="cuda")
+    o32 = torch.empty_like(o)
+    chk(L().tcx_attention_split(qh.data_ptr(), o.data_ptr(), Bt, N, C, heads, st()))
+    chk(L().tcx_attention(qd.data_ptr(), o32.data_ptr(), Bt, N, C, heads, st()))
+    torch.cuda.synchronize()
+    x = qd.double().cpu().numpy()
+    d = C // heads
+    sp = lambda a: a.reshape(Bt, N, heads, d).transpose(0, 2, 1, 3)  # noqa: E731
+    ref = nn_np.sdpa(sp(x[:, :, :C]), sp(x[:, :, C:2 * C]), sp(x[:, :, 2 * C:])).transpose(0, 2, 1, 3).reshape(Bt, N, C)
+    got = from_h2(o).double().cpu().numpy()
+    e32 = float(np.abs(o32.double().cpu().numpy() - ref).max())
+    err = close_ops(got, ref)
+    scale = max(1.0, float(np.abs(ref).max()))
+    # + 2^-21 of the scale: the h2 output itself carries 22 significant bits
+    assert err <= 2 * e32 + (2e-7 + 2.0 ** -21) * scale, (err, e32)
+
+
 def test_unet_range_fallback_to_fp32():
     """An activation beyond the f16 range raises the flag and the evaluator recomputes in fp32."""
     import warnings

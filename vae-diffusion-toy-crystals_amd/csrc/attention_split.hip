@@ -1,0 +1,198 @@
+// f16x3 split flash attention for the split-precision U-Net evaluator: the bottleneck
+// self-attention of SelfAttention2d (/root/reference/src/toycrystals/models/sde_score_model.py:
+// 136-167, softmax(q k^T / sqrt(d)) v per (batch, head) over N = H*W tokens) with qkv and the
+// output in h2 storage (h2.hpp), both products on v_mfma_f32_32x32x16_f16: 3 MFMAs per fp32
+// product (hi*lo + lo*hi + hi*hi, f32 accumulation) at 16x the fp32 MFMA rate.
+//
+// Same key-tiled online softmax as k_attention_flash (attention.hip):
+//   S^T = K Q^T : A = K rows (key = lane, the 8 dims of step s on lane half h) read from LDS as
+//                 one hi and one lo b128; B = Q^T fragments held in registers (query on the lane).
+//   P           : the S accumulators (query on the lane, keys (r&3)+8(r>>2)+4h of a 32-key
+//                 subtile) are exponentiated, scaled by 2^10 (so p >= 2^-24 keeps its lo half out
+//                 of the f16 subnormal range) and split; register r = 8s+e of step s is k-slot 8h+e.
+//   O^T = V^T P^T: A = V^T, staged TRANSPOSED in LDS as [d][slot] hi / lo f16 rows with keys
+//                 permuted into the slot order above (slot 16s+8h+e <-> key 16s+8(e>>2)+4h+(e&3)),
+//                 so a lane's 8 k-slots are one b128 read.  D = 48 pads O^T to 64 rows (zero V).
+// Per 128-key tile: K rows copied (h2 as is), V transposed with b32 writes (two keys per dword).
+// The output is a convex combination of V rows, so |O| <= max|V| < 65504: no range flag.
+#include "common.hpp"
+#include "h2.hpp"
+
+namespace tcx {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int D>
+__global__ __launch_bounds__(512) void k_attention_split(const char* __restrict__ qkv, char* __restrict__ out, int N,
+                                                         int C, float scale) {
+    static_assert(D % 16 == 0 && D <= 64, "split attention: head dim multiple of 16, <= 64");
+    constexpr int KT = 128;            // keys per staged tile
+    constexpr int NST = KT / 32;       // 32-key subtiles
+    constexpr int DS = D / 16;         // 16-deep steps of Q.K
+    constexpr int DT = (D + 31) / 32;  // 32-row tiles of O^T
+    constexpr int DP = DT * 32;
+    constexpr int KSB = D * 4 + 16;    // bytes per staged key row (h2) + 16 B pad
+    constexpr int VSW = KT / 2 + 4;    // dwords per V^T row (two f16 slots each) + 16 B pad
+    constexpr float PSC = 1024.f;
+    __shared__ __attribute__((aligned(16))) char Ks[KT * KSB];
+    __shared__ __attribute__((aligned(16))) unsigned Vh[DP * VSW];
+    __shared__ __attribute__((aligned(16))) unsigned Vl[DP * VSW];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int tid = threadIdx.x;
+    const size_t rs = 12 * (size_t)C;  // bytes per token row of qkv (3C channels, 4 B each)
+    const char* base = qkv + (size_t)b * N * rs;
+    const int lane = tid & 63, w = tid >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    const int q = blockIdx.x * 256 + w * 32 + li;
+    h8 qh[DS], ql[DS];
+    {
+        const char* qr = base + (size_t)q * rs + (size_t)h * D * 4;
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+            qh[s] = *reinterpret_cast<const h8*>(qr + (2 * s + lh) * 32);
+            ql[s] = *reinterpret_cast<const h8*>(qr + (2 * s + lh) * 32 + 16);
+        }
+    }
+    if (DP > D) {
+        for (int i = tid; i < (DP - D) * VSW; i += 512) {
+            Vh[D * VSW + i] = 0u;
+            Vl[D * VSW + i] = 0u;
+        }
+    }
+    f32x16 oacc[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) oacc[t] = (f32x16){};
+    float m = -INFINITY, l = 0.f;
+    constexpr int KP = D / 4;  // 16-B pieces per K row
+    constexpr int G = D / 8;   // 8-dim groups per V row
+    for (int k0 = 0; k0 < N; k0 += KT) {
+        __syncthreads();  // previous tile fully consumed
+        for (int i = tid; i < KT * KP; i += 512) {
+            const int j = i / KP, pc = i - (i / KP) * KP;
+            *reinterpret_cast<float4*>(Ks + j * KSB + pc * 16) =
+                *reinterpret_cast<const float4*>(base + (size_t)(k0 + j) * rs + (size_t)(C + h * D) * 4 + pc * 16);
+        }
+        for (int i = tid; i < (KT / 2) * G; i += 512) {
+            const int g = i / (KT / 2), jp = i - g * (KT / 2);  // key pair (2 jp, 2 jp + 1), dim group g
+            const int j = 2 * jp;
+            const char* src = base + (size_t)(k0 + j) * rs + (size_t)(2 * C + h * D) * 4 + g * 32;
+            const uint4 h0 = *reinterpret_cast<const uint4*>(src), l0 = *reinterpret_cast<const uint4*>(src + 16);
+            const uint4 h1 = *reinterpret_cast<const uint4*>(src + rs);
+            const uint4 l1 = *reinterpret_cast<const uint4*>(src + rs + 16);
+            // slot of key j within its subtile: kk = 16s + 8(e>>2) + 4h + (e&3) -> 16s + 8h + e
+            const int kk = j & 31, rem = kk & 15;
+            const int slot = (j & ~31) + (kk & 16) + 8 * ((rem >> 2) & 1) + ((rem & 3) | ((rem >> 3) << 2));
+            const int col = slot >> 1;  // j even -> slot even; key j + 1 takes slot + 1
+            const unsigned hw0[4] = {h0.x, h0.y, h0.z, h0.w}, hw1[4] = {h1.x, h1.y, h1.z, h1.w};
+            const unsigned lw0[4] = {l0.x, l0.y, l0.z, l0.w}, lw1[4] = {l1.x, l1.y, l1.z, l1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int sh = 16 * (e & 1);
+                const unsigned a = (hw0[e >> 1] >> sh) & 0xffffu, c = (hw1[e >> 1] >> sh) & 0xffffu;
+                const unsigned al = (lw0[e >> 1] >> sh) & 0xffffu, cl = (lw1[e >> 1] >> sh) & 0xffffu;
+                Vh[(g * 8 + e) * VSW + col] = a | (c << 16);
+                Vl[(g * 8 + e) * VSW + col] = al | (cl << 16);
+            }
+        }
+        __syncthreads();
+        f32x16 sacc[NST];
+#pragma unroll
+        for (int n = 0; n < NST; ++n) {
+            sacc[n] = (f32x16){};
+            const char* kr = Ks + (n * 32 + li) * KSB;
+#pragma unroll
+            for (int s = 0; s < DS; ++s) {
+                const h8 kh = *reinterpret_cast<const h8*>(kr + (2 * s + lh) * 32);
+                const h8 kl = *reinterpret_cast<const h8*>(kr + (2 * s + lh) * 32 + 16);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[s], sacc[n], 0, 0, 0);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[s], sacc[n], 0, 0, 0);
+                sacc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[s], sacc[n], 0, 0, 0);
+            }
+        }
+        float mt = -INFINITY;
+#pragma unroll
+        for (int n = 0; n < NST; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sacc[n][r]);
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float mn = fmaxf(m, mt);
+        const float alpha = expf((m - mn) * scale);  // 0 on the first tile (m = -inf)
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[t][r] *= alpha;
+        float lt = 0.f;
+#pragma unroll
+        for (int n = 0; n < NST; ++n) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                h8 ph, pl;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float pv = expf((sacc[n][8 * s + e] - mn) * scale);
+                    lt += pv;
+                    const float v = pv * PSC;
+                    const _Float16 hh = (_Float16)v;
+                    ph[e] = hh;
+                    pl[e] = (_Float16)(v - (float)hh);
+                }
+                const int c0 = (n * 32 + 16 * s + 8 * lh) >> 1;
+#pragma unroll
+                for (int t = 0; t < DT; ++t) {
+                    const h8 vh = *reinterpret_cast<const h8*>(&Vh[(t * 32 + li) * VSW + c0]);
+                    const h8 vl = *reinterpret_cast<const h8*>(&Vl[(t * 32 + li) * VSW + c0]);
+                    oacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, oacc[t], 0, 0, 0);
+                    oacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, oacc[t], 0, 0, 0);
+                    oacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, oacc[t], 0, 0, 0);
+                }
+            }
+        }
+        lt += __shfl_xor(lt, 32);
+        l += lt;
+    }
+    const float inv = 1.f / (l * PSC);
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int d = t * 32 + 8 * i + 4 * lh;
+            if (d < D) {
+                const float4 v = make_float4(oacc[t][4 * i] * inv, oacc[t][4 * i + 1] * inv, oacc[t][4 * i + 2] * inv,
+                                             oacc[t][4 * i + 3] * inv);
+                store4_h2(out, ((size_t)b * N + q) * C * 4, (h * D + d) >> 2, v);
+            }
+        }
+}
+
+template <int D>
+int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
+    const float scale = (float)(1.0 / std::sqrt((double)D));
+    hipLaunchKernelGGL((k_attention_split<D>), dim3(N / 256, heads, Bt), dim3(512), 0, st, (const char*)qkv,
+                       (char*)out, N, C, scale);
+    return check_launch("tcx_attention_split");
+}
+
+}  // namespace
+}  // namespace tcx
+
+using namespace tcx;
+
+extern "C" int tcx_attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream) {
+    TCX_REQUIRE(qkv && out && heads > 0 && C % heads == 0, "tcx_attention_split: bad args");
+    TCX_REQUIRE(N > 0 && N % 256 == 0, "tcx_attention_split: needs N %% 256 == 0");
+    TCX_REQUIRE(aligned16(qkv) && aligned16(out), "tcx_attention_split: pointers must be 16-B aligned");
+    if (Bt == 0) return TCX_OK;
+    hipStream_t st = (hipStream_t)stream;
+    switch (C / heads) {
+        case 16: return launch_split<16>(qkv, out, Bt, N, C, heads, st);
+        case 32: return launch_split<32>(qkv, out, Bt, N, C, heads, st);
+        case 48: return launch_split<48>(qkv, out, Bt, N, C, heads, st);
+        case 64: return launch_split<64>(qkv, out, Bt, N, C, heads, st);
+        default:
+            set_error("tcx_attention_split: head dim %d unsupported (16, 32, 48, 64)", C / heads);
+            return TCX_EUNSUP;
+    }
+}

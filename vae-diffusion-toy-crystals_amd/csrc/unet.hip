@@ -447,6 +447,15 @@ int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2
     return TCX_OK;
 }
 
+// TCX_ATTN_SPLIT=0 keeps the split evaluator's attention on fp32 MFMA (A/B measurements)
+bool attn_split_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("TCX_ATTN_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 int groups_of(int ch) {
     for (int g : {8, 4, 2})
         if (ch % g == 0) return g;
@@ -565,9 +574,15 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         else TCX_TRY(tcx_gn_apply_tab(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, st));
         const tcx_conv& q = net->qkv;
         int dummy = 0;
+        // split path with N % 256 == 0 and a supported head dim: the qkv conv writes h2 and the
+        // attention runs on f16x3 MFMA (attention_split.hip); else fp32 qkv + fp32-MFMA attention
+        const int D = C2 / net->heads;
+        const bool split_attn = h2.on && attn_split_enabled() && P.P2 % 256 == 0 && C2 % net->heads == 0 &&
+                                (D == 16 || D == 32 || D == 48 || D == 64);
         TCX_TRY(conv_gn(q, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 0, nullptr, nullptr, P.qkv, nullptr, &dummy, st,
-                        nullptr, nullptr, nullptr, nullptr, h2));
-        if (h2.on) TCX_TRY(tcx_attention_h2(P.qkv, P.b16, Bt, P.P2, C2, net->heads, h2.ovf, st));
+                        nullptr, nullptr, nullptr, nullptr, h2, split_attn ? 1 : 0));
+        if (split_attn) TCX_TRY(tcx_attention_split(P.qkv, P.b16, Bt, P.P2, C2, net->heads, st));
+        else if (h2.on) TCX_TRY(tcx_attention_h2(P.qkv, P.b16, Bt, P.P2, C2, net->heads, h2.ovf, st));
         else TCX_TRY(tcx_attention(P.qkv, P.b16, Bt, P.P2, C2, net->heads, st));
         const tcx_conv& pr = net->proj;
         TCX_TRY(conv_gn(pr, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 0, nullptr, P.a16, P.a16, nullptr, &dummy, st,

@@ -80,6 +80,7 @@ _SIGS = {
     "tcx_gn_apply_tab_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp, c_fp]),
     "tcx_upsample2x_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
     "tcx_attention_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),
+    "tcx_attention_split": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_f32_to_h2": (c_int, [c_fp, c_fp, c_size, c_fp, c_fp]),
     "tcx_h2_to_f32": (c_int, [c_fp, c_fp, c_size, c_fp]),
     "tcx_unet_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int]),
