@@ -158,56 +158,78 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const double* __restrict__ 
     }
 }
 
+constexpr int UPK = 4;  // output quads per thread of the upsample (4 x 4 float4 loads in flight)
 template <bool OUTH2>
 __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ x, float* __restrict__ y, int Bt, int H,
                                                     int W, int C, const float* __restrict__ tsc,
                                                     const float* __restrict__ tsh, unsigned* ovf) {
+    // one output row (b, oy) per blockIdx.x, a chunk of UPK * 256 of its 2W * C/4 channel quads
+    // per blockIdx.y.  The row's two source rows and weights are block-uniform (32-bit index
+    // math only: the former flat 64-bit div/mod per element was the cost); the 4 x UPK source
+    // loads of a thread are issued before any is used.
     bool bad = false;
     const int C4 = C / 4;
-    const size_t n = (size_t)Bt * 4 * H * W * C4;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const int c4 = (int)(i % C4);
-        size_t r = i / C4;
-        const int ox = (int)(r % (2 * W));
-        r /= (2 * W);
-        const int oy = (int)(r % (2 * H));
-        const int b = (int)(r / (2 * H));
-        float sy = 0.5f * ((float)oy + 0.5f) - 0.5f;
-        sy = sy < 0.f ? 0.f : sy;
-        float sx = 0.5f * ((float)ox + 0.5f) - 0.5f;
-        sx = sx < 0.f ? 0.f : sx;
-        const int y0 = (int)sy, x0 = (int)sx;
-        const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
-        const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
-        const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
-        const float* src = x + (size_t)b * H * W * C + c4 * 4;
-        float4 a = *reinterpret_cast<const float4*>(src + (size_t)(y0 * W + x0) * C);
-        float4 bq = *reinterpret_cast<const float4*>(src + (size_t)(y0 * W + x1) * C);
-        float4 c = *reinterpret_cast<const float4*>(src + (size_t)(y1 * W + x0) * C);
-        float4 d = *reinterpret_cast<const float4*>(src + (size_t)(y1 * W + x1) * C);
-        if (tsc) {  // fused GN+SiLU of the source (up2's last GroupNorm before us1)
-            const float4 s4 = *reinterpret_cast<const float4*>(tsc + (size_t)b * C + c4 * 4);
-            const float4 h4 = *reinterpret_cast<const float4*>(tsh + (size_t)b * C + c4 * 4);
-            auto tr = [&](float4& v) {
-                v.x = silu_f(fmaf(v.x, s4.x, h4.x)); v.y = silu_f(fmaf(v.y, s4.y, h4.y));
-                v.z = silu_f(fmaf(v.z, s4.z, h4.z)); v.w = silu_f(fmaf(v.w, s4.w, h4.w));
-            };
-            tr(a); tr(bq); tr(c); tr(d);
+    const int oy = blockIdx.x % (2 * H), b = blockIdx.x / (2 * H);
+    float sy = 0.5f * ((float)oy + 0.5f) - 0.5f;
+    sy = sy < 0.f ? 0.f : sy;
+    const int y0 = (int)sy;
+    const int y1 = y0 + (y0 < H - 1 ? 1 : 0);
+    const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
+    const float* r0 = x + ((size_t)b * H + y0) * W * C;
+    const float* r1 = x + ((size_t)b * H + y1) * W * C;
+    const int nq = 2 * W * C4;
+    const size_t orow = ((size_t)b * 2 * H + oy) * 2 * W * C4;  // first quad of the output row
+    const int i0 = blockIdx.y * (UPK * 256) + threadIdx.x;
+    float4 a[UPK], bq[UPK], c[UPK], d[UPK];
+#pragma unroll
+    for (int k = 0; k < UPK; ++k) {
+        const int i = i0 + 256 * k;
+        if (i < nq) {
+            const int ox = i / C4, c4 = i - (i / C4) * C4;
+            float sx = 0.5f * ((float)ox + 0.5f) - 0.5f;
+            sx = sx < 0.f ? 0.f : sx;
+            const int x0 = (int)sx, x1 = x0 + (x0 < W - 1 ? 1 : 0);
+            a[k] = *reinterpret_cast<const float4*>(r0 + x0 * C + c4 * 4);
+            bq[k] = *reinterpret_cast<const float4*>(r0 + x1 * C + c4 * 4);
+            c[k] = *reinterpret_cast<const float4*>(r1 + x0 * C + c4 * 4);
+            d[k] = *reinterpret_cast<const float4*>(r1 + x1 * C + c4 * 4);
         }
-        // explicit fmaf: the same rounding in every instantiation (fp32 and h2 outputs)
-        auto bl = [&](float va, float vb, float vc, float vd) {
-            return fmaf(ly1, fmaf(lx1, vd, lx0 * vc), ly0 * fmaf(lx1, vb, lx0 * va));
-        };
-        float4 o;
-        o.x = bl(a.x, bq.x, c.x, d.x);
-        o.y = bl(a.y, bq.y, c.y, d.y);
-        o.z = bl(a.z, bq.z, c.z, d.z);
-        o.w = bl(a.w, bq.w, c.w, d.w);
-        if constexpr (OUTH2) {
-            store4_h2(reinterpret_cast<char*>(y), (i / C4) * (size_t)C * 4, c4, o);
-            bad = bad || h2_bad(o.x) || h2_bad(o.y) || h2_bad(o.z) || h2_bad(o.w);
-        } else {
-            *reinterpret_cast<float4*>(y + i * 4) = o;
+    }
+#pragma unroll
+    for (int k = 0; k < UPK; ++k) {
+        const int i = i0 + 256 * k;
+        if (i < nq) {
+            const int ox = i / C4, c4 = i - (i / C4) * C4;
+            float sx = 0.5f * ((float)ox + 0.5f) - 0.5f;
+            sx = sx < 0.f ? 0.f : sx;
+            const int x0 = (int)sx;
+            const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
+            if (tsc) {  // fused GN+SiLU of the source
+                const float4 s4 = *reinterpret_cast<const float4*>(tsc + (size_t)b * C + c4 * 4);
+                const float4 h4 = *reinterpret_cast<const float4*>(tsh + (size_t)b * C + c4 * 4);
+                auto tr = [&](float4& v) {
+                    v.x = silu_f(fmaf(v.x, s4.x, h4.x)); v.y = silu_f(fmaf(v.y, s4.y, h4.y));
+                    v.z = silu_f(fmaf(v.z, s4.z, h4.z)); v.w = silu_f(fmaf(v.w, s4.w, h4.w));
+                };
+                tr(a[k]); tr(bq[k]); tr(c[k]); tr(d[k]);
+            }
+            // explicit fmaf: the same rounding in every instantiation (fp32 and h2 outputs)
+            auto bl = [&](float va, float vb, float vc, float vd) {
+                return fmaf(ly1, fmaf(lx1, vd, lx0 * vc), ly0 * fmaf(lx1, vb, lx0 * va));
+            };
+            float4 o;
+            o.x = bl(a[k].x, bq[k].x, c[k].x, d[k].x);
+            o.y = bl(a[k].y, bq[k].y, c[k].y, d[k].y);
+            o.z = bl(a[k].z, bq[k].z, c[k].z, d[k].z);
+            o.w = bl(a[k].w, bq[k].w, c[k].w, d[k].w);
+            const size_t q = orow + i;
+            if constexpr (OUTH2) {
+                const size_t pix = ((size_t)b * 2 * H + oy) * 2 * W + ox;
+                store4_h2(reinterpret_cast<char*>(y), pix * C * 4, c4, o);
+                bad = bad || h2_bad(o.x) || h2_bad(o.y) || h2_bad(o.z) || h2_bad(o.w);
+            } else {
+                *reinterpret_cast<float4*>(y + q * 4) = o;
+            }
         }
     }
     h2_flag(ovf, bad);
@@ -270,7 +292,42 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
     const int C8 = C / 8;
     const int n8 = (p1 - p0) * C8;
     bool bad = false;
-    for (int i = threadIdx.x; i < n8; i += 256) {
+    // In place (x == y): the compiler must assume each store may alias the next loads, so the
+    // loads of GU groups are issued explicitly before any of their stores (each thread's groups
+    // are distinct elements) — one group in flight per thread measured 4.85 TB/s.
+    constexpr int GU = 4;
+    int i = threadIdx.x;
+    for (; i + (GU - 1) * 256 < n8; i += GU * 256) {
+        float4 u0[GU], u1[GU];
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+            const float* src = x + base + (size_t)(i + 256 * k) * 8;
+            u0[k] = *reinterpret_cast<const float4*>(src);
+            u1[k] = *reinterpret_cast<const float4*>(src + 4);
+        }
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+            const int c0 = ((i + 256 * k) % C8) * 8;
+            float4 v0 = u0[k], v1 = u1[k];
+            v0.x = fmaf(v0.x, sc[c0], sh[c0]); v0.y = fmaf(v0.y, sc[c0 + 1], sh[c0 + 1]);
+            v0.z = fmaf(v0.z, sc[c0 + 2], sh[c0 + 2]); v0.w = fmaf(v0.w, sc[c0 + 3], sh[c0 + 3]);
+            v1.x = fmaf(v1.x, sc[c0 + 4], sh[c0 + 4]); v1.y = fmaf(v1.y, sc[c0 + 5], sh[c0 + 5]);
+            v1.z = fmaf(v1.z, sc[c0 + 6], sh[c0 + 6]); v1.w = fmaf(v1.w, sc[c0 + 7], sh[c0 + 7]);
+            if (silu) {
+                v0.x = silu_f(v0.x); v0.y = silu_f(v0.y); v0.z = silu_f(v0.z); v0.w = silu_f(v0.w);
+                v1.x = silu_f(v1.x); v1.y = silu_f(v1.y); v1.z = silu_f(v1.z); v1.w = silu_f(v1.w);
+            }
+            uint2 h0, l0, h1, l1;
+            split4(v0, h0, l0);
+            split4(v1, h1, l1);
+            char* g = y + (base + (size_t)(i + 256 * k) * 8) * 4;
+            *reinterpret_cast<uint4*>(g) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+            *reinterpret_cast<uint4*>(g + 16) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+            bad = bad || h2_bad(v0.x) || h2_bad(v0.y) || h2_bad(v0.z) || h2_bad(v0.w) || h2_bad(v1.x) ||
+                  h2_bad(v1.y) || h2_bad(v1.z) || h2_bad(v1.w);
+        }
+    }
+    for (; i < n8; i += 256) {
         const int c0 = (i % C8) * 8;
         const float* src = x + base + (size_t)i * 8;
         float4 v0 = *reinterpret_cast<const float4*>(src);
@@ -366,11 +423,10 @@ extern "C" int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, in
                               const float* shift, void* stream) {
     TCX_REQUIRE(x && y && C % 4 == 0 && aligned16(x) && aligned16(y), "tcx_upsample2x: bad args");
     TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x: scale/shift pair");
-    const size_t n = (size_t)Bt * 4 * H * W * (C / 4);
-    if (n == 0) return TCX_OK;
-    const int blocks = (int)std::min<size_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_upsample2x<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, y, Bt, H, W, C, scale,
-                       shift, nullptr);
+    if ((size_t)Bt * H * W * C == 0) return TCX_OK;
+    const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 4), UPK * 256));
+    hipLaunchKernelGGL(k_upsample2x<false>, grid, dim3(256), 0, (hipStream_t)stream, x, y, Bt, H, W, C, scale, shift,
+                       nullptr);
     return check_launch("tcx_upsample2x");
 }
 
@@ -378,11 +434,10 @@ extern "C" int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, 
                                  const float* shift, unsigned* ovf, void* stream) {
     TCX_REQUIRE(x && y && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_upsample2x_h2: bad args");
     TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x_h2: scale/shift pair");
-    const size_t n = (size_t)Bt * 4 * H * W * (C / 4);
-    if (n == 0) return TCX_OK;
-    const int blocks = (int)std::min<size_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_upsample2x<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (float*)y, Bt, H, W, C,
-                       scale, shift, ovf);
+    if ((size_t)Bt * H * W * C == 0) return TCX_OK;
+    const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 4), UPK * 256));
+    hipLaunchKernelGGL(k_upsample2x<true>, grid, dim3(256), 0, (hipStream_t)stream, x, (float*)y, Bt, H, W, C, scale,
+                       shift, ovf);
     return check_launch("tcx_upsample2x_h2");
 }
 

@@ -28,11 +28,37 @@ struct CondArgs {
     int E, n_types, ycd, time_ch, cond_ch, C0;
 };
 
-// One block per (CFG-doubled) batch row.
-__global__ __launch_bounds__(256) void k_cond(CondArgs a, const float* __restrict__ t, int t_per_sample,
-                                              const int64_t* __restrict__ y_cat, const float* __restrict__ y_cont,
-                                              int B, int cfg, float* __restrict__ bias_b) {
-    __shared__ float te[256], h1[256], te2[256], yv[16], g1[256], u[512], ce[256], maps[64];
+// One block of CT threads per (CFG-doubled) batch row.  Every linear layer is a split-K matvec
+// (kgroups of threads each reduce K/kgroups products, then one fixed-order fold over the groups):
+// the serial dependency per layer is ~K/8 loads instead of K (one thread per output), which made
+// this latency-bound kernel ~58 us per evaluation.
+constexpr int CT = 1024;
+
+// out[n] = act(bias[n] + sum_k wt[k*N + n] * in[k]) for n < N (wt: [K][N]); all CT threads call it.
+__device__ void cond_mv(const float* __restrict__ wt, const float* __restrict__ bias, const float* in, int K, int N,
+                        float* out, float* red, bool silu) {
+    const int j = threadIdx.x;
+    const int G = max(1, min(CT / N, 16));
+    const int n = j % N, g = j / N;
+    if (g < G) {
+        float s = 0.f;
+        for (int k = g; k < K; k += G) s = fmaf(wt[k * N + n], in[k], s);
+        red[g * N + n] = s;
+    }
+    __syncthreads();
+    if (j < N) {
+        float s = bias[n];
+        for (int gg = 0; gg < G; ++gg) s += red[gg * N + n];
+        out[n] = silu ? silu_f(s) : s;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(CT) void k_cond(CondArgs a, const float* __restrict__ t, int t_per_sample,
+                                             const int64_t* __restrict__ y_cat, const float* __restrict__ y_cont,
+                                             int B, int cfg, float* __restrict__ bias_b) {
+    __shared__ float te[256], h1[256], te2[256], yv[16], g1[256], c2[256], u[512], ce[256], maps[64];
+    __shared__ float red[16 * 256];
     const int bb = blockIdx.x;
     const int bs = bb % B;
     const bool null_c = cfg && bb < B;  // first half of a CFG batch = unconditional
@@ -57,46 +83,22 @@ __global__ __launch_bounds__(256) void k_cond(CondArgs a, const float* __restric
         yv[j] = v;
     }
     __syncthreads();
+    cond_mv(a.time_w1t, a.time_b1, te, E, E, h1, red, true);
+    cond_mv(a.cmlp_w1t, a.cmlp_b1, yv, a.ycd, E, g1, red, true);
+    cond_mv(a.time_w2t, a.time_b2, h1, E, E, te2, red, false);
+    cond_mv(a.cmlp_w2t, a.cmlp_b2, g1, E, E, c2, red, false);
     if (j < E) {
-        float s = a.time_b1[j];
-        for (int k = 0; k < E; ++k) s = fmaf(a.time_w1t[k * E + j], te[k], s);
-        h1[j] = silu_f(s);
-        float g = a.cmlp_b1[j];
-        for (int k = 0; k < a.ycd; ++k) g = fmaf(a.cmlp_w1t[k * E + j], yv[k], g);
-        g1[j] = silu_f(g);
-    }
-    __syncthreads();
-    if (j < E) {
-        float s = a.time_b2[j];
-        for (int k = 0; k < E; ++k) s = fmaf(a.time_w2t[k * E + j], h1[k], s);
-        te2[j] = s;
-        float c = a.cmlp_b2[j];
-        for (int k = 0; k < E; ++k) c = fmaf(a.cmlp_w2t[k * E + j], g1[k], c);
         long long yc = null_c ? a.n_types : y_cat[bs];
         yc = yc < 0 ? 0 : (yc > a.n_types ? a.n_types : yc);
         u[j] = silu_f(a.cat_emb[(size_t)yc * E + j]);
-        u[E + j] = silu_f(c);
+        u[E + j] = silu_f(c2[j]);
     }
     __syncthreads();
-    if (j < E) {
-        float s = a.cout_b[j];
-        for (int k = 0; k < 2 * E; ++k) s = fmaf(a.cout_wt[k * E + j], u[k], s);
-        ce[j] = s;
-    }
-    __syncthreads();
+    cond_mv(a.cout_wt, a.cout_b, u, 2 * E, E, ce, red, false);
     const int nm = a.time_ch + a.cond_ch;
-    if (j < a.time_ch) {
-        float s = a.ttm_b[j];
-        for (int k = 0; k < E; ++k) s = fmaf(a.ttm_wt[k * a.time_ch + j], te2[k], s);
-        maps[j] = s;
-    } else if (j < nm) {
-        const int c = j - a.time_ch;
-        float s = a.tcm_b[c];
-        for (int k = 0; k < E; ++k) s = fmaf(a.tcm_wt[k * a.cond_ch + c], ce[k], s);
-        maps[j] = s;
-    }
-    __syncthreads();
-    for (int co = j; co < a.C0; co += blockDim.x) {
+    cond_mv(a.ttm_wt, a.ttm_b, te2, E, a.time_ch, maps, red, false);
+    cond_mv(a.tcm_wt, a.tcm_b, ce, E, a.cond_ch, maps + a.time_ch, red, false);
+    for (int co = j; co < a.C0; co += CT) {
         float s = a.conv_b[co];
         for (int c = 0; c < nm; ++c) s = fmaf(maps[c], a.map_wsum[co * nm + c], s);
         bias_b[(size_t)bb * a.C0 + co] = s;
@@ -204,6 +206,23 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int H
     const int b = blockIdx.y;
     const int p0 = blockIdx.x * HEAD_PX;
     const int tid = threadIdx.x;
+    const int C4 = C / 4;
+    const int npx = min(HEAD_PX, HW - p0);
+    const float* src = h + ((size_t)b * HW + p0) * C;
+    // the tile's loads are all issued before anything waits on them (HK float4 per thread in
+    // flight: the block's whole 64 x C tile for C <= 128); a load-transform-store loop keeps one
+    // load per thread in flight and ran at 2.8 TB/s
+    constexpr int HK = 8;
+    const int nq = npx * C4;
+    const bool hoist = nq <= HK * 256;
+    float4 v[HK];
+    if (hoist) {
+#pragma unroll
+        for (int k = 0; k < HK; ++k) {
+            const int i = tid + 256 * k;
+            if (i < nq) v[k] = *reinterpret_cast<const float4*>(src + (size_t)i * 4);
+        }
+    }
     for (int i = tid; i < 9 * C; i += 256) {
         const int c = i / 9, k = i - (i / 9) * 9;  // w_out is [C][9]; stored tap-major
         w[k * C + c] = w_out[i];
@@ -213,17 +232,22 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int H
         sh[c] = tsh[(size_t)b * C + c];
     }
     __syncthreads();
-    const int C4 = C / 4;
-    const int npx = min(HEAD_PX, HW - p0);
-    const float* src = h + ((size_t)b * HW + p0) * C;
-    for (int i = tid; i < npx * C4; i += 256) {
+    auto put = [&](int i, float4 u) {
         const int px = i / C4, c = (i - (i / C4) * C4) * 4;
-        float4 v = *reinterpret_cast<const float4*>(src + (size_t)i * 4);
-        v.x = silu_f(fmaf(v.x, sc[c], sh[c]));
-        v.y = silu_f(fmaf(v.y, sc[c + 1], sh[c + 1]));
-        v.z = silu_f(fmaf(v.z, sc[c + 2], sh[c + 2]));
-        v.w = silu_f(fmaf(v.w, sc[c + 3], sh[c + 3]));
-        *reinterpret_cast<float4*>(&tile[px * LD + c]) = v;
+        u.x = silu_f(fmaf(u.x, sc[c], sh[c]));
+        u.y = silu_f(fmaf(u.y, sc[c + 1], sh[c + 1]));
+        u.z = silu_f(fmaf(u.z, sc[c + 2], sh[c + 2]));
+        u.w = silu_f(fmaf(u.w, sc[c + 3], sh[c + 3]));
+        *reinterpret_cast<float4*>(&tile[px * LD + c]) = u;
+    };
+    if (hoist) {
+#pragma unroll
+        for (int k = 0; k < HK; ++k) {
+            const int i = tid + 256 * k;
+            if (i < nq) put(i, v[k]);
+        }
+    } else {
+        for (int i = tid; i < nq; i += 256) put(i, *reinterpret_cast<const float4*>(src + (size_t)i * 4));
     }
     __syncthreads();
     const int px = tid & (HEAD_PX - 1);
@@ -486,7 +510,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         a.map_wsum = net->map_wsum; a.conv_b = net->down1_0.b;
         a.E = net->emb_dim; a.n_types = net->n_types; a.ycd = net->y_cont_dim;
         a.time_ch = net->time_ch; a.cond_ch = net->cond_ch; a.C0 = C;
-        hipLaunchKernelGGL(k_cond, dim3(Bt), dim3(256), 0, st, a, t, t_per_sample, y_cat, y_cont, B, cfg, P.bias0);
+        hipLaunchKernelGGL(k_cond, dim3(Bt), dim3(CT), 0, st, a, t, t_per_sample, y_cat, y_cont, B, cfg, P.bias0);
         TCX_TRY(check_launch("k_cond"));
     }
     int ns = 1;
