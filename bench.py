@@ -94,6 +94,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--lanes-alt", type=int, default=3,
+                    help="after the timed region, time --steps more passes with this many concurrent sampling "
+                         "lanes (tcx_set_sample_lanes; 0/1 = skip) and report them under 'lanes_alt'")
     ap.add_argument("--precision", choices=["f16x3", "fp32"], default="f16x3",
                     help="conv arithmetic: f16x3 split MFMA (fp32-grade, default) or fp32 MFMA")
     args = ap.parse_args()
@@ -192,6 +195,30 @@ def main() -> int:
                      "launches": n.value,
                      "conv_share_of_step": round(ms.value / 1e3 / elapsed, 4)},
     }
+    if args.lanes_alt > 1:
+        # Concurrent lanes: the batch split into per-stream sampling chains (bit-identical images)
+        # so one lane's HBM-bound passes overlap another's MFMA-bound convs.  Reported beside, not
+        # as, `value`: with kernels of several streams co-running, per-launch event durations no
+        # longer measure a kernel alone, so the roofline above comes from the one-stream region.
+        prev = L.tcx_set_sample_lanes(args.lanes_alt)
+        run(-100)
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            out = run(100 + i)
+        torch.cuda.synchronize(device)
+        el2 = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+            t = torch.tensor([el2], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+        L.tcx_set_sample_lanes(prev)
+        result["lanes_alt"] = {"lanes": args.lanes_alt, "value": round(images / el2, 4), "unit": "images/s",
+                               "ms_per_step": round(el2 / args.steps * 1e3, 3), "steps": args.steps,
+                               "speedup_vs_value": round(elapsed / el2, 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model.state_dict(), args.cpu_batch, args.cpu_steps, args.cfg, args.t_end)
     if rank == 0:

@@ -202,6 +202,12 @@ typedef struct tcx_unet {
 
 size_t tcx_unet_workspace_size(const tcx_unet* net, int Bt, int H, int W);
 
+/* Concurrent sampling lanes of tcx_sde_sample: the batch is split into `lanes` (1-4) groups of
+ * images advanced step by step on their own HIP streams (joined to the caller's stream at the
+ * end); results are identical to one lane.  0 restores the TCX_LANES environment default (1).
+ * Returns the previous setting.  Workspace queries made after the call size for the lanes. */
+int tcx_set_sample_lanes(int lanes);
+
 /* Per-step scalar table used by the fused step kernels: row i = {t_i, t_{i+1}, dt, beta(t_i),
  * sigma(t_i), sqrt(beta), sqrt|dt|, alpha(t_i)}, computed on the host with the reference's
  * fp32 formulas (sde_score_model.py:273-298,540-550). */

@@ -697,23 +697,82 @@ int chunk_images(int B, int cap_images) {
     return std::max(1, std::min(c, cap_images));
 }
 
-}  // namespace
-}  // namespace tcx
+// Concurrent sampling lanes (TCX_LANES = L > 1, default 1): the batch is split into L contiguous
+// groups of images, each an independent sampling chain (GroupNorm is per image, CFG pairs stay
+// together) advanced step by step on its own HIP stream, so the HBM-bound passes of one lane
+// (GroupNorm apply, upsample, head) can run beside the MFMA-bound convs of another.  The noise
+// counters use absolute element offsets: the result is identical to one lane.
+int g_lanes = 0;  // set by tcx_set_sample_lanes; 0: TCX_LANES from the environment
+int lanes_setting() {
+    static const int env = [] {
+        const char* e = getenv("TCX_LANES");
+        return e ? atoi(e) : 1;
+    }();
+    const int v = g_lanes > 0 ? g_lanes : env;
+    return v < 1 ? 1 : (v > 4 ? 4 : v);
+}
 
-using namespace tcx;
+struct LaneSync {
+    hipStream_t s[4];
+    hipEvent_t ev[5];
+    bool ok = false;
+};
 
-extern "C" size_t tcx_unet_workspace_size(const tcx_unet* net, int Bt, int H, int W) {
-    if (!net) return 0;
+LaneSync* lane_sync() {
+    static LaneSync ls;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        bool ok = true;
+        for (int i = 0; i < 4; ++i) ok = ok && hipStreamCreateWithFlags(&ls.s[i], hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; i < 5; ++i) ok = ok && hipEventCreateWithFlags(&ls.ev[i], hipEventDisableTiming) == hipSuccess;
+        ls.ok = ok;
+    }
+    return ls.ok ? &ls : nullptr;
+}
+
+// workspace of one lane (rows 2*ceil(Bt/(2L)) >= ceil(Bt/L): an upper bound for B or 2B rows)
+size_t single_ws_bytes(const tcx_unet* net, int Bt, int H, int W) {
     // Bt = B or 2B (CFG): size for the largest pass of either reading
     const int cap = max_pass_rows(net, H, W);
     const int Btc = std::min(std::min(Bt, 2 * chunk_images(Bt, cap)), cap);
     return make_plan(net, Btc, H, W, nullptr).bytes + 256;
 }
 
-extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, const float* t, int t_per_sample,
-                             const int64_t* y_cat, const float* y_cont, int B, int H, int W, float guidance, int mode,
-                             const float* scal, const float* z, uint64_t seed, uint64_t step, float* x_inout,
-                             float* eps_out, void* ws, size_t ws_bytes, void* stream) {
+// workspace of one lane (rows 2*ceil(Bt/(2L)) >= ceil(Bt/L): an upper bound for B or 2B rows)
+size_t lane_ws_bytes(const tcx_unet* net, int Bt, int H, int W, int L) {
+    const int rows = 2 * ((Bt + 2 * L - 1) / (2 * L));
+    return align_up(single_ws_bytes(net, rows, H, W), 256);
+}
+
+}  // namespace
+}  // namespace tcx
+
+using namespace tcx;
+
+extern "C" int tcx_set_sample_lanes(int lanes) {
+    const int prev = lanes_setting();
+    g_lanes = lanes < 0 ? 0 : (lanes > 4 ? 4 : lanes);
+    return prev;
+}
+
+extern "C" size_t tcx_unet_workspace_size(const tcx_unet* net, int Bt, int H, int W) {
+    if (!net) return 0;
+    const int L = lanes_setting();
+    const size_t one = single_ws_bytes(net, Bt, H, W);
+    return L > 1 ? std::max(one, (size_t)L * lane_ws_bytes(net, Bt, H, W, L) + 256) : one;
+}
+
+namespace tcx {
+namespace {
+
+// One (possibly chunked) U-Net evaluation + sampler step.  e_base: element offset of x[0] within
+// the whole sampling batch (the Philox noise counter of element i is e_base + i, so a batch
+// evaluated in pieces — chunks or concurrent lanes — draws the same noise as in one piece).
+int unet_eval_impl(const tcx_unet* net, const float* x, float* x2, const float* t, int t_per_sample,
+                   const int64_t* y_cat, const float* y_cont, int B, int H, int W, float guidance, int mode,
+                   const float* scal, const float* z, uint64_t seed, uint64_t step, float* x_inout, float* eps_out,
+                   void* ws, size_t ws_bytes, hipStream_t st, size_t e_base) {
     TCX_TRY(validate(net, B, H, W));
     TCX_REQUIRE(x && t && y_cat && y_cont && ws, "tcx_unet_eval: null pointer");
     TCX_REQUIRE(mode >= 0 && mode <= 4, "tcx_unet_eval: bad mode");
@@ -728,7 +787,6 @@ extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, con
     const size_t need = make_plan(net, Btc, H, W, nullptr).bytes;
     TCX_REQUIRE(need + (base - (char*)ws) <= ws_bytes, "tcx_unet_eval: workspace too small (%zu < %zu)", ws_bytes,
                 need + 256);
-    hipStream_t st = (hipStream_t)stream;
     const size_t HW = (size_t)H * W;
     for (int c0 = 0; c0 < B; c0 += Bc) {
         const int bc = std::min(Bc, B - c0);
@@ -741,10 +799,21 @@ extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, con
         a.r = P.r; a.out_b = net->out_b; a.B = bc; a.H = H; a.W = W; a.cfg = cfg; a.guidance = guidance;
         a.mode = mode; a.scal = scal; a.x = x + e0; a.x_inout = x_inout ? x_inout + e0 : nullptr;
         a.x2 = x2 ? x2 + e0 : nullptr; a.eps_out = eps_out ? eps_out + e0 : nullptr; a.z = z ? z + e0 : nullptr;
-        a.seed = seed; a.step = step; a.e0 = e0;
+        a.seed = seed; a.step = step; a.e0 = e_base + e0;
         TCX_TRY(launch_step(a, st));
     }
     return TCX_OK;
+}
+
+}  // namespace
+}  // namespace tcx
+
+extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, const float* t, int t_per_sample,
+                             const int64_t* y_cat, const float* y_cont, int B, int H, int W, float guidance, int mode,
+                             const float* scal, const float* z, uint64_t seed, uint64_t step, float* x_inout,
+                             float* eps_out, void* ws, size_t ws_bytes, void* stream) {
+    return unet_eval_impl(net, x, x2, t, t_per_sample, y_cat, y_cont, B, H, W, guidance, mode, scal, z, seed, step,
+                          x_inout, eps_out, ws, ws_bytes, (hipStream_t)stream, 0);
 }
 
 extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
@@ -752,6 +821,40 @@ extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_ca
                               uint64_t seed, void* ws, size_t ws_bytes, void* stream) {
     TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_sde_sample: bad args");
     const size_t img = (size_t)B * H * W;
+    const int L = std::min(lanes_setting(), B);
+    const int rows = guidance > 0.f ? 2 * B : B;
+    LaneSync* ls = L > 1 ? lane_sync() : nullptr;
+    if (ls && ws_bytes >= (size_t)L * lane_ws_bytes(net, rows, H, W, L) + 256) {
+        const size_t HW = (size_t)H * W;
+        const size_t lws = lane_ws_bytes(net, rows, H, W, L);
+        char* wbase = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
+        hipStream_t st = (hipStream_t)stream;
+        TCX_REQUIRE(hipEventRecord(ls->ev[4], st) == hipSuccess, "tcx_sde_sample: event record");
+        for (int l = 0; l < L; ++l)
+            TCX_REQUIRE(hipStreamWaitEvent(ls->s[l], ls->ev[4], 0) == hipSuccess, "tcx_sde_sample: stream wait");
+        for (int i = 0; i <= n_steps; ++i) {
+            const float* row = scal_table + (size_t)i * TCX_SCAL;
+            for (int l = 0; l < L; ++l) {
+                const int b0 = (int)((long long)B * l / L), b1 = (int)((long long)B * (l + 1) / L);
+                const size_t e = (size_t)b0 * HW;
+                if (i < n_steps) {
+                    TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, y_cat + b0, y_cont + (size_t)b0 * net->y_cont_dim,
+                                           b1 - b0, H, W, guidance, 1, row,
+                                           noise ? noise + (size_t)i * img + e : nullptr, seed, (uint64_t)i, x + e,
+                                           nullptr, wbase + l * lws, lws, ls->s[l], e));
+                } else {  // final projection -> image written over x
+                    TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, y_cat + b0, y_cont + (size_t)b0 * net->y_cont_dim,
+                                           b1 - b0, H, W, guidance, 2, row, nullptr, seed, 0, nullptr, x + e,
+                                           wbase + l * lws, lws, ls->s[l], e));
+                }
+            }
+        }
+        for (int l = 0; l < L; ++l) {
+            TCX_REQUIRE(hipEventRecord(ls->ev[l], ls->s[l]) == hipSuccess, "tcx_sde_sample: event record");
+            TCX_REQUIRE(hipStreamWaitEvent(st, ls->ev[l], 0) == hipSuccess, "tcx_sde_sample: stream wait");
+        }
+        return TCX_OK;
+    }
     for (int i = 0; i < n_steps; ++i) {
         const float* row = scal_table + (size_t)i * TCX_SCAL;
         TCX_TRY(tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 1, row,
