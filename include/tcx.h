@@ -278,6 +278,17 @@ int tcx_gemm(int M, int N, int K, float alpha, const float* A, long long sa_m, l
              const float* B, long long sb_k, long long sb_n, float beta, float* C, long long sc_m,
              long long sc_n, const float* bias, int batch, int bdiv, long long sa_hi, long long sa_lo,
              long long sb_hi, long long sb_lo, long long sc_hi, long long sc_lo, void* stream);
+/* tcx_gemm with caller scratch for split-K: when the output tiles cannot fill the chip (e.g. the
+ * batch-256 linears of DiffusionPriorFiLM, diffusion_prior.py:39-54) the reduction is split into
+ * up to 16 ranges written to ws as raw partials and summed in a fixed order by a second kernel
+ * (deterministic).  tcx_gemm_workspace returns the bytes needed (0: no split for this shape);
+ * with less scratch than that the call runs unsplit. */
+size_t tcx_gemm_workspace(int M, int N, int K, int batch);
+int tcx_gemm_ws(int M, int N, int K, float alpha, const float* A, long long sa_m, long long sa_k,
+                const float* B, long long sb_k, long long sb_n, float beta, float* C, long long sc_m,
+                long long sc_n, const float* bias, int batch, int bdiv, long long sa_hi, long long sa_lo,
+                long long sb_hi, long long sb_lo, long long sc_hi, long long sc_lo, void* ws,
+                size_t ws_bytes, void* stream);
 
 /* Conv2d weight gradient dw[Cout][C1+C2][ks][ks] (= beta*dw + ...) from the NHWC input
  * [x1 | x2] [Bt][H][W][C1+C2] and the output gradient dy [Bt][Ho][Wo][Cout] (circular or zero

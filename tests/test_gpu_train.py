@@ -233,6 +233,30 @@ def test_gemm_strided_batched_vs_torch():
     assert err(Cd, ref) < 2e-5
 
 
+def test_gemm_split_k_vs_torch_and_deterministic():
+    """Few output tiles + long K: tcx_gemm_ws splits the reduction (raw partials + fixed-order sum,
+    then alpha/beta/bias) — checked against fp64 torch, strided/batched, and for bitwise
+    run-to-run reproducibility."""
+    from toycrystals_amd._lib import lib
+    from toycrystals_amd.functional import gemm
+    M, N, K = 64, 200, 2048
+    assert int(lib().tcx_gemm_workspace(M, N, K, 2)) > 0  # this shape splits
+    g = torch.Generator().manual_seed(17)
+    A = torch.randn(2, M, K, generator=g)
+    Bm = torch.randn(2, N, K, generator=g)  # used transposed: B(k, n) = Bm[n, k]
+    C = torch.randn(2, M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    ref = 0.5 * A.double() @ Bm.double().transpose(1, 2) + 2.0 * C.double() + bias.double()
+    outs = []
+    for _ in range(2):
+        Ad, Bd, Cd, bd = cu(A), cu(Bm), cu(C), cu(bias)
+        gemm(M, N, K, Ad, K, 1, Bd, 1, K, Cd, N, 1, alpha=0.5, beta=2.0, bias=bd, batch=2, bdiv=2,
+             a_hl=(0, M * K), b_hl=(0, N * K), c_hl=(0, M * N))
+        outs.append(Cd)
+    assert err(outs[0], ref) < 2e-5
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_embedding_cat_layernorm_film_vs_torch():
     from toycrystals_amd import functional as TF
     g = torch.Generator().manual_seed(17)

@@ -36,6 +36,10 @@ struct GemmParams {
     int bdiv;  // batch z -> (z / bdiv, z % bdiv) offsets
     long long sah, sal, sbh, sbl, sch, scl;
     int nmblk, nnblk;
+    // split-K (tcx_gemm_ws): part != null -> grid.y = batch * nsplit, split s reduces chunks
+    // [s*kcs, (s+1)*kcs) into part[s][z][M][N] (raw sums); k_gemm_reduce applies alpha/beta/bias
+    float* part;
+    int nsplit, kcs;
 };
 
 __device__ __forceinline__ float4 ld4g(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -46,7 +50,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
     constexpr int BN = 32 * NT;
     __shared__ __attribute__((aligned(16))) float As[2][GBM * GLD];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN * GLD];
-    const int z = blockIdx.y;
+    const int zz = blockIdx.y;
+    const int z = p.part ? zz / p.nsplit : zz;
+    const int sk = p.part ? zz - z * p.nsplit : 0;
     const int zh = z / p.bdiv, zl = z - zh * p.bdiv;
     const float* A = p.A + zh * p.sah + zl * p.sal;
     const float* B = p.B + zh * p.sbh + zl * p.sbl;
@@ -157,13 +163,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
     const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
-    const int nch = (p.K + GBK - 1) / GBK;
-    load(0);
+    const int nch_all = (p.K + GBK - 1) / GBK;
+    const int cb = p.part ? sk * p.kcs : 0;
+    const int nch = p.part ? min(p.kcs, nch_all - cb) : nch_all;
+    load(cb * GBK);
     store(0);
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
         const int cur = c & 1;
-        if (c + 1 < nch) load((c + 1) * GBK);
+        if (c + 1 < nch) load((cb + c + 1) * GBK);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const float4 fa = *reinterpret_cast<const float4*>(&As[cur][(wv * 32 + li) * GLD + lh * 16 + g * 4]);
@@ -183,6 +191,20 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
         if (c + 1 < nch) store(cur ^ 1);
         __syncthreads();
     }
+    if (p.part) {  // raw partial sums of this K split, dense [M][N]
+        float* P = p.part + ((size_t)sk * gridDim.y / p.nsplit + z) * (size_t)p.M * p.N;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int col = n0 + n * 32 + li;
+            if (col >= p.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (row < p.M) P[(size_t)row * p.N + col] = acc[n][r];
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
         const int col = n0 + n * 32 + li;
@@ -201,9 +223,27 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
     }
 }
 
+// C[z][m][n] = alpha * sum_s part[s][z][m][n] (fixed order) + beta * C + bias[n]
+__global__ __launch_bounds__(256) void k_gemm_reduce(GemmParams p, int batch) {
+    const size_t MN = (size_t)p.M * p.N;
+    const size_t n_all = MN * batch;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n_all; i += (size_t)gridDim.x * blockDim.x) {
+        const int z = (int)(i / MN);
+        const size_t e = i - (size_t)z * MN;
+        const int row = (int)(e / p.N), col = (int)(e - (size_t)row * p.N);
+        float v = 0.f;
+        for (int s = 0; s < p.nsplit; ++s) v += p.part[((size_t)s * batch + z) * MN + e];
+        const int zh = z / p.bdiv, zl = z - zh * p.bdiv;
+        float* cp = p.C + zh * p.sch + zl * p.scl + row * p.scm + col * p.scn;
+        float o = p.alpha * v;
+        if (p.beta != 0.f) o += p.beta * *cp;
+        *cp = o + (p.bias ? p.bias[col] : 0.f);
+    }
+}
+
 template <int NT>
 int launch_gemm_nt(const GemmParams& p, int la, int lb, int batch, hipStream_t st) {
-    const dim3 grid(p.nmblk * p.nnblk, batch);
+    const dim3 grid(p.nmblk * p.nnblk, batch * (p.part ? p.nsplit : 1));
 #define TCX_G(A_, B_) hipLaunchKernelGGL((k_gemm<NT, A_, B_>), grid, dim3(256), 0, st, p)
     if (la == 0 && lb == 0) TCX_G(0, 0);
     else if (la == 0 && lb == 1) TCX_G(0, 1);
@@ -402,10 +442,29 @@ void wgrad_plan(int M, int K, int Cout, int* nt, int* nsplit, int* cps, int* nkb
 
 using namespace tcx;
 
-extern "C" int tcx_gemm(int M, int N, int K, float alpha, const float* A, long long sa_m, long long sa_k,
-                        const float* B, long long sb_k, long long sb_n, float beta, float* C, long long sc_m,
-                        long long sc_n, const float* bias, int batch, int bdiv, long long sa_hi, long long sa_lo,
-                        long long sb_hi, long long sb_lo, long long sc_hi, long long sc_lo, void* stream) {
+namespace tcx {
+namespace {
+
+// split-K plan: when the output tiles cannot fill the chip (fewer than 256) and K is long, split
+// the reduction so that ~512 workgroups run; each split covers >= 4 chunks of 32
+void gemm_split_plan(int M, int N, int K, int batch, int* nsplit, int* kcs) {
+    const int nt = N <= 32 ? 1 : (N <= 64 ? 2 : 3);
+    const long long tiles = (long long)cdiv(M, GBM) * cdiv(N, 32 * nt) * batch;
+    const int nch = (K + GBK - 1) / GBK;
+    *nsplit = 1;
+    *kcs = nch;
+    if (tiles >= 256 || nch < 8) return;
+    int s = (int)std::min<long long>((512 + tiles - 1) / tiles, 16);
+    s = std::min(s, nch / 4);
+    if (s < 2) return;
+    *kcs = (nch + s - 1) / s;
+    *nsplit = (nch + *kcs - 1) / *kcs;
+}
+
+int gemm_impl(int M, int N, int K, float alpha, const float* A, long long sa_m, long long sa_k, const float* B,
+              long long sb_k, long long sb_n, float beta, float* C, long long sc_m, long long sc_n, const float* bias,
+              int batch, int bdiv, long long sa_hi, long long sa_lo, long long sb_hi, long long sb_lo,
+              long long sc_hi, long long sc_lo, void* ws, size_t ws_bytes, hipStream_t st) {
     TCX_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 0 && bdiv >= 1, "tcx_gemm: bad sizes");
     TCX_REQUIRE(C && (K == 0 || (A && B)), "tcx_gemm: null pointer");
     if (M == 0 || N == 0 || batch == 0) return TCX_OK;
@@ -427,13 +486,52 @@ extern "C" int tcx_gemm(int M, int N, int K, float alpha, const float* A, long l
     const int nt = N <= 32 ? 1 : (N <= 64 ? 2 : 3);
     p.nmblk = cdiv(M, GBM);
     p.nnblk = cdiv(N, 32 * nt);
-    hipStream_t st = (hipStream_t)stream;
     if (K == 0) {  // C = beta * C + bias: run the kernel with an empty reduction
         la = 2; lb = 2;
     }
-    if (nt == 3) return launch_gemm_nt<3>(p, la, lb, batch, st);
-    if (nt == 2) return launch_gemm_nt<2>(p, la, lb, batch, st);
-    return launch_gemm_nt<1>(p, la, lb, batch, st);
+    int ns = 1, kcs = 0;
+    if (ws && K > 0) gemm_split_plan(M, N, K, batch, &ns, &kcs);
+    if (ns > 1 && ws_bytes >= (size_t)ns * batch * M * N * sizeof(float)) {
+        p.part = static_cast<float*>(ws);
+        p.nsplit = ns;
+        p.kcs = kcs;
+    }
+    int rc;
+    if (nt == 3) rc = launch_gemm_nt<3>(p, la, lb, batch, st);
+    else if (nt == 2) rc = launch_gemm_nt<2>(p, la, lb, batch, st);
+    else rc = launch_gemm_nt<1>(p, la, lb, batch, st);
+    if (rc != TCX_OK || !p.part) return rc;
+    const size_t n_all = (size_t)batch * M * N;
+    const int blocks = (int)std::min<size_t>((n_all + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_gemm_reduce, dim3(blocks), dim3(256), 0, st, p, batch);
+    return check_launch("tcx_gemm(split-K reduce)");
+}
+
+}  // namespace
+}  // namespace tcx
+
+extern "C" int tcx_gemm(int M, int N, int K, float alpha, const float* A, long long sa_m, long long sa_k,
+                        const float* B, long long sb_k, long long sb_n, float beta, float* C, long long sc_m,
+                        long long sc_n, const float* bias, int batch, int bdiv, long long sa_hi, long long sa_lo,
+                        long long sb_hi, long long sb_lo, long long sc_hi, long long sc_lo, void* stream) {
+    return gemm_impl(M, N, K, alpha, A, sa_m, sa_k, B, sb_k, sb_n, beta, C, sc_m, sc_n, bias, batch, bdiv, sa_hi,
+                     sa_lo, sb_hi, sb_lo, sc_hi, sc_lo, nullptr, 0, (hipStream_t)stream);
+}
+
+extern "C" size_t tcx_gemm_workspace(int M, int N, int K, int batch) {
+    if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
+    int ns, kcs;
+    gemm_split_plan(M, N, K, batch, &ns, &kcs);
+    return ns > 1 ? (size_t)ns * batch * M * N * sizeof(float) : 0;
+}
+
+extern "C" int tcx_gemm_ws(int M, int N, int K, float alpha, const float* A, long long sa_m, long long sa_k,
+                           const float* B, long long sb_k, long long sb_n, float beta, float* C, long long sc_m,
+                           long long sc_n, const float* bias, int batch, int bdiv, long long sa_hi, long long sa_lo,
+                           long long sb_hi, long long sb_lo, long long sc_hi, long long sc_lo, void* ws,
+                           size_t ws_bytes, void* stream) {
+    return gemm_impl(M, N, K, alpha, A, sa_m, sa_k, B, sb_k, sb_n, beta, C, sc_m, sc_n, bias, batch, bdiv, sa_hi,
+                     sa_lo, sb_hi, sb_lo, sc_hi, sc_lo, ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" size_t tcx_conv_wgrad_workspace(int Bt, int Ho, int Wo, int Cin, int Cout, int ks) {

@@ -328,6 +328,41 @@ __global__ __launch_bounds__(256) void k_colsum_fold(const double* __restrict__ 
     }
 }
 
+// Column sums of one short [rows][C] matrix (a Linear bias gradient over the batch, rows <= 4096)
+// in ONE launch: block = 32 float4 column quads x 8 row groups; each thread sums its rows in fp64,
+// then a fixed-order fold over the 8 groups (deterministic).  The general path (partials, fold,
+// total) launched 4 blocks for a 256 x 4096 matrix and three kernels per bias.
+__global__ __launch_bounds__(256) void k_colsum_small(const float* __restrict__ x, int rows, int C,
+                                                      float* __restrict__ total, float beta) {
+    __shared__ double red[8][32][4];
+    const int q = blockIdx.x * 32 + (threadIdx.x & 31);  // column quad
+    const int rg = threadIdx.x >> 5;
+    const bool ok = q * 4 < C;
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    if (ok) {
+#pragma unroll 8
+        for (int r = rg; r < rows; r += 8) {
+            const float4 v = *reinterpret_cast<const float4*>(x + (size_t)r * C + q * 4);
+            s0 += v.x; s1 += v.y; s2 += v.z; s3 += v.w;
+        }
+    }
+    red[rg][threadIdx.x & 31][0] = s0;
+    red[rg][threadIdx.x & 31][1] = s1;
+    red[rg][threadIdx.x & 31][2] = s2;
+    red[rg][threadIdx.x & 31][3] = s3;
+    __syncthreads();
+    if (threadIdx.x < 128) {
+        const int cq = threadIdx.x >> 2, e = threadIdx.x & 3;
+        const int c = (blockIdx.x * 32 + cq) * 4 + e;
+        if (c < C) {
+            double t = 0;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) t += red[g][cq][e];
+            total[c] = beta != 0.f ? beta * total[c] + (float)t : (float)t;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_colsum_total(const double* __restrict__ tot_b, int Bt, int C,
                                                       float* __restrict__ total, float beta) {
     const int lane = threadIdx.x & 31;
@@ -947,6 +982,10 @@ extern "C" int tcx_colsum(const float* x, int Bt, int HW, int C, float* per_batc
     double* part = reinterpret_cast<double*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
     double* tot_b = part + (size_t)Bt * nsplit * C;
     hipStream_t st = (hipStream_t)stream;
+    if (Bt == 1 && !per_batch && total && HW <= 4096 && C % 4 == 0 && aligned16(x)) {
+        hipLaunchKernelGGL(k_colsum_small, dim3(cdiv(C / 4, 32)), dim3(256), 0, st, x, HW, C, total, beta);
+        return check_launch("tcx_colsum small");
+    }
     if (Bt > 0) {
         const bool vec = C % 4 == 0 && aligned16(x);
         const int ncol = vec ? C / 4 : C;

@@ -97,6 +97,9 @@ _SIGS = {
     # training path
     "tcx_gemm": (c_int, [c_int, c_int, c_int, c_float, c_fp, c_ll, c_ll, c_fp, c_ll, c_ll, c_float, c_fp, c_ll, c_ll,
                          c_fp, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_fp]),
+    "tcx_gemm_workspace": (c_size, [c_int, c_int, c_int, c_int]),
+    "tcx_gemm_ws": (c_int, [c_int, c_int, c_int, c_float, c_fp, c_ll, c_ll, c_fp, c_ll, c_ll, c_float, c_fp, c_ll,
+                            c_ll, c_fp, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_fp, c_size, c_fp]),
     "tcx_conv_wgrad_workspace": (c_size, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "tcx_conv_wgrad": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_int, c_int, c_int, c_int, c_int,
                                c_float, c_fp, c_fp, c_size, c_fp]),

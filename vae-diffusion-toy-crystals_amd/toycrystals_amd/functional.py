@@ -58,11 +58,14 @@ def _c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 # ---------------------------------------------------------------- GEMM helper
 def gemm(M, N, K, A, sa_m, sa_k, B, sb_k, sb_n, C, sc_m, sc_n, alpha=1.0, beta=0.0, bias=None, batch=1, bdiv=1,
          a_hl=(0, 0), b_hl=(0, 0), c_hl=(0, 0), a_off=0, b_off=0, c_off=0):
-    """C = alpha A B + beta C (+ bias) through tcx_gemm; offsets are in floats."""
+    """C = alpha A B + beta C (+ bias) through tcx_gemm_ws (split-K scratch when the shape wants it);
+    offsets are in floats."""
     L = lib()
-    check(L.tcx_gemm(M, N, K, float(alpha), ptr(A) + 4 * a_off, sa_m, sa_k, ptr(B) + 4 * b_off, sb_k, sb_n,
-                     float(beta), ptr(C) + 4 * c_off, sc_m, sc_n, ptr(bias), batch, bdiv, a_hl[0], a_hl[1], b_hl[0],
-                     b_hl[1], c_hl[0], c_hl[1], _st(C)), "tcx_gemm")
+    nb = int(L.tcx_gemm_workspace(M, N, K, batch))
+    ws = _ws(C.device, nb) if nb else None
+    check(L.tcx_gemm_ws(M, N, K, float(alpha), ptr(A) + 4 * a_off, sa_m, sa_k, ptr(B) + 4 * b_off, sb_k, sb_n,
+                        float(beta), ptr(C) + 4 * c_off, sc_m, sc_n, ptr(bias), batch, bdiv, a_hl[0], a_hl[1], b_hl[0],
+                        b_hl[1], c_hl[0], c_hl[1], ptr(ws) if ws is not None else None, nb, _st(C)), "tcx_gemm")
 
 
 def _colsum_total(x: torch.Tensor, rows: int, C: int) -> torch.Tensor:
