@@ -259,6 +259,15 @@ int tcx_randn(float* out, size_t n, uint64_t seed, uint64_t stream_id, void* str
  * (diffusion_prior.py:39-54, 103-110) and the VAE FCs (vae.py:28-33). */
 int tcx_linear(const float* x1, int K1, const float* x2, int K2, const float* wpk, const float* b,
                const float* resid, float* y, int M, int N, int npad, int kpad, int act, void* stream);
+/* tcx_linear with caller scratch: for skinny batches whose output tiles cannot fill the chip
+ * (DDIM sampling of the prior over 36 samples, diffusion_prior.py:203-252) each source is a
+ * split-K GEMM (raw partials in ws) and one fixed-order reduce applies bias, residual and the
+ * activation (deterministic).  tcx_linear_workspace returns the bytes needed (0: plain
+ * tcx_linear, which tcx_linear_ws then runs). */
+size_t tcx_linear_workspace(int M, int N, int K1, int K2);
+int tcx_linear_ws(const float* x1, int K1, const float* x2, int K2, const float* wpk, const float* b,
+                  const float* resid, float* y, int M, int N, int npad, int kpad, int act, void* ws,
+                  size_t ws_bytes, void* stream);
 
 /* LayerNorm over the last dim with optional FiLM: y = LN(x)*(1+gamma)+beta where
  * gamma = gb[:, :W], beta = gb[:, W:2W] (FiLMResBlock, diffusion_prior.py:49-52). */

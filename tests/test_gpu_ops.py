@@ -270,9 +270,13 @@ def test_attention(B, C, N, heads):
     close(o.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("split", [False, True], ids=["plain", "ws"])
 @pytest.mark.parametrize("M,K1,K2,N,act", [(256, 1024, 0, 4096, 3), (5, 64, 64, 1024, 0), (7, 4, 0, 64, 3),
-                                            (300, 2048, 2048, 200, 1)])
-def test_linear(M, K1, K2, N, act):
+                                            (300, 2048, 2048, 200, 1), (36, 1024, 0, 2048, 3),
+                                            (36, 1024, 1024, 1024, 0), (36, 4096, 0, 1024, 2)])
+def test_linear(M, K1, K2, N, act, split):
+    """tcx_linear, and tcx_linear_ws (split-K over caller scratch for skinny batches: the DDIM
+    sampler's 36-row linears; it falls back to tcx_linear where the tiles fill the chip)."""
     x1 = rng.standard_normal((M, K1))
     x2 = rng.standard_normal((M, K2)) if K2 else None
     w = rng.standard_normal((N, K1 + K2)) / np.sqrt(K1 + K2)
@@ -285,8 +289,17 @@ def test_linear(M, K1, K2, N, act):
     y = torch.empty((M, N), device="cuda")
     x1d, rd, bd = dev(x1), dev(r), dev(b)
     x2d = dev(x2) if x2 is not None else None
-    chk(L().tcx_linear(x1d.data_ptr(), K1, x2d.data_ptr() if x2d is not None else None, K2, wpk.data_ptr(),
-                       bd.data_ptr(), rd.data_ptr(), y.data_ptr(), M, N, npad, kpad, act, st()))
+    if split:
+        nb = int(L().tcx_linear_workspace(M, N, K1, K2))
+        if M == 36:
+            assert nb > 0
+        ws = torch.empty(max(nb, 1), dtype=torch.uint8, device="cuda")
+        chk(L().tcx_linear_ws(x1d.data_ptr(), K1, x2d.data_ptr() if x2d is not None else None, K2, wpk.data_ptr(),
+                              bd.data_ptr(), rd.data_ptr(), y.data_ptr(), M, N, npad, kpad, act, ws.data_ptr(), nb,
+                              st()))
+    else:
+        chk(L().tcx_linear(x1d.data_ptr(), K1, x2d.data_ptr() if x2d is not None else None, K2, wpk.data_ptr(),
+                           bd.data_ptr(), rd.data_ptr(), y.data_ptr(), M, N, npad, kpad, act, st()))
     torch.cuda.synchronize()
     close(y.cpu().numpy(), ref)
 

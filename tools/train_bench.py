@@ -116,8 +116,29 @@ def bench_prior():
             "samples_per_s": round(B / dt, 1), "tflops": round(0.6180e9 * B / dt / 1e12, 2)}
 
 
+def bench_ddim():
+    """DDIM-50 sampling of the w1024 x 8 prior for the 36-sample grid (config 4's sampler, HBM-bound:
+    the 412 MB of weights are read once per step)."""
+    from toycrystals_amd.models.diffusion_prior import DiffusionPriorFiLM, DiffusionSchedule
+    torch.manual_seed(0)
+    n = 36
+    m = DiffusionPriorFiLM(32, 4, 4, t_emb_dim=64, width=1024, n_blocks=8, y_cat_emb_dim=64).cuda().eval()
+    sched = DiffusionSchedule.linear(1000, 1e-4, 0.05, torch.device("cuda"))
+    y_cat = (torch.arange(n, device="cuda") % 4).to(torch.int64)
+    y_cont = torch.rand(n, 4, device="cuda")
+    wbytes = sum(p.numel() for p in m.parameters()) * 4
+
+    def step():
+        with torch.no_grad():
+            sched.ddim_sample(m, y_cat, y_cont, n_steps=50)
+
+    dt = timed(step)
+    return {"model": "DiffusionPriorFiLM(w=1024, 8 blocks) DDIM-50", "batch": n, "ms_per_sample_call": round(dt * 1e3, 3),
+            "ms_per_ddim_step": round(dt * 1e3 / 50, 4), "weight_stream_TBps": round(wbytes * 50 / dt / 1e12, 2)}
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["score", "vae", "prior"]
-    fns = {"score": bench_score, "vae": bench_vae, "prior": bench_prior}
+    fns = {"score": bench_score, "vae": bench_vae, "prior": bench_prior, "ddim": bench_ddim}
     for w in which:
         print(json.dumps(fns[w]()), flush=True)

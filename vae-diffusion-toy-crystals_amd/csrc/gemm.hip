@@ -40,6 +40,9 @@ struct GemmParams {
     // [s*kcs, (s+1)*kcs) into part[s][z][M][N] (raw sums); k_gemm_reduce applies alpha/beta/bias
     float* part;
     int nsplit, kcs;
+    // reduce-only extras (tcx_linear_ws): residual [M][N] (row stride N) and activation
+    const float* resid;
+    int act;
 };
 
 __device__ __forceinline__ float4 ld4g(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -237,7 +240,12 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmParams p, int batch) {
         float* cp = p.C + zh * p.sch + zl * p.scl + row * p.scm + col * p.scn;
         float o = p.alpha * v;
         if (p.beta != 0.f) o += p.beta * *cp;
-        *cp = o + (p.bias ? p.bias[col] : 0.f);
+        o += p.bias ? p.bias[col] : 0.f;
+        if (p.resid) o += p.resid[(size_t)row * p.N + col];
+        if (p.act == 1) o = fmaxf(o, 0.f);
+        else if (p.act == 2) o = 1.f / (1.f + expf(-o));
+        else if (p.act == 3) o = silu_f(o);
+        *cp = o;
     }
 }
 
@@ -532,6 +540,80 @@ extern "C" int tcx_gemm_ws(int M, int N, int K, float alpha, const float* A, lon
                            size_t ws_bytes, void* stream) {
     return gemm_impl(M, N, K, alpha, A, sa_m, sa_k, B, sb_k, sb_n, beta, C, sc_m, sc_n, bias, batch, bdiv, sa_hi,
                      sa_lo, sb_hi, sb_lo, sc_hi, sc_lo, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------- skinny linears (split-K)
+namespace tcx {
+namespace {
+
+// y[M][N] = act(x1 W1^T + x2 W2^T + b + resid) with W = wpk [npad][kpad] (k < K1 from x1, then x2):
+// each source is a split-K GEMM writing raw partials (splits >= 2 chunks of 32), one fixed-order
+// reduce applies bias / residual / activation.  Plan: the splits of both sources together.
+struct LinPlan {
+    int s1, k1cs, s2, k2cs;
+};
+
+LinPlan linear_plan(int M, int N, int K1, int K2) {
+    const long long tiles = (long long)cdiv(M, GBM) * cdiv(N, 96);
+    auto one = [&](int K, int& s, int& kcs) {
+        const int nch = (K + GBK - 1) / GBK;
+        s = (int)std::min<long long>((512 + tiles - 1) / tiles, 16);
+        s = std::max(1, std::min(s, nch / 2));
+        kcs = (nch + s - 1) / s;
+        s = (nch + kcs - 1) / kcs;
+    };
+    LinPlan lp{};
+    one(K1, lp.s1, lp.k1cs);
+    if (K2 > 0) one(K2, lp.s2, lp.k2cs);
+    return lp;
+}
+
+bool linear_wants_split(int M, int N, int K1, int K2, const float* x1, const float* x2) {
+    const long long tiles = (long long)cdiv(M, GBM) * cdiv(N, 96);
+    return tiles < 128 && K1 % 4 == 0 && K2 % 4 == 0 && K1 + K2 >= 256 && aligned16(x1) && (!x2 || aligned16(x2));
+}
+
+}  // namespace
+}  // namespace tcx
+
+extern "C" size_t tcx_linear_workspace(int M, int N, int K1, int K2) {
+    if (M <= 0 || N <= 0 || K1 <= 0 || K2 < 0 || !linear_wants_split(M, N, K1, K2, nullptr, nullptr)) return 0;
+    const LinPlan lp = linear_plan(M, N, K1, K2);
+    return (size_t)(lp.s1 + lp.s2) * M * N * sizeof(float);
+}
+
+extern "C" int tcx_linear_ws(const float* x1, int K1, const float* x2, int K2, const float* wpk, const float* b,
+                             const float* resid, float* y, int M, int N, int npad, int kpad, int act, void* ws,
+                             size_t ws_bytes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const size_t need = tcx_linear_workspace(M, N, K1, K2);
+    if (need == 0 || !ws || ws_bytes < need || !linear_wants_split(M, N, K1, K2, x1, x2) || !aligned16(wpk))
+        return tcx_linear(x1, K1, x2, K2, wpk, b, resid, y, M, N, npad, kpad, act, stream);
+    TCX_REQUIRE(x1 && wpk && y && M >= 0 && N > 0 && K1 > 0 && K2 >= 0 && (K2 == 0) == (x2 == nullptr),
+                "tcx_linear_ws: bad args");
+    TCX_REQUIRE(npad >= N && kpad >= K1 + K2 && kpad % 4 == 0 && act >= 0 && act <= 3, "tcx_linear_ws: bad padding");
+    const LinPlan lp = linear_plan(M, N, K1, K2);
+    float* part = static_cast<float*>(ws);
+    auto src = [&](const float* x, int K, int koff, int s, int kcs, float* pbase) -> int {
+        GemmParams p{};
+        p.M = M; p.N = N; p.K = K; p.alpha = 1.f; p.beta = 0.f;
+        p.A = x; p.sam = K; p.sak = 1;
+        p.B = wpk + koff; p.sbk = 1; p.sbn = kpad;
+        p.C = y; p.scm = N; p.scn = 1; p.bdiv = 1;
+        p.nmblk = cdiv(M, GBM);
+        p.nnblk = cdiv(N, 96);
+        p.part = pbase; p.nsplit = s; p.kcs = kcs;
+        return launch_gemm_nt<3>(p, 0, 0, 1, st);
+    };
+    TCX_TRY(src(x1, K1, 0, lp.s1, lp.k1cs, part));
+    if (K2 > 0) TCX_TRY(src(x2, K2, K1, lp.s2, lp.k2cs, part + (size_t)lp.s1 * M * N));
+    GemmParams r{};
+    r.M = M; r.N = N; r.alpha = 1.f; r.beta = 0.f; r.C = y; r.scm = N; r.scn = 1; r.bdiv = 1;
+    r.bias = b; r.part = part; r.nsplit = lp.s1 + lp.s2; r.resid = resid; r.act = act;
+    const size_t n_all = (size_t)M * N;
+    hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)std::min<size_t>((n_all + 255) / 256, 4096)), dim3(256), 0, st,
+                       r, 1);
+    return check_launch("tcx_linear_ws reduce");
 }
 
 extern "C" size_t tcx_conv_wgrad_workspace(int Bt, int Ho, int Wo, int Cin, int Cout, int ks) {

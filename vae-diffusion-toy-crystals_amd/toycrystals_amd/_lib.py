@@ -93,6 +93,9 @@ _SIGS = {
                                c_fp, c_size, c_fp]),
     "tcx_randn": (c_int, [c_fp, c_size, c_u64, c_u64, c_fp]),
     "tcx_linear": (c_int, [c_fp, c_int, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp]),
+    "tcx_linear_workspace": (c_size, [c_int, c_int, c_int, c_int]),
+    "tcx_linear_ws": (c_int, [c_fp, c_int, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp,
+                              c_size, c_fp]),
     "tcx_layernorm_film": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_float, c_fp]),
     # training path
     "tcx_gemm": (c_int, [c_int, c_int, c_int, c_float, c_fp, c_ll, c_ll, c_fp, c_ll, c_ll, c_float, c_fp, c_ll, c_ll,

@@ -118,8 +118,11 @@ def _lin(x1, x2, packed, act, resid=None, out=None):
     K2 = x2.shape[1] if x2 is not None else 0
     assert K1 + K2 == k, (K1, K2, k)
     y = out if out is not None else torch.empty((M, n), device=x1.device, dtype=torch.float32)
-    check(lib().tcx_linear(ptr(x1), K1, ptr(x2), K2, ptr(wpk), ptr(b), ptr(resid), ptr(y), M, n, npad, kpad, act,
-                           stream_ptr(x1.device)), "tcx_linear")
+    # skinny batches (DDIM over 36 samples) split K over the chip (tcx_linear_ws scratch)
+    nb = int(lib().tcx_linear_workspace(M, n, K1, K2))
+    ws = TF._ws(x1.device, nb) if nb else None
+    check(lib().tcx_linear_ws(ptr(x1), K1, ptr(x2), K2, ptr(wpk), ptr(b), ptr(resid), ptr(y), M, n, npad, kpad, act,
+                              ptr(ws), nb, stream_ptr(x1.device)), "tcx_linear")
     return y
 
 

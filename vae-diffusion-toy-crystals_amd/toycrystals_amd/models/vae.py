@@ -82,8 +82,10 @@ def _linear(x1, x2, packed, bias, act, resid=None):
     K2 = x2.shape[1] if x2 is not None else 0
     assert K1 + K2 == k
     y = torch.empty((M, n), device=x1.device, dtype=torch.float32)
-    check(lib().tcx_linear(ptr(x1), K1, ptr(x2), K2, ptr(wpk), ptr(bias), ptr(resid), ptr(y), M, n, npad, kpad, act,
-                           stream_ptr(x1.device)), "tcx_linear")
+    nb = int(lib().tcx_linear_workspace(M, n, K1, K2))
+    ws = TF._ws(x1.device, nb) if nb else None
+    check(lib().tcx_linear_ws(ptr(x1), K1, ptr(x2), K2, ptr(wpk), ptr(bias), ptr(resid), ptr(y), M, n, npad, kpad,
+                              act, ptr(ws), nb, stream_ptr(x1.device)), "tcx_linear")
     return y
 
 
