@@ -74,3 +74,19 @@ def test_vae_then_prior(tmp_path, dataset):
     assert (tmp_path / "results" / "diffusion_samples.png").exists()
     run(tmp_path, "train_diffusion_prior.py", "--data-path", dataset, "--width", 64, "--T", 50, "--ddim-steps", 3,
         "--latent-cache", tmp_path / "lat.pt", "--sample-only")
+
+
+def test_build_dataset_and_preview(tmp_path):
+    """build_dataset.py writes the reference's file ({x_u8 [N,1,S,S] uint8, y_cat [N] int64,
+    y_cont [N,4] f32}) from the GPU renderer; preview_data.py saves the 6 x 6 PNG grid."""
+    out = tmp_path / "data" / "toy.pt"
+    run(tmp_path, "build_dataset.py", "--out", out, "--n-samples", 50, "--render-batch", 16)
+    d = torch.load(out, weights_only=True)
+    assert set(d) == {"x_u8", "y_cat", "y_cont"}
+    assert d["x_u8"].shape == (50, 1, 64, 64) and d["x_u8"].dtype == torch.uint8
+    assert d["y_cat"].shape == (50,) and d["y_cat"].dtype == torch.int64
+    assert d["y_cont"].shape == (50, 4) and d["y_cont"].dtype == torch.float32
+    assert int(d["x_u8"].max()) == 255  # every image is max-normalised
+    run(tmp_path, "preview_data.py")
+    png = tmp_path / "results" / "preview_toycrystals.png"
+    assert png.exists() and png.stat().st_size > 10_000
