@@ -204,6 +204,26 @@ def test_sampling_lanes_match_one_lane(golden, prec, host_noise):
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
+def test_ode_lanes_match_one_lane(golden):
+    """The PF-ODE Heun sampler under tcx_set_sample_lanes: bit-identical to one lane."""
+    from toycrystals_amd._lib import lib
+    from toycrystals_amd.models.sde_score_model import VPSDE, sample_probability_flow_ode
+    m = unet(32, golden("trained32_state"))
+    B = 7
+    y_cat = (torch.arange(B) % 5).cuda()
+    y_cont = torch.rand(B, 4, generator=torch.Generator().manual_seed(5)).cuda()
+    x0 = torch.randn(B, 1, 64, 64, generator=torch.Generator().manual_seed(6)).cuda()
+    outs = []
+    try:
+        for lanes in (1, 3):
+            lib().tcx_set_sample_lanes(lanes)
+            outs.append(sample_probability_flow_ode(m, VPSDE(0.1, 30.0), y_cat, y_cont, (B, 1, 64, 64), n_steps=4,
+                                                    guidance_scale=1.5, t_end=0.005, x_init=x0.clone()))
+    finally:
+        lib().tcx_set_sample_lanes(0)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_cpu_tensors_are_rejected():
     from toycrystals_amd._lib import TcxError
     from toycrystals_amd.models.sde_score_model import CondUNetTiny

@@ -878,6 +878,43 @@ extern "C" int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_ca
     char* tail = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>((char*)ws + need), 256));
     float* d = reinterpret_cast<float*>(tail);
     float* xe = d + align_up(img, 64);
+    // concurrent lanes (tcx_set_sample_lanes): image groups on their own streams, d / x_e sliced
+    const int L = std::min(lanes_setting(), B);
+    const int rows = guidance > 0.f ? 2 * B : B;
+    LaneSync* ls = L > 1 ? lane_sync() : nullptr;
+    if (ls && need >= (size_t)L * lane_ws_bytes(net, rows, H, W, L) + 256) {
+        const size_t HW = (size_t)H * W;
+        const size_t lws = lane_ws_bytes(net, rows, H, W, L);
+        char* wbase = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
+        hipStream_t st = (hipStream_t)stream;
+        TCX_REQUIRE(hipEventRecord(ls->ev[4], st) == hipSuccess, "tcx_ode_sample: event record");
+        for (int l = 0; l < L; ++l)
+            TCX_REQUIRE(hipStreamWaitEvent(ls->s[l], ls->ev[4], 0) == hipSuccess, "tcx_ode_sample: stream wait");
+        for (int i = 0; i <= n_steps; ++i) {
+            const float* row = scal_table + (size_t)i * TCX_SCAL;
+            for (int l = 0; l < L; ++l) {
+                const int b0 = (int)((long long)B * l / L), b1 = (int)((long long)B * (l + 1) / L);
+                const size_t e = (size_t)b0 * HW;
+                const int64_t* yc = y_cat + b0;
+                const float* yv = y_cont + (size_t)b0 * net->y_cont_dim;
+                char* w = wbase + l * lws;
+                if (i < n_steps) {
+                    TCX_TRY(unet_eval_impl(net, x + e, xe + e, row, 0, yc, yv, b1 - b0, H, W, guidance, 3, row, nullptr,
+                                           0, 0, x + e, d + e, w, lws, ls->s[l], e));
+                    TCX_TRY(unet_eval_impl(net, xe + e, nullptr, row + TCX_SCAL, 0, yc, yv, b1 - b0, H, W, guidance, 4,
+                                           row, nullptr, 0, 0, x + e, d + e, w, lws, ls->s[l], e));
+                } else {
+                    TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, yc, yv, b1 - b0, H, W, guidance, 2, row,
+                                           nullptr, 0, 0, nullptr, x + e, w, lws, ls->s[l], e));
+                }
+            }
+        }
+        for (int l = 0; l < L; ++l) {
+            TCX_REQUIRE(hipEventRecord(ls->ev[l], ls->s[l]) == hipSuccess, "tcx_ode_sample: event record");
+            TCX_REQUIRE(hipStreamWaitEvent(st, ls->ev[l], 0) == hipSuccess, "tcx_ode_sample: stream wait");
+        }
+        return TCX_OK;
+    }
     for (int i = 0; i < n_steps; ++i) {
         const float* row = scal_table + (size_t)i * TCX_SCAL;
         TCX_TRY(tcx_unet_eval(net, x, xe, row, 0, y_cat, y_cont, B, H, W, guidance, 3, row, nullptr, 0, 0, x, d, ws,
