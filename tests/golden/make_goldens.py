@@ -131,7 +131,7 @@ def draw_noise(seed: int, shape, n: int):
 
 
 def gen_sampler(name: str, sampler: str, base_ch: int, B: int, steps: int, cfg: float, t_end: float,
-                beta_max: float = 30.0, state_dict=None, store_noise: bool = True) -> None:
+                beta_max: float = 30.0, state_dict=None, store_noise: bool = True, H: int = 64) -> None:
     torch.manual_seed(0)
     model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=base_ch)
     if state_dict is not None:
@@ -141,7 +141,7 @@ def gen_sampler(name: str, sampler: str, base_ch: int, B: int, steps: int, cfg: 
     y_cat = torch.tensor([i % 4 for i in range(B)], dtype=torch.int64)
     y_cont = torch.zeros(B, 4)
     y_cont[:, 1] = torch.linspace(0.0, math.pi / 3, B)
-    shape = (B, 1, 64, 64)
+    shape = (B, 1, H, H)
     seed = 1234
     n_draws = steps + 1 if sampler == "sde" else 1
     noise = draw_noise(seed, shape, n_draws)
@@ -464,6 +464,8 @@ def main() -> int:
     if want("unet256"):
         # config 5's resolution: 64x64 = 4096 tokens at the attention level (key-tiled kernel)
         gen_unet(96, 2, "unet96_b2_h256", store_weights=False, H=256)
+        # the metric's sampler at 256^2 (config 5): 2 reverse-SDE steps + projection, noise by seed
+        gen_sampler("sde96_2step_h256", "sde", 96, 2, 2, 1.5, 0.005, store_noise=False, H=256)
     if want("cfg"):
         gen_cfg("cfg16_b3")
     if want("vpsde"):

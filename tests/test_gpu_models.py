@@ -168,6 +168,25 @@ def test_trained_sde300_vs_reference(golden, prec):
     assert err < 1e-4
 
 
+def test_sde_256px_vs_reference(golden, prec):
+    """Config 5's sampler at 256x256 (base_ch 96, CFG 1.5): 2 reverse-SDE steps + the final
+    projection against the reference, noise regenerated from its seed (tests/golden/make_goldens.py
+    unet256).  Gate as for the short samplers: 1e-4 on the output and relative on x0_hat."""
+    from toycrystals_amd.models.sde_score_model import VPSDE, host_noise, sample_reverse_sde_euler_maruyama
+    g = golden("sde96_2step_h256")
+    m = unet(96)
+    B = int(g["B"])
+    shape = (B, 1, 256, 256)
+    torch.manual_seed(int(g["noise_seed"]))
+    noise = host_noise(shape, int(g["steps"]) + 1)
+    out = sample_reverse_sde_euler_maruyama(m, VPSDE(0.1, 30.0), cu(g["y_cat"]), cu(g["y_cont"]), shape,
+                                            n_steps=int(g["steps"]), guidance_scale=float(g["cfg"]),
+                                            t_end=float(g["t_end"]), noise=noise.cuda()).cpu().numpy()
+    assert out.shape == g["out"].shape
+    assert 0.0 < float(g["out"].mean()) < 1.0
+    assert np.abs(out - g["out"]).max() < 1e-4
+
+
 def test_in_kernel_noise_is_seeded_and_standard():
     from toycrystals_amd.models.sde_score_model import VPSDE, sample_reverse_sde_euler_maruyama
     m = unet(16)
