@@ -277,6 +277,87 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int H
         if (j < nk) dst[(size_t)(tg + 4 * j) * HW] = acc[j];
 }
 
+// ---------------------------------------------------------------- 8-lanes-per-pixel forms
+// For C = 32*Q (every split-path net): a pixel's C channels are 8 contiguous runs of 4Q channels,
+// one per lane of an 8-lane group, so a wave reads/writes 8 whole pixels (8*C*4 contiguous bytes)
+// per instruction group and nothing goes through an LDS tile; per-pixel reductions are three
+// xor-shuffles inside the group (fixed order).
+
+// (A first-conv of this form measured slower than k_conv_first: its per-lane 48-B output runs
+// leave every store instruction one-third coalesced, where the LDS tile writes 1 KB contiguous.)
+// Head, 8-lane form: r[b][tap][p] = sum_c silu(gn(h))[b,p,c] * w_out[c][tap].  Block 256 threads =
+// 32 pixels per pass, HP8 pixels per block (all in one image: HW % HP8 == 0).  w_out and the
+// image's scale/shift rows are staged in LDS once per block.
+constexpr int HP8 = 128;
+template <int Q>
+__global__ __launch_bounds__(256) void k_head8(const float* __restrict__ h, int HW, const float* __restrict__ tsc,
+                                               const float* __restrict__ tsh, const float* __restrict__ w_out,
+                                               float* __restrict__ r) {
+    constexpr int C = 32 * Q;
+    constexpr int CL = 4 * Q;  // channels per lane
+    __shared__ __attribute__((aligned(16))) float ws[C * 9];
+    __shared__ __attribute__((aligned(16))) float ssc[C], ssh[C];
+    const int p0 = blockIdx.x * HP8;  // first pixel (flat over b, p)
+    const int b = p0 / HW;
+    const int tid = threadIdx.x;
+    const int sub = tid & 7, pl = tid >> 3;  // lane in the pixel group, pixel of the pass
+    const int c0 = sub * CL;
+    // the first pass's loads go out before the tables are staged
+    float4 v[Q];
+    {
+        const float* src = h + (size_t)(p0 + pl) * C + c0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) v[q] = *reinterpret_cast<const float4*>(src + 4 * q);
+    }
+    for (int i = tid; i < C * 9; i += 256) ws[i] = w_out[i];
+    for (int i = tid; i < C; i += 256) {
+        ssc[i] = tsc[(size_t)b * C + i];
+        ssh[i] = tsh[(size_t)b * C + i];
+    }
+    __syncthreads();
+    for (int pass = 0; pass < HP8 / 32; ++pass) {
+        const int pg = p0 + pass * 32 + pl;
+        float4 vn[Q];
+        if (pass + 1 < HP8 / 32) {  // next pass's loads in flight during this pass's math
+            const float* src = h + (size_t)(pg + 32) * C + c0;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) vn[q] = *reinterpret_cast<const float4*>(src + 4 * q);
+        }
+        float acc[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t] = 0.f;
+#pragma unroll 1
+        for (int q = 0; q < Q; ++q) {
+            float4 vq = v[0];  // register select (a runtime-indexed v[q] would go to scratch)
+#pragma unroll
+            for (int j = 1; j < Q; ++j)
+                if (q == j) vq = v[j];
+            const float xs[4] = {vq.x, vq.y, vq.z, vq.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = c0 + 4 * q + e;
+                const float x = silu_f(fmaf(xs[e], ssc[c], ssh[c]));
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc[t] = fmaf(x, ws[c * 9 + t], acc[t]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            acc[t] += __shfl_xor(acc[t], 1);
+            acc[t] += __shfl_xor(acc[t], 2);
+            acc[t] += __shfl_xor(acc[t], 4);
+        }
+        const int p = pg - b * HW;
+        float* dst = r + (size_t)b * 9 * HW + p;
+        dst[(size_t)sub * HW] = acc[sub];  // lane sub writes tap sub; lane 0 also tap 8
+        if (sub == 0) dst[(size_t)8 * HW] = acc[8];
+        if (pass + 1 < HP8 / 32) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) v[q] = vn[q];
+        }
+    }
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -471,6 +552,15 @@ int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2
     return TCX_OK;
 }
 
+// TCX_PIX8=0 keeps the LDS-tile head kernel (A/B measurements)
+bool first8_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("TCX_PIX8");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // TCX_ATTN_SPLIT=0 keeps the split evaluator's attention on fp32 MFMA (A/B measurements)
 bool attn_split_enabled() {
     static const bool on = [] {
@@ -642,10 +732,19 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     {
         TCX_TRY(gn_tab(net, P, 10, P.P0, C, gn, ns, st));
         TCX_REQUIRE(C % 4 == 0, "head: C %% 4");
-        const size_t shm = ((size_t)HEAD_PX * (C + 4) + 11 * (size_t)C) * sizeof(float);
-        const dim3 grid(cdiv(P.P0, HEAD_PX), Bt);
-        hipLaunchKernelGGL(k_head, grid, dim3(256), shm, st, P.a64, P.P0, C, P.sc(10), P.sh(10), net->out_w, P.r);
-        TCX_TRY(check_launch("k_head"));
+        if (P.P0 % HP8 == 0 && (C == 96 || C == 64 || C == 128 || C == 32) && first8_enabled()) {
+            const dim3 g8(Bt * P.P0 / HP8);
+            if (C == 96) hipLaunchKernelGGL(k_head8<3>, g8, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
+            else if (C == 64) hipLaunchKernelGGL(k_head8<2>, g8, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
+            else if (C == 128) hipLaunchKernelGGL(k_head8<4>, g8, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
+            else hipLaunchKernelGGL(k_head8<1>, g8, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
+            TCX_TRY(check_launch("k_head8"));
+        } else {
+            const size_t shm = ((size_t)HEAD_PX * (C + 4) + 11 * (size_t)C) * sizeof(float);
+            const dim3 grid(cdiv(P.P0, HEAD_PX), Bt);
+            hipLaunchKernelGGL(k_head, grid, dim3(256), shm, st, P.a64, P.P0, C, P.sc(10), P.sh(10), net->out_w, P.r);
+            TCX_TRY(check_launch("k_head"));
+        }
     }
     return TCX_OK;
 }
