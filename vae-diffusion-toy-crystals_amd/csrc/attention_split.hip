@@ -34,7 +34,6 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     constexpr int DP = DT * 32;
     constexpr int KSB = D * 4 + 16;    // bytes per staged key row (h2) + 16 B pad
     constexpr int VSW = KT / 2 + 4;    // dwords per V^T row (two f16 slots each) + 16 B pad
-    constexpr float PSC = 1024.f;
     __shared__ __attribute__((aligned(16))) char Ks[KT * KSB];
     __shared__ __attribute__((aligned(16))) unsigned Vh[DP * VSW];
     __shared__ __attribute__((aligned(16))) unsigned Vl[DP * VSW];
@@ -45,6 +44,7 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     const int lane = tid & 63, w = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
     const int q = blockIdx.x * 256 + w * 32 + li;
+    const float scale2 = scale * 1.4426950408889634f;  // log2(e) / sqrt(D)
     h8 qh[DS], ql[DS];
     {
         const char* qr = base + (size_t)q * rs + (size_t)h * D * 4;
@@ -117,7 +117,10 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
             for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sacc[n][r]);
         mt = fmaxf(mt, __shfl_xor(mt, 32));
         const float mn = fmaxf(m, mt);
-        const float alpha = expf((m - mn) * scale);  // 0 on the first tile (m = -inf)
+        // exponentials as hardware exp2 of pre-scaled logits (v_exp_f32; the VALU of the
+        // softmax, not the MFMA, bounds this loop)
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale2);  // 0 on the first tile (m = -inf)
+        const float mb = fmaf(-mn, scale2, 10.f);  // + 10: p is produced pre-scaled by 2^10
         m = mn;
         l *= alpha;
 #pragma unroll
@@ -132,9 +135,8 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
                 h8 ph, pl;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    const float pv = expf((sacc[n][8 * s + e] - mn) * scale);
-                    lt += pv;
-                    const float v = pv * PSC;
+                    const float v = __builtin_amdgcn_exp2f(fmaf(sacc[n][8 * s + e], scale2, mb));
+                    lt += v;  // l, like the P operand, carries the 2^10 scale
                     const _Float16 hh = (_Float16)v;
                     ph[e] = hh;
                     pl[e] = (_Float16)(v - (float)hh);
@@ -153,7 +155,7 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
         lt += __shfl_xor(lt, 32);
         l += lt;
     }
-    const float inv = 1.f / (l * PSC);
+    const float inv = 1.f / l;
 #pragma unroll
     for (int t = 0; t < DT; ++t)
 #pragma unroll
