@@ -22,6 +22,64 @@ namespace tcx {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+// tile load (global -> registers) and store (registers -> LDS stage, V transposed) of the kernel below
+#define TCX_ATT_LOAD(k0) \
+    do { \
+_Pragma("unroll") \
+        for (int u = 0; u < KI; ++u) {  /* KT * KP = 32 D: a multiple of 512 for every D here */ \
+            const int i = tid + 512 * u; \
+            const int j = i / KP, pc = i - (i / KP) * KP; \
+            kreg[u] = *reinterpret_cast<const f4*>(base + (size_t)(k0 + j) * rs + (size_t)(C + h * D) * 4 + pc * 16); \
+        } \
+_Pragma("unroll") \
+        for (int u = 0; u < VI; ++u) { \
+            const int i = tid + 512 * u; \
+            if (i < (KT / 2) * G) { \
+                const int g = i / (KT / 2), jp = i - g * (KT / 2);  /* key pair (2 jp, 2 jp + 1), dim group g */ \
+                const char* src = base + (size_t)(k0 + 2 * jp) * rs + (size_t)(2 * C + h * D) * 4 + g * 32; \
+                vreg[u][0] = *reinterpret_cast<const u4*>(src); \
+                vreg[u][1] = *reinterpret_cast<const u4*>(src + 16); \
+                vreg[u][2] = *reinterpret_cast<const u4*>(src + rs); \
+                vreg[u][3] = *reinterpret_cast<const u4*>(src + rs + 16); \
+            } \
+        } \
+    } while (0)
+#define TCX_ATT_STORE(st) \
+    do { \
+        char* Ks = Kb(st); \
+        unsigned* Vh = Vhb(st); \
+        unsigned* Vl = Vlb(st); \
+_Pragma("unroll") \
+        for (int u = 0; u < KI; ++u) { \
+            const int i = tid + 512 * u; \
+            const int j = i / KP, pc = i - (i / KP) * KP; \
+            *reinterpret_cast<f4*>(Ks + j * KSB + pc * 16) = kreg[u]; \
+        } \
+_Pragma("unroll") \
+        for (int u = 0; u < VI; ++u) { \
+            const int i = tid + 512 * u; \
+            if (i < (KT / 2) * G) { \
+                const int g = i / (KT / 2), jp = i - g * (KT / 2); \
+                const int j = 2 * jp; \
+                /* slot of key j within its subtile: kk = 16s + 8(e>>2) + 4h + (e&3) -> 16s + 8h + e */ \
+                const int kk = j & 31, rem = kk & 15; \
+                const int slot = (j & ~31) + (kk & 16) + 8 * ((rem >> 2) & 1) + ((rem & 3) | ((rem >> 3) << 2)); \
+                const int col = slot >> 1;  /* j even -> slot even; key j + 1 takes slot + 1 */ \
+                const u4 h0 = vreg[u][0], l0 = vreg[u][1], h1 = vreg[u][2], l1 = vreg[u][3]; \
+_Pragma("unroll") \
+                for (int e = 0; e < 8; ++e) { \
+                    const int sh = 16 * (e & 1); \
+                    const unsigned a = (h0[e >> 1] >> sh) & 0xffffu, c = (h1[e >> 1] >> sh) & 0xffffu; \
+                    const unsigned al = (l0[e >> 1] >> sh) & 0xffffu, cl = (l1[e >> 1] >> sh) & 0xffffu; \
+                    Vh[(g * 8 + e) * VSW + col] = a | (c << 16); \
+                    Vl[(g * 8 + e) * VSW + col] = al | (cl << 16); \
+                } \
+            } \
+        } \
+    } while (0)
 
 template <int D>
 __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict__ qkv, char* __restrict__ out, int N,
@@ -34,9 +92,10 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     constexpr int DP = DT * 32;
     constexpr int KSB = D * 4 + 16;    // bytes per staged key row (h2) + 16 B pad
     constexpr int VSW = KT / 2 + 4;    // dwords per V^T row (two f16 slots each) + 16 B pad
-    __shared__ __attribute__((aligned(16))) char Ks[KT * KSB];
-    __shared__ __attribute__((aligned(16))) unsigned Vh[DP * VSW];
-    __shared__ __attribute__((aligned(16))) unsigned Vl[DP * VSW];
+    // two LDS stages (tile t computed from one while tile t+1, loaded into registers during that
+    // compute, is written to the other): [2][K | V^T hi | V^T lo]
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int STAGE = KT * KSB + 2 * DP * VSW * 4;
     const int b = blockIdx.z, h = blockIdx.y;
     const int tid = threadIdx.x;
     const size_t rs = 12 * (size_t)C;  // bytes per token row of qkv (3C channels, 4 B each)
@@ -54,10 +113,16 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
             ql[s] = *reinterpret_cast<const h8*>(qr + (2 * s + lh) * 32 + 16);
         }
     }
+    auto Kb = [&](int st) { return smem + st * STAGE; };
+    auto Vhb = [&](int st) { return reinterpret_cast<unsigned*>(smem + st * STAGE + KT * KSB); };
+    auto Vlb = [&](int st) { return reinterpret_cast<unsigned*>(smem + st * STAGE + KT * KSB + DP * VSW * 4); };
     if (DP > D) {
         for (int i = tid; i < (DP - D) * VSW; i += 512) {
-            Vh[D * VSW + i] = 0u;
-            Vl[D * VSW + i] = 0u;
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                Vhb(st)[D * VSW + i] = 0u;
+                Vlb(st)[D * VSW + i] = 0u;
+            }
         }
     }
     f32x16 oacc[DT];
@@ -66,36 +131,21 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     float m = -INFINITY, l = 0.f;
     constexpr int KP = D / 4;  // 16-B pieces per K row
     constexpr int G = D / 8;   // 8-dim groups per V row
-    for (int k0 = 0; k0 < N; k0 += KT) {
-        __syncthreads();  // previous tile fully consumed
-        for (int i = tid; i < KT * KP; i += 512) {
-            const int j = i / KP, pc = i - (i / KP) * KP;
-            *reinterpret_cast<float4*>(Ks + j * KSB + pc * 16) =
-                *reinterpret_cast<const float4*>(base + (size_t)(k0 + j) * rs + (size_t)(C + h * D) * 4 + pc * 16);
-        }
-        for (int i = tid; i < (KT / 2) * G; i += 512) {
-            const int g = i / (KT / 2), jp = i - g * (KT / 2);  // key pair (2 jp, 2 jp + 1), dim group g
-            const int j = 2 * jp;
-            const char* src = base + (size_t)(k0 + j) * rs + (size_t)(2 * C + h * D) * 4 + g * 32;
-            const uint4 h0 = *reinterpret_cast<const uint4*>(src), l0 = *reinterpret_cast<const uint4*>(src + 16);
-            const uint4 h1 = *reinterpret_cast<const uint4*>(src + rs);
-            const uint4 l1 = *reinterpret_cast<const uint4*>(src + rs + 16);
-            // slot of key j within its subtile: kk = 16s + 8(e>>2) + 4h + (e&3) -> 16s + 8h + e
-            const int kk = j & 31, rem = kk & 15;
-            const int slot = (j & ~31) + (kk & 16) + 8 * ((rem >> 2) & 1) + ((rem & 3) | ((rem >> 3) << 2));
-            const int col = slot >> 1;  // j even -> slot even; key j + 1 takes slot + 1
-            const unsigned hw0[4] = {h0.x, h0.y, h0.z, h0.w}, hw1[4] = {h1.x, h1.y, h1.z, h1.w};
-            const unsigned lw0[4] = {l0.x, l0.y, l0.z, l0.w}, lw1[4] = {l1.x, l1.y, l1.z, l1.w};
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int sh = 16 * (e & 1);
-                const unsigned a = (hw0[e >> 1] >> sh) & 0xffffu, c = (hw1[e >> 1] >> sh) & 0xffffu;
-                const unsigned al = (lw0[e >> 1] >> sh) & 0xffffu, cl = (lw1[e >> 1] >> sh) & 0xffffu;
-                Vh[(g * 8 + e) * VSW + col] = a | (c << 16);
-                Vl[(g * 8 + e) * VSW + col] = al | (cl << 16);
-            }
-        }
-        __syncthreads();
+    static_assert((KT * KP) % 512 == 0, "K tile pieces must tile the block");
+    constexpr int KI = KT * KP / 512;                // K pieces per thread
+    constexpr int VI = ((KT / 2) * G + 511) / 512;   // V (key pair, dim group) items per thread
+    f4 kreg[KI];        // native vectors: arrays of HIP's float4/uint4 structs stayed in scratch here
+    u4 vreg[VI][4];
+    TCX_ATT_LOAD(0);
+    TCX_ATT_STORE(0);
+    __syncthreads();
+    const int ntile = N / KT;
+    for (int tt = 0; tt < ntile; ++tt) {
+        const int cur = tt & 1;
+        if (tt + 1 < ntile) TCX_ATT_LOAD((tt + 1) * KT);  // in flight during this tile's math
+        const char* Ks = Kb(cur);
+        const unsigned* Vh = Vhb(cur);
+        const unsigned* Vl = Vlb(cur);
         f32x16 sacc[NST];
 #pragma unroll
         for (int n = 0; n < NST; ++n) {
@@ -154,6 +204,8 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
         }
         lt += __shfl_xor(lt, 32);
         l += lt;
+        if (tt + 1 < ntile) TCX_ATT_STORE(cur ^ 1);  // that stage was last read in tile tt - 1
+        __syncthreads();
     }
     const float inv = 1.f / l;
 #pragma unroll
@@ -172,10 +224,24 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
 template <int D>
 int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
     const float scale = (float)(1.0 / std::sqrt((double)D));
-    hipLaunchKernelGGL((k_attention_split<D>), dim3(N / 256, heads, Bt), dim3(512), 0, st, (const char*)qkv,
+    constexpr int DP = (D + 31) / 32 * 32;
+    constexpr size_t shm = 2 * ((size_t)128 * (D * 4 + 16) + 2 * (size_t)DP * (128 / 2 + 4) * 4);
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) {
+            set_error("tcx_attention_split: cannot enable %zu B of dynamic LDS", shm);
+            return TCX_EHIP;
+        }
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_attention_split<D>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
                        (char*)out, N, C, scale);
     return check_launch("tcx_attention_split");
 }
+
+#undef TCX_ATT_LOAD
+#undef TCX_ATT_STORE
 
 }  // namespace
 }  // namespace tcx
