@@ -363,6 +363,28 @@ __global__ __launch_bounds__(256) void k_colsum_small(const float* __restrict__ 
     }
 }
 
+// fold for many splits (a flattened [rows][C] matrix: Bt = 1, nsplit up to 4096): one block per
+// (b, c), 256 threads striding the splits, then a fixed wave-xor + cross-wave fold.  The 32-lane
+// fold above left one lane group per output walking 64 strided partials each (~46 us per bias).
+__global__ __launch_bounds__(256) void k_colsum_fold_wide(const double* __restrict__ part, int nsplit, int C,
+                                                          float* __restrict__ per_b, double* __restrict__ tot_b) {
+    __shared__ double wsum[4];
+    const size_t i = blockIdx.x;  // b * C + c
+    const int b = (int)(i / C), c = (int)(i - (size_t)b * C);
+    const double* pp = part + (size_t)b * nsplit * C + c;
+    double s = 0;
+    for (int sp = threadIdx.x; sp < nsplit; sp += 256) s += pp[(size_t)sp * C];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double t = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        if (per_b) per_b[i] = (float)t;
+        tot_b[i] = t;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_colsum_total(const double* __restrict__ tot_b, int Bt, int C,
                                                       float* __restrict__ total, float beta) {
     const int lane = threadIdx.x & 31;
@@ -995,8 +1017,11 @@ extern "C" int tcx_colsum(const float* x, int Bt, int HW, int C, float* per_batc
         else hipLaunchKernelGGL(k_colsum_part<false>, dim3(nsplit, Bt), dim3(256), shm, st, x, HW, C, nsplit, part);
         TCX_TRY(check_launch("tcx_colsum part"));
         const size_t n = (size_t)Bt * C;
-        hipLaunchKernelGGL(k_colsum_fold, dim3((unsigned)std::min<size_t>((n + 7) / 8, 16384)), dim3(256), 0, st, part,
-                           Bt, nsplit, C, per_batch, tot_b);
+        if (nsplit > 256 && n <= 65535)
+            hipLaunchKernelGGL(k_colsum_fold_wide, dim3((unsigned)n), dim3(256), 0, st, part, nsplit, C, per_batch, tot_b);
+        else
+            hipLaunchKernelGGL(k_colsum_fold, dim3((unsigned)std::min<size_t>((n + 7) / 8, 16384)), dim3(256), 0, st,
+                               part, Bt, nsplit, C, per_batch, tot_b);
         TCX_TRY(check_launch("tcx_colsum fold"));
     }
     if (total) {
