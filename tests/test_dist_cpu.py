@@ -7,7 +7,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from toycrystals_amd.dist import allreduce_grads_, gather_shards, rank_seed, shard_range
+from toycrystals_amd.dist import BucketedGradAllReduce, allreduce_grads_, gather_shards, rank_seed, shard_range
 
 
 @pytest.mark.parametrize("n,world", [(128, 1), (128, 2), (128, 8), (37, 4), (3, 8), (0, 2)])
@@ -70,3 +70,57 @@ def test_gloo_world2_gather_and_grad_average(n):
         assert p.exitcode == 0
     for rank, ok_gather, ok_grad, tmax in res:
         assert ok_gather and ok_grad and tmax == world - 1
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.SiLU(), torch.nn.Linear(64, 64),
+                                    torch.nn.SiLU(), torch.nn.Linear(64, 4))
+        ref = [p.detach().clone() for p in model.parameters()]
+        ar = BucketedGradAllReduce(model.parameters(), bucket_mb=0.0005)  # three buckets
+        assert len(ar.buckets) >= 3, len(ar.buckets)
+        res = []
+        for step in range(2):
+            g = torch.Generator().manual_seed(100 * step + rank)
+            x = torch.randn(8, 16, generator=g)
+            for p in model.parameters():
+                p.grad = None
+            model(x).square().mean().backward()
+            ar.finish()
+            got = [p.grad.clone() for p in model.parameters()]
+            # the same step with the flat post-backward all-reduce
+            for p in model.parameters():
+                p.grad = None
+            ar.remove()
+            model(x).square().mean().backward()
+            allreduce_grads_(list(model.parameters()))
+            want = [p.grad.clone() for p in model.parameters()]
+            ar = BucketedGradAllReduce(model.parameters(), bucket_mb=0.0005)
+            res.append(all(torch.allclose(a, b, atol=1e-7, rtol=1e-6) for a, b in zip(got, want)))
+        unchanged = all(torch.equal(a, b.detach()) for a, b in zip(ref, model.parameters()))
+        q.put((rank, all(res), unchanged))
+    except Exception as e:  # report instead of leaving the parent waiting on the queue
+        q.put((rank, False, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_bucketed_grad_allreduce_matches_flat():
+    """BucketedGradAllReduce (hooks launch each bucket's all-reduce during backward) averages the
+    gradients exactly as the flat post-backward all-reduce does, over two steps."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, unchanged in res:
+        assert ok and unchanged is True, (rank, ok, unchanged)

@@ -19,7 +19,7 @@ from tqdm import tqdm
 
 from toycrystals_amd import functional as TF
 from toycrystals_amd._lib import check, lib, ptr, stream_ptr
-from toycrystals_amd.dist import allreduce_grads_
+from toycrystals_amd.dist import BucketedGradAllReduce
 from toycrystals_amd.disk_data import DeviceBatches, ToyCrystalsDiskDataset
 from toycrystals_amd.models.diffusion_prior import DiffusionPriorFiLM, DiffusionSchedule
 from toycrystals_amd.models.vae import CondVAE
@@ -153,6 +153,8 @@ def main() -> int:
         return 0
     opt = Adam(prior.parameters(), lr=args.lr)
     params = [p for p in prior.parameters() if p.requires_grad]
+    # gradient averaging overlapped with backward (bucketed RCCL all-reduces; no-op on one GPU)
+    grad_ar = BucketedGradAllReduce(params)
     loss_hist = []
     if lead:
         print("starting diffusion training loop.")
@@ -189,7 +191,7 @@ def main() -> int:
                 bucket_n.index_add_(0, q, torch.ones_like(per_s))
             opt.zero_grad(set_to_none=True)
             loss.backward()
-            allreduce_grads_(params)
+            grad_ar.finish()
             opt.step()
             total += loss.detach()
         avg = _common.allreduce_scalar_mean(float(total.item()) / max(nb, 1), world, device)

@@ -21,7 +21,7 @@ import _common  # noqa: F401  (package path)
 import torch
 from tqdm import tqdm
 
-from toycrystals_amd.dist import allreduce_grads_
+from toycrystals_amd.dist import BucketedGradAllReduce
 from toycrystals_amd.disk_data import DeviceBatches, ToyCrystalsDiskDataset
 from toycrystals_amd.models.sde_score_model import CondUNetTiny, VPSDE, diffusion_loss_eps, save_sde_samples
 from toycrystals_amd.optim import Adam, ema_update
@@ -129,6 +129,8 @@ def main() -> int:
         if not os.path.exists(metrics_path):
             open(metrics_path, "w", encoding="utf-8").close()
     params = [p for p in model.parameters() if p.requires_grad]
+    # gradient averaging overlapped with backward (bucketed RCCL all-reduces; no-op on one GPU)
+    grad_ar = BucketedGradAllReduce(params)
     for epoch in range(start_epoch, args.epochs):
         model.train()
         total = torch.zeros((), device=device, dtype=torch.float64)
@@ -138,7 +140,7 @@ def main() -> int:
                                       p_uncond=args.p_uncond, t_power=args.t_power)
             opt.zero_grad(set_to_none=True)
             loss.backward()
-            allreduce_grads_(params)
+            grad_ar.finish()
             opt.step()
             if ema_model is not None:
                 ema_update(ema_model, model, float(args.ema_decay))

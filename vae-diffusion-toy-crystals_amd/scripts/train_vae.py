@@ -16,7 +16,7 @@ import _common  # noqa: F401
 import torch
 
 from toycrystals_amd import functional as TF
-from toycrystals_amd.dist import allreduce_grads_
+from toycrystals_amd.dist import BucketedGradAllReduce
 from toycrystals_amd.data import ToyCrystalsDataset
 from toycrystals_amd.disk_data import DeviceBatches, ToyCrystalsDiskDataset
 from toycrystals_amd.models.vae import CondVAE, VAE
@@ -174,6 +174,8 @@ def main() -> int:
                         cond_drop=args.cond_drop).to(device)
     opt = Adam(model.parameters(), lr=args.lr)
     params = [p for p in model.parameters() if p.requires_grad]
+    # gradient averaging overlapped with backward (bucketed RCCL all-reduces; no-op on one GPU)
+    grad_ar = BucketedGradAllReduce(params)
     loss_hist, recon_hist, kl_hist, klr_hist = [], [], [], []
     if lead:
         print("starting training loop...")
@@ -189,7 +191,7 @@ def main() -> int:
             loss = recon + beta * kl_used
             opt.zero_grad(set_to_none=True)
             loss.backward()
-            allreduce_grads_(params)
+            grad_ar.finish()
             opt.step()
             tot += torch.stack([loss.detach(), recon.detach(), kl_used.detach(), kl_raw.detach()]).double()
         nb = max(len(dl), 1)

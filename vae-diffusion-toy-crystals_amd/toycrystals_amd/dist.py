@@ -76,3 +76,84 @@ def allreduce_grads_(params, group=None) -> None:
         n = g.numel()
         g.copy_(flat[off:off + n].view_as(g))
         off += n
+
+
+class BucketedGradAllReduce:
+    """Gradient averaging overlapped with the backward pass (batch-DP training).
+
+    Parameters are grouped, in reverse registration order (roughly the order backward produces
+    their gradients), into buckets of about `bucket_mb` MB.  A post-accumulate-grad hook per
+    parameter copies the fresh gradient into its bucket's flat buffer; when the last gradient of
+    a bucket has arrived, the bucket's all-reduce is launched asynchronously (RCCL runs it on its
+    own stream, ordered after the producing kernels) while the rest of the backward pass is still
+    being computed.  `finish()` waits for the outstanding buckets, divides by the world size and
+    points every `p.grad` at its slice of the averaged buffer.  Same result as `allreduce_grads_`
+    (one flat bucket after backward); the 412 MB of FiLM-prior gradients no longer serialise
+    behind the backward pass.
+
+    Usage per step: ``opt.zero_grad(set_to_none=True); loss.backward(); ar.finish(); opt.step()``.
+    """
+
+    def __init__(self, params, bucket_mb: float = 25.0, group=None) -> None:
+        self.group = group
+        self.params = [p for p in params if p.requires_grad]
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.buckets = []  # [params], flat buffer, offsets
+        self.where = {}  # id(param) -> (bucket index, offset)
+        cur, cur_bytes = [], 0
+        for p in reversed(self.params):
+            cur.append(p)
+            cur_bytes += p.numel() * p.element_size()
+            if cur_bytes >= bucket_mb * 1e6:
+                self._add_bucket(cur)
+                cur, cur_bytes = [], 0
+        if cur:
+            self._add_bucket(cur)
+        self.pending = [0] * len(self.buckets)
+        self.works = [None] * len(self.buckets)
+        self.hooks = []
+        if self.world > 1:
+            for p in self.params:
+                self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _add_bucket(self, ps) -> None:
+        n = sum(p.numel() for p in ps)
+        flat = torch.empty(n, dtype=ps[0].dtype, device=ps[0].device)
+        off = 0
+        bi = len(self.buckets)
+        for p in ps:
+            self.where[id(p)] = (bi, off)
+            off += p.numel()
+        self.buckets.append((ps, flat))
+
+    def _on_grad(self, p) -> None:
+        bi, off = self.where[id(p)]
+        ps, flat = self.buckets[bi]
+        flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
+        self.pending[bi] += 1
+        if self.pending[bi] == len(ps):
+            self.works[bi] = dist.all_reduce(flat, group=self.group, async_op=True)
+
+    def finish(self) -> None:
+        if self.world <= 1:
+            return
+        for bi, (ps, flat) in enumerate(self.buckets):
+            if self.works[bi] is None:  # a parameter without a gradient this step: zeros in its slot
+                for p in ps:
+                    if p.grad is None:
+                        bj, off = self.where[id(p)]
+                        flat[off:off + p.numel()].zero_()
+                self.works[bi] = dist.all_reduce(flat, group=self.group, async_op=True)
+        for bi, (ps, flat) in enumerate(self.buckets):
+            self.works[bi].wait()
+            flat.div_(self.world)
+            for p in ps:
+                _, off = self.where[id(p)]
+                p.grad = flat[off:off + p.numel()].view_as(p)
+            self.pending[bi] = 0
+            self.works[bi] = None
+
+    def remove(self) -> None:
+        for h in self.hooks:
+            h.remove()
+        self.hooks = []
