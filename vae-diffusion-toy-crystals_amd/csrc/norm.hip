@@ -235,6 +235,84 @@ __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ x,
     h2_flag(ovf, bad);
 }
 
+// h2-output upsample with one 8-channel group per item: a thread reads 2 x 16 B per source tap and
+// writes the group's 16-B hi and 16-B lo records (the quad form above writes 8-B halves).
+typedef float f4v __attribute__((ext_vector_type(4)));
+constexpr int UPG = 2;  // 8-channel groups per thread
+__global__ __launch_bounds__(256) void k_upsample2x_g8(const float* __restrict__ x, char* __restrict__ y, int H, int W,
+                                                       int C, const float* __restrict__ tsc,
+                                                       const float* __restrict__ tsh, unsigned* ovf) {
+    bool bad = false;
+    const int C8 = C / 8;
+    const int oy = blockIdx.x % (2 * H), b = blockIdx.x / (2 * H);
+    float sy = 0.5f * ((float)oy + 0.5f) - 0.5f;
+    sy = sy < 0.f ? 0.f : sy;
+    const int y0 = (int)sy;
+    const int y1 = y0 + (y0 < H - 1 ? 1 : 0);
+    const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
+    const float* r0 = x + ((size_t)b * H + y0) * W * C;
+    const float* r1 = x + ((size_t)b * H + y1) * W * C;
+    const int ng = 2 * W * C8;
+    const int i0 = blockIdx.y * (UPG * 256) + threadIdx.x;
+    f4v a[UPG][2], bq[UPG][2], c[UPG][2], d[UPG][2];
+#pragma unroll
+    for (int k = 0; k < UPG; ++k) {
+        const int i = i0 + 256 * k;
+        if (i < ng) {
+            const int ox = i / C8, g = i - (i / C8) * C8;
+            float sx = 0.5f * ((float)ox + 0.5f) - 0.5f;
+            sx = sx < 0.f ? 0.f : sx;
+            const int x0 = (int)sx, x1 = x0 + (x0 < W - 1 ? 1 : 0);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                a[k][h] = *reinterpret_cast<const f4v*>(r0 + x0 * C + 8 * g + 4 * h);
+                bq[k][h] = *reinterpret_cast<const f4v*>(r0 + x1 * C + 8 * g + 4 * h);
+                c[k][h] = *reinterpret_cast<const f4v*>(r1 + x0 * C + 8 * g + 4 * h);
+                d[k][h] = *reinterpret_cast<const f4v*>(r1 + x1 * C + 8 * g + 4 * h);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < UPG; ++k) {
+        const int i = i0 + 256 * k;
+        if (i < ng) {
+            const int ox = i / C8, g = i - (i / C8) * C8;
+            float sx = 0.5f * ((float)ox + 0.5f) - 0.5f;
+            sx = sx < 0.f ? 0.f : sx;
+            const int x0 = (int)sx;
+            const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
+            uint2 hi[2], lo[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                f4v va = a[k][h], vb = bq[k][h], vc = c[k][h], vd = d[k][h];
+                if (tsc) {  // fused GN+SiLU of the source
+                    const f4v s4 = *reinterpret_cast<const f4v*>(tsc + (size_t)b * C + 8 * g + 4 * h);
+                    const f4v h4 = *reinterpret_cast<const f4v*>(tsh + (size_t)b * C + 8 * g + 4 * h);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        va[e] = silu_f(fmaf(va[e], s4[e], h4[e]));
+                        vb[e] = silu_f(fmaf(vb[e], s4[e], h4[e]));
+                        vc[e] = silu_f(fmaf(vc[e], s4[e], h4[e]));
+                        vd[e] = silu_f(fmaf(vd[e], s4[e], h4[e]));
+                    }
+                }
+                float o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {  // the quad kernel's fmaf order: identical values
+                    o[e] = fmaf(ly1, fmaf(lx1, vd[e], lx0 * vc[e]), ly0 * fmaf(lx1, vb[e], lx0 * va[e]));
+                    bad = bad || h2_bad(o[e]);
+                }
+                split4(make_float4(o[0], o[1], o[2], o[3]), hi[h], lo[h]);
+            }
+            const size_t pix = ((size_t)b * 2 * H + oy) * 2 * W + ox;
+            char* gp = y + pix * C * 4 + 32 * (size_t)g;
+            *reinterpret_cast<uint4*>(gp) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
+            *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo[0].x, lo[0].y, lo[1].x, lo[1].y);
+        }
+    }
+    h2_flag(ovf, bad);
+}
+
 // LayerNorm over rows of width Wd (+ optional FiLM h*(1+gamma)+beta), one wave per row.
 __global__ __launch_bounds__(256) void k_layernorm_film(const float* __restrict__ x, float* __restrict__ y, int M,
                                                         int Wd, const float* __restrict__ lw,
@@ -435,6 +513,16 @@ extern "C" int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, 
     TCX_REQUIRE(x && y && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_upsample2x_h2: bad args");
     TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x_h2: scale/shift pair");
     if ((size_t)Bt * H * W * C == 0) return TCX_OK;
+    static const bool g8 = [] {
+        const char* e = getenv("TCX_UPS8");  // 0: the quad form (A/B)
+        return !(e && e[0] == '0');
+    }();
+    if (g8) {
+        const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 8), UPG * 256));
+        hipLaunchKernelGGL(k_upsample2x_g8, grid, dim3(256), 0, (hipStream_t)stream, x, (char*)y, H, W, C, scale,
+                           shift, ovf);
+        return check_launch("tcx_upsample2x_h2");
+    }
     const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 4), UPK * 256));
     hipLaunchKernelGGL(k_upsample2x<true>, grid, dim3(256), 0, (hipStream_t)stream, x, (float*)y, Bt, H, W, C, scale,
                        shift, ovf);
