@@ -159,6 +159,15 @@ int tcx_attention_split(const void* qkv, void* out, int Bt, int N, int C, int he
 /* Conversions of n elements (n % 8 == 0, channel-fastest tensors with C % 8 == 0). */
 int tcx_f32_to_h2(const float* x, void* y, size_t n, unsigned* ovf, void* stream);
 int tcx_h2_to_f32(const void* x, float* y, size_t n, void* stream);
+/* Power-of-two operand scaling for the split convs of the training path (activations and
+ * gradients, which may sit below the f16 normal range or above its maximum):
+ * tcx_absmax atomically maxes max|x| (as float bits, exact) into *bits (zero it first; several
+ * tensors may share one word); tcx_f32_to_h2_scaled writes h2(x * s) with s = 2^k chosen so that
+ * max|x|*s lies in [2^13, 2^14), and, if comb is non-NULL, *comb = *wscale / s (the factor the
+ * conv epilogue applies: tcx_conv2d_h2's wscale argument). */
+int tcx_absmax(const float* x, size_t n, unsigned* bits, void* stream);
+int tcx_f32_to_h2_scaled(const float* x, void* y, size_t n, const unsigned* absmax_bits,
+                         const float* wscale, float* comb, void* stream);
 
 /* Multi-head self-attention core of SelfAttention2d (sde_score_model.py:150-160):
  * qkv [Bt,N,3C] (1x1-conv output, channel order [q,k,v], head-major inside each),

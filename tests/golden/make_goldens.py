@@ -338,6 +338,32 @@ def _grad_sample(name: str, g: torch.Tensor, k: int = 64) -> dict:
     return out
 
 
+def gen_train_score32(name: str) -> None:
+    """One diffusion_loss_eps backward at base_ch=32 (every conv eligible for the split path of the
+    training convs), draws recorded; gradients as checksums + fixed-index samples."""
+    torch.manual_seed(0)
+    model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=32)
+    perturb_norms(model, 5)
+    ck = sd_checksums(model)
+    sde = ref_sde.VPSDE(0.1, 30.0)
+    g = torch.Generator().manual_seed(29)
+    B = 4
+    x0 = torch.rand(B, 1, 64, 64, generator=g)
+    y_cat, y_cont = cond_inputs(B, null_last=False)
+    torch.manual_seed(200)
+    u = torch.rand((B,))
+    eps = torch.randn((B, 1, 64, 64))
+    drop_u = torch.rand((B,))
+    torch.manual_seed(200)
+    loss = ref_sde.diffusion_loss_eps(model, sde, x0, y_cat, y_cont, p_uncond=0.5, t_power=1.0)
+    loss.backward()
+    gs = {}
+    for k, p in model.named_parameters():
+        gs.update(_grad_sample(k, p.grad))
+    save(name, x0=x0.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), u=u.numpy(), eps=eps.numpy(),
+         drop=drop_u.numpy(), loss=np.float64(loss.item()), p_uncond=np.float64(0.5), base_ch=np.int64(32), **ck, **gs)
+
+
 def gen_train_score(name: str) -> None:
     """diffusion_loss_eps backward (all parameter grads) + two torch.optim.Adam steps + EMA
     (train_sde_score_model.py:217-240) at base_ch=16, draws recorded."""
@@ -489,6 +515,8 @@ def main() -> int:
     if want("prior"):
         gen_prior("prior_w64_b2", 64, 2, store_weights=True)
         gen_prior("prior_w1024_b8", 1024, 8, store_weights=False)
+    if want("train32"):
+        gen_train_score32("train32_b4")
     if want("train"):
         gen_train_score("train16_b3")
         gen_train_vae("train_condvae_b4")

@@ -86,7 +86,13 @@ def _conv_case(C1, C2, Cout, ks, stride, pad, circular, H, B=2, resid=False, see
     (32, 0, 64, 4, 2, 1, False, 8),     # VAE enc conv
     (12, 0, 20, 3, 1, 1, True, 12),     # odd channel counts (scalar / unaligned paths)
 ])
-def test_conv2d_fn_vs_torch(C1, C2, Cout, ks, stride, pad, circ, H):
+@pytest.mark.parametrize("split", [False, True], ids=["auto", "split-forced"])
+def test_conv2d_fn_vs_torch(C1, C2, Cout, ks, stride, pad, circ, H, split, monkeypatch):
+    """split-forced: the training convs' f16x3 path (power-of-two scaled h2 operands) wherever the
+    shape allows it, regardless of the size threshold; the same 2e-5 gate as fp32."""
+    if split:
+        from toycrystals_amd import functional as TF
+        monkeypatch.setattr(TF, "_SPLIT_MIN_MACS", 0.0)
     _conv_case(C1, C2, Cout, ks, stride, pad, circ, H)
 
 
@@ -351,6 +357,34 @@ def test_score_training_step_vs_reference(golden):
             got = (names if key.startswith("p2/") else enames)[k].detach().cpu().numpy()
             d = np.abs(got - gd[key])
             assert float(d.max()) < 5e-5 and float(d.mean()) < 1e-6, (key, float(d.max()), float(d.mean()))
+
+
+@pytest.mark.parametrize("split", [True, False], ids=["split-convs", "fp32-convs"])
+def test_score_training_step_base32_vs_reference(golden, monkeypatch, split):
+    """diffusion_loss_eps backward at base_ch 32 (every conv but the first eligible for the split
+    training path) against the reference: loss and sampled gradients of every parameter."""
+    from toycrystals_amd import _lib
+    from toycrystals_amd import functional as TF
+    from toycrystals_amd.models.sde_score_model import CondUNetTiny, VPSDE, diffusion_loss_eps
+    monkeypatch.setattr(TF, "_SPLIT_MIN_MACS", 0.0 if split else float("inf"))
+    old = _lib.conv_precision()
+    _lib.set_conv_precision("f16x3")
+    try:
+        gd = golden("train32_b4")
+        torch.manual_seed(0)
+        model = CondUNetTiny(4, 4, 32)
+        _perturb_norms(model, 5)
+        _check_checksums(model, gd)
+        model = model.cuda()
+        draws = (cu(gd["u"]), cu(gd["eps"]), cu(gd["drop"]))
+        loss = diffusion_loss_eps(model, VPSDE(0.1, 30.0), cu(gd["x0"]), cu(gd["y_cat"], torch.int64), cu(gd["y_cont"]),
+                                  p_uncond=float(gd["p_uncond"]), draws=draws)
+        loss.backward()
+        assert abs(float(loss) - float(gd["loss"])) <= 1e-5 * float(gd["loss"])
+        for k, p in model.named_parameters():
+            _cmp_grad_samples(k, p.grad, gd)
+    finally:
+        _lib.set_conv_precision(old)
 
 
 def test_adam_matches_torch_adam():

@@ -430,6 +430,54 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
     h2_flag(ovf, bad);
 }
 
+// |x| max as the bit pattern of a non-negative float (ordered like the value: an atomicMax on the
+// bits is exact and order-independent).  For the power-of-two operand scaling of the training
+// path's split convs.
+__global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, size_t n4, unsigned* __restrict__ bits) {
+    __shared__ float red[4];
+    float m = 0.f;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    auto take = [&](const float4 v) {
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    };
+    for (; i + 3 * stride < n4; i += 4 * stride) {  // four loads in flight per thread
+        const float4 v0 = reinterpret_cast<const float4*>(x)[i];
+        const float4 v1 = reinterpret_cast<const float4*>(x)[i + stride];
+        const float4 v2 = reinterpret_cast<const float4*>(x)[i + 2 * stride];
+        const float4 v3 = reinterpret_cast<const float4*>(x)[i + 3 * stride];
+        take(v0); take(v1); take(v2); take(v3);
+    }
+    for (; i < n4; i += stride) take(reinterpret_cast<const float4*>(x)[i]);
+    for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(bits, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+// the exact power of two s with max|x| * s in [2^13, 2^14) (s = 1 for an all-zero tensor)
+__device__ __forceinline__ float pow2_scale(unsigned bits) {
+    const float m = __uint_as_float(bits);
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+    int e;
+    frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1)
+    return ldexpf(1.f, min(14 - e, 100));
+}
+
+// h2(x * s), s from the absmax bits; comb (optional) = *wscale / s: the conv epilogue's factor that
+// undoes both the weight scale and this operand scale (all exact powers of two).
+__global__ __launch_bounds__(256) void k_f32_to_h2_scaled(const float* __restrict__ x, char* __restrict__ y, size_t n4,
+                                                          const unsigned* __restrict__ bits,
+                                                          const float* __restrict__ wscale, float* __restrict__ comb) {
+    const float s = pow2_scale(*bits);
+    if (comb && blockIdx.x == 0 && threadIdx.x == 0) *comb = *wscale / s;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        float4 v = reinterpret_cast<const float4*>(x)[i];
+        v.x *= s; v.y *= s; v.z *= s; v.w *= s;
+        store4_h2(y, (i >> 1) * 32, (int)(i & 1), v);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_f32_to_h2(const float* __restrict__ x, char* __restrict__ y, size_t n4,
                                                    unsigned* ovf) {
     bool bad = false;
@@ -566,4 +614,23 @@ extern "C" int tcx_layernorm_film(const float* x, float* y, int M, int Wd, const
     hipLaunchKernelGGL(k_layernorm_film, dim3(cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, x, y, M, Wd, ln_w, ln_b,
                        gb, ld_gb, eps);
     return check_launch("tcx_layernorm_film");
+}
+
+extern "C" int tcx_absmax(const float* x, size_t n, unsigned* bits, void* stream) {
+    TCX_REQUIRE(x && bits && n % 4 == 0 && aligned16(x), "tcx_absmax: n %% 4 and 16-B alignment");
+    if (n == 0) return TCX_OK;
+    const int blocks = (int)std::min<size_t>((n / 4 + 1023) / 1024, 2048);
+    hipLaunchKernelGGL(k_absmax, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n / 4, bits);
+    return check_launch("tcx_absmax");
+}
+
+extern "C" int tcx_f32_to_h2_scaled(const float* x, void* y, size_t n, const unsigned* absmax_bits,
+                                    const float* wscale, float* comb, void* stream) {
+    TCX_REQUIRE(x && y && absmax_bits && n % 8 == 0 && aligned16(x) && aligned16(y) && (!comb || wscale),
+                "tcx_f32_to_h2_scaled: bad args");
+    if (n == 0) return TCX_OK;
+    const int blocks = (int)std::min<size_t>((n / 4 + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_f32_to_h2_scaled, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (char*)y, n / 4,
+                       absmax_bits, wscale, comb);
+    return check_launch("tcx_f32_to_h2_scaled");
 }

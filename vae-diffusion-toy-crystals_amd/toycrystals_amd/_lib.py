@@ -83,6 +83,8 @@ _SIGS = {
     "tcx_attention_split": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_f32_to_h2": (c_int, [c_fp, c_fp, c_size, c_fp, c_fp]),
     "tcx_h2_to_f32": (c_int, [c_fp, c_fp, c_size, c_fp]),
+    "tcx_absmax": (c_int, [c_fp, c_size, c_fp, c_fp]),
+    "tcx_f32_to_h2_scaled": (c_int, [c_fp, c_fp, c_size, c_fp, c_fp, c_fp, c_fp]),
     "tcx_unet_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int]),
     "tcx_set_sample_lanes": (c_int, [c_int]),
     "tcx_unet_eval": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_fp, c_fp, c_int, c_int, c_int,

@@ -18,6 +18,7 @@ Reference ops mirrored (file:line in /root/reference):
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -95,12 +96,60 @@ def _pack_conv(w: torch.Tensor):
     return wpk, kpad, cpad
 
 
+# Training convs on the f16x3 split path (csrc/h2.hpp) when the conv precision is f16x3 and the
+# shape allows it (source channels % 32, a concat of equal halves, k*k <= 16): the operand (an
+# activation in the forward, dY in the stride-1 data gradient) is converted to h2 after an exact
+# power-of-two scaling from its max |value| (gradients sit far below the f16 normal range,
+# activations can exceed its maximum), the weight is packed to h2 with its own power-of-two scale,
+# and the conv epilogue applies the product of both inverse scales.  TCX_TRAIN_SPLIT=0 keeps them
+# on fp32 MFMA.  The weight gradient stays fp32.
+_TRAIN_SPLIT = os.environ.get("TCX_TRAIN_SPLIT", "1") != "0"
+
+
+_SPLIT_MIN_MACS = 4e9  # below this the scaling / conversion launches cost more than the MFMA saves
+
+
+def _split_ok(x1, x2, C1, C2, ks, kpad, macs) -> bool:
+    from ._lib import conv_precision
+    return (_TRAIN_SPLIT and conv_precision() == "f16x3" and macs >= _SPLIT_MIN_MACS and C1 % 32 == 0
+            and C2 in (0, C1) and ks * ks <= 16 and kpad == ks * ks * (C1 + C2) and x1.numel() % 8 == 0
+            and max(x1.numel(), 0 if x2 is None else x2.numel()) * 4 < (1 << 31))
+
+
+def _conv_fwd_split(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride, pad, circular, y):
+    L = lib()
+    st = _st(x1)
+    B, H, W, C1 = x1.shape
+    C2 = 0 if x2 is None else x2.shape[3]
+    # one scratch: [absmax bits of x][absmax bits of w][1.0][1/s_w][1/(s_w s_x)], 16 B apart
+    sc = torch.zeros(20, dtype=torch.int32, device=x1.device)
+    sc[8:12].view(torch.float32).fill_(1.0)
+    bx, bw, one, winv, comb = (ptr(sc) + 16 * i for i in range(5))
+    check(L.tcx_absmax(ptr(x1), x1.numel(), bx, st), "tcx_absmax")
+    if x2 is not None:
+        check(L.tcx_absmax(ptr(x2), x2.numel(), bx, st), "tcx_absmax")
+    check(L.tcx_absmax(ptr(wpk), wpk.numel(), bw, st), "tcx_absmax")
+    wh = torch.empty_like(wpk)  # h2 of the packed weight (the layout of tcx_pack_conv_weight_h2)
+    check(L.tcx_f32_to_h2_scaled(ptr(wpk), ptr(wh), wpk.numel(), bw, one, winv, st), "w to h2")
+    x1h = torch.empty_like(x1)
+    check(L.tcx_f32_to_h2_scaled(ptr(x1), ptr(x1h), x1.numel(), bx, winv, comb, st), "to h2")
+    x2h = None
+    if x2 is not None:
+        x2h = torch.empty_like(x2)
+        check(L.tcx_f32_to_h2_scaled(ptr(x2), ptr(x2h), x2.numel(), bx, None, None, st), "to h2")
+    check(L.tcx_conv2d_h2(ptr(x1h), ptr(x2h), B, 0, H, W, C1, C2, ptr(wh), comb, ptr(b), ptr(bias_b), ptr(resid),
+                          ptr(y), 0, Cout, cpad, kpad, ks, stride, pad, circular, 0, None, None, st), "tcx_conv2d_h2")
+    return y
+
+
 def _conv_fwd(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride, pad, circular, out_hw=None):
     B, H, W, C1 = x1.shape
     C2 = 0 if x2 is None else x2.shape[3]
     Ho = (H + 2 * pad - ks) // stride + 1
     Wo = (W + 2 * pad - ks) // stride + 1
     y = _empty((B, Ho, Wo, Cout), x1)
+    if _split_ok(x1, x2, C1, C2, ks, kpad, float(B) * Ho * Wo * Cout * ks * ks * (C1 + C2)):
+        return _conv_fwd_split(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride, pad, circular, y)
     check(lib().tcx_conv2d(ptr(x1), ptr(x2), B, 0, H, W, C1, C2, ptr(wpk), ptr(b), ptr(bias_b), ptr(resid), ptr(y),
                            Cout, cpad, kpad, ks, stride, pad, circular, 0, 0, None, None, None, None, None, _st(x1)),
           "tcx_conv2d")
