@@ -94,9 +94,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--lanes-alt", type=int, default=3,
-                    help="after the timed region, time --steps more passes with this many concurrent sampling "
-                         "lanes (tcx_set_sample_lanes; 0/1 = skip) and report them under 'lanes_alt'")
+    ap.add_argument("--lanes", "--lanes-alt", dest="lanes", type=int, default=3,
+                    help="concurrent sampling lanes of the timed region (tcx_set_sample_lanes, 1-4; images are "
+                         "bit-identical for every value); the roofline pass after it always runs one lane")
     ap.add_argument("--precision", choices=["f16x3", "fp32"], default="f16x3",
                     help="conv arithmetic: f16x3 split MFMA (fp32-grade, default) or fp32 MFMA")
     args = ap.parse_args()
@@ -129,29 +129,49 @@ def main() -> int:
                                                  guidance_scale=args.cfg, t_end=args.t_end,
                                                  seed=1_000_003 * (rank + 1) + i)
 
+    _last_out = [None]
+
+    def timed(fn) -> float:
+        """K passes bracketed by a barrier + synchronize on both sides; max over ranks."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            _last_out[0] = fn(i)
+        torch.cuda.synchronize(device)
+        el = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    L = lib()
+    # The timed region runs the sampler with args.lanes concurrent sampling lanes (tcx_set_sample_lanes:
+    # the batch split into per-stream chains, images bit-identical to one lane) so one lane's
+    # HBM-bound passes overlap another's MFMA-bound convs.
+    prev_lanes = L.tcx_set_sample_lanes(max(1, args.lanes))
     for i in range(args.warmup):
         run(-1 - i)
     torch.cuda.synchronize(device)
+    elapsed = timed(lambda i: run(i))
+    L.tcx_set_sample_lanes(prev_lanes)
 
-    L = lib()
+    # Roofline pass: the same K passes on ONE stream with the conv launches bracketed by HIP events
+    # (with kernels of several streams co-running, a per-launch event duration no longer times a
+    # kernel alone).  Not part of `value`.
+    L.tcx_set_sample_lanes(1)
+    run(-100)
+    torch.cuda.synchronize(device)
     L.tcx_prof_enable(1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    out = None
-    for i in range(args.steps):
-        out = run(i)
-    torch.cuda.synchronize(device)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    el1 = timed(lambda i: run(100 + i))
     ms, n, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
     L.tcx_prof_read(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl))
     L.tcx_prof_enable(0)
+    L.tcx_set_sample_lanes(prev_lanes)
+    out = _last_out[0]
     assert out is not None and bool(torch.isfinite(out).all()) and float(out.min()) >= 0.0 and float(out.max()) <= 1.0
 
     if args.precision == "f16x3":
@@ -183,7 +203,7 @@ def main() -> int:
         "config": {"workload": f"reverse-SDE {args.n_steps} steps, CFG {args.cfg}, t_end {args.t_end}, "
                                f"CondUNetTiny(base_ch={args.base_ch}) {S}x{S}, batch {B}/GPU",
                    "batch_per_gpu": B, "global_batch": world * B, "n_steps": args.n_steps, "cfg": args.cfg,
-                   "image": [1, S, S], "conv_precision": args.precision,
+                   "image": [1, S, S], "conv_precision": args.precision, "sample_lanes": max(1, args.lanes),
                    "parallelism": "replicas" if world == 1 else f"dp{world} (independent shards)"},
         "path_tflops": round(value / world * FWD_PER_IMG * GFLOP_PER_IMG_FWD / 1e3, 3) if S == 64 else None,
         "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": round(peak, 1),
@@ -191,34 +211,13 @@ def main() -> int:
                      "traffic": TRAFFIC_BYTES_PER_CONV_LAUNCH.get(args.precision) if S == 64 else None,
                      "traffic_unit": "HBM bytes per conv launch", "traffic_source": TRAFFIC_SOURCE,
                      "peak_basis": peak_basis,
+                     "measured_on": "one-lane roofline pass (same K sampling passes on one stream, HIP events per conv launch)",
                      "avg_launch_ms": round(conv_avg_ms, 5), "avg_launch_gflop": round(conv_avg_flop / 1e9, 4),
                      "launches": n.value,
-                     "conv_share_of_step": round(ms.value / 1e3 / elapsed, 4)},
+                     "conv_share_of_step": round(ms.value / 1e3 / el1, 4)},
+        "one_lane": {"value": round(images / el1, 4), "unit": "images/s", "ms_per_step": round(el1 / args.steps * 1e3, 3),
+                     "lanes_speedup": round(el1 / elapsed, 4)},
     }
-    if args.lanes_alt > 1:
-        # Concurrent lanes: the batch split into per-stream sampling chains (bit-identical images)
-        # so one lane's HBM-bound passes overlap another's MFMA-bound convs.  Reported beside, not
-        # as, `value`: with kernels of several streams co-running, per-launch event durations no
-        # longer measure a kernel alone, so the roofline above comes from the one-stream region.
-        prev = L.tcx_set_sample_lanes(args.lanes_alt)
-        run(-100)
-        torch.cuda.synchronize(device)
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            out = run(100 + i)
-        torch.cuda.synchronize(device)
-        el2 = time.perf_counter() - t0
-        if world > 1:
-            dist.barrier()
-            t = torch.tensor([el2], device=device, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el2 = float(t.item())
-        L.tcx_set_sample_lanes(prev)
-        result["lanes_alt"] = {"lanes": args.lanes_alt, "value": round(images / el2, 4), "unit": "images/s",
-                               "ms_per_step": round(el2 / args.steps * 1e3, 3), "steps": args.steps,
-                               "speedup_vs_value": round(elapsed / el2, 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model.state_dict(), args.cpu_batch, args.cpu_steps, args.cfg, args.t_end)
     if rank == 0:
