@@ -101,6 +101,11 @@ def fp32_grade(got, fp32, ref):
     (2, 32, 64, 16, 3, 1, False), (2, 64, 128, 16, 4, 2, False),  # zero padding
     # halo-staged 3x3 kernel (conv3h.hip: Cout % 96 == 0, W in {16, 32, 64})
     (2, 64, 96, 32, 3, 1, False), (1, 32, 192, 64, 3, 1, True), (3, 96, 96, 16, 3, 1, False),
+    # halo-staged 4x4/s2 kernel (conv4s2h.hip: Cout % 96 == 0, Cin % 16 == 0, Wo in {16, 32, 64});
+    # the two ds cases above (96 @ 64^2, 192 @ 32^2) also run on it
+    (2, 32, 96, 64, 4, 2, True),    # two 16-channel slices (the fewest the C1 % 32 rule allows)
+    (3, 64, 192, 32, 4, 2, False),  # zero padding, two column blocks
+    (1, 32, 96, 128, 4, 2, True),   # Wo = 64 (the 256^2 config's ds2)
 ])
 def test_conv_h2_vs_oracle(B, Ci, Co, H, ks, stride, circ):
     x = rng.standard_normal((B, Ci, H, H))
@@ -122,6 +127,21 @@ def test_conv_h2_concat_out_h2_gn_stats():
     fp32 = run_conv(x1, w, b, 1, 1, True, x2=x2)
     fp32_grade(got, fp32, ref)
     s = part.sum(axis=1)  # [B][C][2]
+    r = ref.reshape(2, 96, -1)
+    np.testing.assert_allclose(s[..., 0], r.sum(-1), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[..., 1], (r * r).sum(-1), rtol=1e-5, atol=1e-3)
+
+
+def test_conv_h2_ds_halo_out_h2_gn_stats():
+    """The 4x4/s2 halo kernel with h2 output and fused GroupNorm partials (ds1's shape at B = 2)."""
+    x = rng.standard_normal((2, 96, 64, 64)) * 2.0
+    w = rng.standard_normal((96, 96, 4, 4)) / 40
+    b = rng.standard_normal(96)
+    ref = nn_np.conv2d(x, w, b, stride=2, padding=1, mode="circular")
+    got, part = run_conv_h2(x, w, b, 2, 1, True, gn=True, out_h2=True)
+    fp32 = run_conv(x, w, b, 2, 1, True)
+    fp32_grade(got, fp32, ref)
+    s = part.sum(axis=1)
     r = ref.reshape(2, 96, -1)
     np.testing.assert_allclose(s[..., 0], r.sum(-1), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(s[..., 1], (r * r).sum(-1), rtol=1e-5, atol=1e-3)

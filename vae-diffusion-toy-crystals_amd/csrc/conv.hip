@@ -612,6 +612,7 @@ extern "C" int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, i
     p.bytes1 = (unsigned)b1; p.bytes2 = (unsigned)b2; p.bytesw = (unsigned)bw;
     p.wscale = wscale; p.out_h2 = out_h2; p.ovf = ovf;
     if (conv3h_applies(p, cout_pad)) return launch_conv3h(p, cout_pad, (hipStream_t)stream);
+    if (conv4s2h_applies(p, cout_pad)) return launch_conv4s2h(p, cout_pad, (hipStream_t)stream);
     return launch_conv(p, cout_pad, 0, (hipStream_t)stream);
 }
 

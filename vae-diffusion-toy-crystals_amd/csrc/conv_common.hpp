@@ -40,6 +40,9 @@ struct ConvParams {
 // Halo-staged 3x3 kernel (conv3h.hip): applicability test and launcher for tcx_conv2d_h2.
 bool conv3h_applies(const ConvParams& p, int cout_pad);
 int launch_conv3h(ConvParams& p, int cout_pad, hipStream_t st);
+// Halo-staged 4x4 stride-2 kernel (conv4s2h.hip): the U-Net downsamples on the split path.
+bool conv4s2h_applies(const ConvParams& p, int cout_pad);
+int launch_conv4s2h(ConvParams& p, int cout_pad, hipStream_t st);
 
 namespace {
 
