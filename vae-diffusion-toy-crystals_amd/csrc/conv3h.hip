@@ -26,23 +26,26 @@ namespace {
 
 constexpr int HROW = 36;     // floats per staged pixel: 32 (h2 of 32 channels, 128 B) + 16 B pad
 
-// NW waves per workgroup, tile = 32*NW output pixels = whole rows
-__host__ __device__ constexpr int halo_px(int W, int NW) { return (32 * NW / W + 2) * (W + 2); }
-// halo buffers: two at NW = 8 (one workgroup per CU), one at NW = 4 (two workgroups per CU)
-__host__ __device__ constexpr int halo_bufs(int NW) { return NW == 8 ? 2 : 1; }
+// NW waves per workgroup, RT 32-pixel row blocks per wave: tile = 32*NW*RT output pixels = whole rows
+__host__ __device__ constexpr int halo_px(int W, int HB) { return (HB / W + 2) * (W + 2); }
+// halo buffers: two at one workgroup per CU (NW = 8, or RT = 2), one at NW = 4 (two per CU)
+__host__ __device__ constexpr int halo_bufs(int NW, int RT) { return (NW == 8 || RT == 2) ? 2 : 1; }
 
-constexpr size_t conv3h_lds_bytes(int NT, int W, int NW) {
-    return (size_t)(halo_bufs(NW) * halo_px(W, NW) + 2 * 32 * NT) * HROW * sizeof(float);
+constexpr size_t conv3h_lds_bytes(int NT, int W, int NW, int RT) {
+    return (size_t)(halo_bufs(NW, RT) * halo_px(W, 32 * NW * RT) + 2 * 32 * NT) * HROW * sizeof(float);
 }
 
-template <int NT, int W, bool CIRC, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void k_conv3h(ConvParams p) {
-    constexpr int HB = 32 * NW;
+// RT = 2: each wave owns 64 pixels (two 32-row blocks) x 32*NT channels, so every B fragment read
+// from LDS feeds two MFMAs and the weight chunk staged per tap serves 256 pixels (one workgroup
+// of 4 waves per CU, accumulators beyond the 256 arch VGPRs in AGPRs).
+template <int NT, int W, bool CIRC, int NW, int RT = 1>
+__global__ __launch_bounds__(64 * NW, RT == 1 ? 2 : 1) void k_conv3h(ConvParams p) {
+    constexpr int HB = 32 * NW * RT;
     constexpr int NTHR = 64 * NW;
-    constexpr int HBUFS = halo_bufs(NW);
+    constexpr int HBUFS = halo_bufs(NW, RT);
     constexpr int BN = 32 * NT;
     constexpr int W2 = W + 2;
-    constexpr int NPX = halo_px(W, NW);
+    constexpr int NPX = halo_px(W, HB);
     constexpr int HPI = (NPX * 8 + NTHR - 1) / NTHR;  // halo pieces (16 B) per thread
     constexpr int HBUF = NPX * HROW;            // floats per halo buffer
     constexpr int BBUF = BN * HROW;
@@ -91,21 +94,30 @@ __global__ __launch_bounds__(64 * NW, 2) void k_conv3h(ConvParams p) {
             hdst[i] = hp * HROW + (e & 7) * 4;
         }
     }
-    float4 hv[HPI];
-    auto halo_load = [&](int j) {  // input-channel chunk j (uniform)
+    // One halo buffer: the whole next halo waits in registers during a chunk.  Two buffers: the
+    // next halo moves in HG = 3 groups, each loaded after one barrier and stored before the barrier
+    // two taps later, so only one group's registers are live at a time.
+    constexpr int HG = HBUFS == 2 ? (HPI + 2) / 3 : HPI;
+    float4 hv[HG];
+    auto halo_load_g = [&](int j, int g) {  // input-channel chunk j (uniform), group g
         const int ci0 = j * BK;
         const bool s1 = ci0 < p.C1;
         const int cc = (s1 ? ci0 : ci0 - p.C1) * 4;
         const __amdgpu_buffer_rsrc_t rs = s1 ? r1 : r2;
 #pragma unroll
-        for (int i = 0; i < HPI; ++i) hv[i] = bld4(rs, hoff[i], cc);
+        for (int i = 0; i < HG; ++i)
+            if (g * HG + i < HPI) hv[i] = bld4(rs, hoff[g * HG + i], cc);
     };
-    auto halo_store = [&](int buf) {
+    auto halo_store_g = [&](int buf, int g) {
 #pragma unroll
-        for (int i = 0; i < HPI; ++i)
-            if ((i + 1) * NTHR <= NPX * 8 || hdst[i] >= 0)  // only the last piece can fall past the halo
-                *reinterpret_cast<float4*>(&Hs[buf * HBUF + hdst[i]]) = hv[i];
+        for (int i = 0; i < HG; ++i) {
+            const int k = g * HG + i;
+            if (k < HPI && ((k + 1) * NTHR <= NPX * 8 || hdst[k] >= 0))  // only the last piece can fall past the halo
+                *reinterpret_cast<float4*>(&Hs[buf * HBUF + hdst[k]]) = hv[i];
+        }
     };
+    auto halo_load = [&](int j) { halo_load_g(j, 0); };
+    auto halo_store = [&](int buf) { halo_store_g(buf, 0); };
     // ---- weight chunk staging: BN rows x 8 pieces
     constexpr int BPI = (BN * 8 + NTHR - 1) / NTHR;
     float4 bv[BPI];
@@ -131,20 +143,29 @@ __global__ __launch_bounds__(64 * NW, 2) void k_conv3h(ConvParams p) {
     };
 
     // ---- fragments
-    const int mloc = wv * 32 + li;                                 // this lane's A row = tile pixel
-    const int abase = ((mloc / W) * W2 + (mloc % W)) * HROW + lh * 8;  // float index in a halo buffer
-    const int bbase = li * HROW + lh * 8;
-    f32x16 acc[NT];
+    int abase[RT];  // float index in a halo buffer of this lane's A row (tile pixel) per row block
 #pragma unroll
-    for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
-    h8 a_h[2], a_l[2], b_h[2][NT], b_l[2][NT];
+    for (int rt = 0; rt < RT; ++rt) {
+        const int mloc = (wv * RT + rt) * 32 + li;
+        abase[rt] = ((mloc / W) * W2 + (mloc % W)) * HROW + lh * 8;
+    }
+    const int bbase = li * HROW + lh * 8;
+    f32x16 acc[RT][NT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[rt][n] = (f32x16){};
+    h8 a_h[RT][2], a_l[RT][2], b_h[2][NT], b_l[2][NT];
     auto rd_a = [&](int hbuf, int t) {  // tap t: both 16-deep steps
         const int dy = t / 3, dx = t - 3 * (t / 3);
-        const float* A = &Hs[hbuf * HBUF + abase + (dy * W2 + dx) * HROW];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            a_h[s] = __builtin_bit_cast(h8, ld4(A + 16 * s));
-            a_l[s] = __builtin_bit_cast(h8, ld4(A + 16 * s + 4));
+        for (int rt = 0; rt < RT; ++rt) {
+            const float* A = &Hs[hbuf * HBUF + abase[rt] + (dy * W2 + dx) * HROW];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                a_h[rt][s] = __builtin_bit_cast(h8, ld4(A + 16 * s));
+                a_l[rt][s] = __builtin_bit_cast(h8, ld4(A + 16 * s + 4));
+            }
         }
     };
     auto rd_b = [&](int bb) {
@@ -159,19 +180,34 @@ __global__ __launch_bounds__(64 * NW, 2) void k_conv3h(ConvParams p) {
     };
     auto mf = [&](int s) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[s], b_l[s][n], acc[n], 0, 0, 0);
+        for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_l[s], b_h[s][n], acc[n], 0, 0, 0);
+            for (int n = 0; n < NT; ++n)
+                acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[rt][s], b_l[s][n], acc[rt][n], 0, 0, 0);
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[s], b_h[s][n], acc[n], 0, 0, 0);
+            for (int n = 0; n < NT; ++n)
+                acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_l[rt][s], b_h[s][n], acc[rt][n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[rt][s], b_h[s][n], acc[rt][n], 0, 0, 0);
+        }
     };
 
-    // ---- prologue: halo 0 and weight chunk 0 in LDS; halo 1 and weight chunk 1 in flight
-    halo_load(0);
+    // ---- prologue: halo 0 and weight chunk 0 in LDS; halo 1 (one buffer) and weight chunk 1 in flight
     w_load(0);
-    halo_store(0);
-    w_store(0);
-    if (cpt > 1) halo_load(1);
+    if constexpr (HBUFS == 2) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            halo_load_g(0, g);
+            halo_store_g(0, g);
+        }
+        w_store(0);
+    } else {
+        halo_load(0);
+        halo_store(0);
+        w_store(0);
+        if (cpt > 1) halo_load(1);
+    }
     w_load(nchunks > 1 ? 1 : 0);
     __syncthreads();
     rd_a(0, 0);
@@ -188,12 +224,13 @@ __global__ __launch_bounds__(64 * NW, 2) void k_conv3h(ConvParams p) {
             mf(1);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (HBUFS == 2) {
-                // halo j+1 (loaded since tap 4 of chunk j-1) into the other buffer; the next tap's
-                // A fragments come from the same halo (no barrier needed) or, after tap 8, the other
-                if (t == 4 && j + 1 < cpt) halo_store(hb ^ 1);
+                // halo j+1 into the other buffer (free since chunk j-1's last barrier): group g
+                // loaded after the barrier of tap 2g, stored before the barrier of tap 2g+2; the
+                // next tap's A fragments come from the same halo or, after tap 8, the other
+                if ((t == 2 || t == 4 || t == 6) && j + 1 < cpt) halo_store_g(hb ^ 1, t / 2 - 1);
                 w_store(cur ^ 1);  // weight chunk c + 1
                 __syncthreads();
-                if (t == 4 && j + 2 < cpt) halo_load(j + 2);
+                if ((t == 0 || t == 2 || t == 4) && j + 1 < cpt) halo_load_g(j + 1, t / 2);
                 if (c + 2 < nchunks) w_load(c + 2);
                 if (t < 8) rd_a(hb, t + 1);
                 else rd_a(hb ^ 1, 0);
@@ -217,7 +254,20 @@ __global__ __launch_bounds__(64 * NW, 2) void k_conv3h(ConvParams p) {
         }
     }
     __syncthreads();  // the halo buffers become the epilogue's reduction scratch
-    conv_epilogue<NT, true, NW>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
+    if constexpr (RT == 1) {
+        conv_epilogue<NT, true, NW>(p, acc[0], m0, n0, wv, tid, reinterpret_cast<double*>(sm));
+    } else {
+        // two explicit calls, not a loop: a rolled loop over the (large) inlined epilogue would index
+        // acc dynamically and keep the whole accumulator array in scratch, stored after every tap
+        double* red = reinterpret_cast<double*>(sm);
+        static_assert(RT == 2, "RT is 1 or 2");
+        conv_epi_store<NT, true, RT * NW>(p, acc[0], m0, n0, RT * wv, lane, red);
+        conv_epi_store<NT, true, RT * NW>(p, acc[1], m0, n0, RT * wv + 1, lane, red);
+        if (p.gn) {
+            __syncthreads();
+            conv_epi_gn<NT, RT * NW>(p, m0, n0, tid, NTHR, red);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -414,8 +464,8 @@ __global__ __launch_bounds__(256, 1) void k_conv3w(ConvParams p) {
 
     __syncthreads();  // halo buffers -> epilogue scratch
     double* red = reinterpret_cast<double*>(sm);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) conv_epi_store<NT, true, 2 * NW>(p, acc[rt], m0, n0, 2 * wv + rt, lane, red);
+    conv_epi_store<NT, true, 2 * NW>(p, acc[0], m0, n0, 2 * wv, lane, red);
+    conv_epi_store<NT, true, 2 * NW>(p, acc[1], m0, n0, 2 * wv + 1, lane, red);
     if (p.gn) {
         __syncthreads();
         conv_epi_gn<NT, 2 * NW>(p, m0, n0, tid, NTHR, red);
@@ -440,11 +490,11 @@ int launch3w(const ConvParams& p, hipStream_t st) {
     return check_launch("tcx_conv2d_h2(halo, wide)");
 }
 
-template <int NT, int W, int NW>
+template <int NT, int W, int NW, int RT = 1>
 int launch3h_w(const ConvParams& p, hipStream_t st) {
-    constexpr size_t shm = conv3h_lds_bytes(NT, W, NW);
+    constexpr size_t shm = conv3h_lds_bytes(NT, W, NW, RT);
     static bool attr[2] = {false, false};
-    auto kc = p.circular ? &k_conv3h<NT, W, true, NW> : &k_conv3h<NT, W, false, NW>;
+    auto kc = p.circular ? &k_conv3h<NT, W, true, NW, RT> : &k_conv3h<NT, W, false, NW, RT>;
     if (!attr[p.circular ? 1 : 0]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)shm) != hipSuccess) {
@@ -453,7 +503,7 @@ int launch3h_w(const ConvParams& p, hipStream_t st) {
         }
         attr[p.circular ? 1 : 0] = true;
     }
-    const int grid = (p.M / (32 * NW)) * p.n_nblk;
+    const int grid = (p.M / (32 * NW * RT)) * p.n_nblk;
     hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * NW), shm, st, p);
     return check_launch("tcx_conv2d_h2(halo)");
 }
@@ -468,6 +518,16 @@ int halo_nw() {
     }();
     return nw;
 }
+// TCX_HALO_RT=2 with TCX_HALO_NW=4: k_conv3h with two 32-pixel row blocks per wave (256-pixel tiles)
+int halo_rt() {
+    static const int rt = [] {
+        const char* e = getenv("TCX_HALO_RT");
+        return (e && atoi(e) == 2 && halo_nw() == 4) ? 2 : 1;
+    }();
+    return rt;
+}
+// output pixels per workgroup tile of the selected variant
+int halo_tile() { return halo_nw() ? 32 * halo_nw() * halo_rt() : 256; }
 
 }  // namespace
 
@@ -475,8 +535,7 @@ int halo_nw() {
 bool conv3h_applies(const ConvParams& p, int cout_pad) {
     static const bool off = getenv("TCX_NO_HALO") != nullptr;
     return !off && p.ks == 3 && p.stride == 1 && p.pad_y == 1 && p.pad_x == 1 && p.Hi == p.H && p.Wi == p.W &&
-           (p.W == 16 || p.W == 32 || p.W == 64) && p.H % ((halo_nw() ? 32 * halo_nw() : 256) / p.W) == 0 &&
-           p.HoWo % (halo_nw() ? 32 * halo_nw() : 256) == 0 &&
+           (p.W == 16 || p.W == 32 || p.W == 64) && p.H % (halo_tile() / p.W) == 0 && p.HoWo % halo_tile() == 0 &&
            cout_pad % 96 == 0 && p.Cin % BK == 0 && p.C1 % BK == 0 && (p.C2 == 0 || p.C2 == p.C1) &&
            p.kpad == 9 * p.Cin && p.osy == 1 && p.osx == 1;
 }
@@ -494,6 +553,10 @@ int launch_conv3h(ConvParams& p, int cout_pad, hipStream_t st) {
         if (p.W == 64) rc = launch3h_w<3, 64, 8>(p, st);
         else if (p.W == 32) rc = launch3h_w<3, 32, 8>(p, st);
         else rc = launch3h_w<3, 16, 8>(p, st);
+    } else if (halo_rt() == 2) {
+        if (p.W == 64) rc = launch3h_w<3, 64, 4, 2>(p, st);
+        else if (p.W == 32) rc = launch3h_w<3, 32, 4, 2>(p, st);
+        else rc = launch3h_w<3, 16, 4, 2>(p, st);
     } else {
         if (p.W == 64) rc = launch3h_w<3, 64, 4>(p, st);
         else if (p.W == 32) rc = launch3h_w<3, 32, 4>(p, st);
