@@ -175,7 +175,8 @@ def main() -> int:
     assert out is not None and bool(torch.isfinite(out).all()) and float(out.min()) >= 0.0 and float(out.max()) <= 1.0
 
     if args.precision == "f16x3":
-        kname = "k_conv<SPL> (f16x3 split implicit-GEMM conv, 3x v_mfma_f32_32x32x16_f16 per fp32 MAC)"
+        kname = ("split-path convs: k_conv3p (3x3 halo), k_conv4s2h (4x4/s2 halo), k_conv<SPL> (1x1) — "
+                 "f16x3, 3x v_mfma_f32_32x32x16_f16 per fp32 MAC; all conv launches of the pass")
         peak = F16_PEAK_TFLOPS / SPLIT_PRODUCTS
         peak_basis = "2500 TFLOP/s dense f16 MFMA / 3 products per fp32 MAC; achieved in fp32-equivalent FLOPs"
     else:
