@@ -285,7 +285,7 @@ constexpr size_t conv3p_lds_bytes(int NT, int W) {
     return (size_t)(halo_px(W, 128) + 3 * 32 * NT) * HROW * sizeof(float);
 }
 
-template <int NT, int W, bool CIRC>
+template <int NT, int W, bool CIRC, bool PRIO = false>
 __global__ __launch_bounds__(256, 2) void k_conv3p(ConvParams p) {
     constexpr int NW = 4, HB = 128, NTHR = 256;
     constexpr int BN = 32 * NT;
@@ -426,11 +426,15 @@ __global__ __launch_bounds__(256, 2) void k_conv3p(ConvParams p) {
             // MFMAs (lgkmcnt(0) before each), which serialises reads and MFMAs again
             rd(1, t, wb);
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
             mf(0);
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
             if (t < 8) rd(0, t + 1, wn);
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
             mf(1);
+            if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
             w_store(wn2);  // chunk c+2 (its buffer held chunk c-1, read before the last barrier)
             __syncthreads();
@@ -675,7 +679,13 @@ template <int NT, int W>
 int launch3p(const ConvParams& p, hipStream_t st) {
     constexpr size_t shm = conv3p_lds_bytes(NT, W);
     static bool attr[2] = {false, false};
-    auto kc = p.circular ? &k_conv3p<NT, W, true> : &k_conv3p<NT, W, false>;
+    // TCX_HALO_PRIO=1: s_setprio(1) around each MFMA cluster (A/B knob)
+    static const bool prio = [] {
+        const char* e = getenv("TCX_HALO_PRIO");
+        return e && atoi(e) == 1;
+    }();
+    auto kc = p.circular ? (prio ? &k_conv3p<NT, W, true, true> : &k_conv3p<NT, W, true, false>)
+                         : &k_conv3p<NT, W, false, false>;
     if (!attr[p.circular ? 1 : 0]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)shm) != hipSuccess) {
