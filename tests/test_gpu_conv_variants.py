@@ -39,6 +39,7 @@ assert worst <= 2e-5, worst
 
 @pytest.mark.parametrize("env", [
     {"TCX_HALO_PIPE": "0"},                       # unpipelined k_conv3h (4 waves, two workgroups per CU)
+    {"TCX_HALO_PNW": "8"},                        # k_conv3p with 8 waves, 256-pixel tiles
     {"TCX_HALO_NW": "8"},                         # k_conv3h, 8 waves, grouped halo staging
     {"TCX_HALO_NW": "4", "TCX_HALO_RT": "2"},     # k_conv3h, 64 pixels per wave
     {"TCX_HALO_NW": "0"},                         # k_conv3w wide waves

@@ -281,13 +281,15 @@ __global__ __launch_bounds__(64 * NW, RT == 1 ? 2 : 1) void k_conv3h(ConvParams 
 // W = 64).  At the last tap of an input-channel chunk the next halo is stored first (one halo
 // buffer), so that tap's step-0 read of the next chunk happens after the extra barrier.
 // ---------------------------------------------------------------------------------------------
-constexpr size_t conv3p_lds_bytes(int NT, int W) {
-    return (size_t)(halo_px(W, 128) + 3 * 32 * NT) * HROW * sizeof(float);
+constexpr size_t conv3p_lds_bytes(int NT, int W, int NW = 4) {
+    return (size_t)(halo_px(W, 32 * NW) + 3 * 32 * NT) * HROW * sizeof(float);
 }
 
-template <int NT, int W, bool CIRC, bool PRIO = false>
-__global__ __launch_bounds__(256, 2) void k_conv3p(ConvParams p) {
-    constexpr int NW = 4, HB = 128, NTHR = 256;
+// NW = 4 (default: 128-pixel tiles, two workgroups per CU) or 8 (TCX_HALO_PNW=8: 256-pixel tiles,
+// one workgroup per CU, half the weight staging per FLOP)
+template <int NT, int W, bool CIRC, bool PRIO = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3p(ConvParams p) {
+    constexpr int HB = 32 * NW, NTHR = 64 * NW;
     constexpr int BN = 32 * NT;
     constexpr int W2 = W + 2;
     constexpr int NPX = halo_px(W, HB);
@@ -675,6 +677,15 @@ int launch3w(const ConvParams& p, hipStream_t st) {
     return check_launch("tcx_conv2d_h2(halo, wide)");
 }
 
+// TCX_HALO_PNW=8: k_conv3p with 8 waves and 256-pixel tiles
+bool pnw8() {
+    static const bool on = [] {
+        const char* e = getenv("TCX_HALO_PNW");
+        return e && atoi(e) == 8;
+    }();
+    return on;
+}
+
 template <int NT, int W>
 int launch3p(const ConvParams& p, hipStream_t st) {
     constexpr size_t shm = conv3p_lds_bytes(NT, W);
@@ -686,6 +697,21 @@ int launch3p(const ConvParams& p, hipStream_t st) {
     }();
     auto kc = p.circular ? (prio ? &k_conv3p<NT, W, true, true> : &k_conv3p<NT, W, true, false>)
                          : &k_conv3p<NT, W, false, false>;
+    if (pnw8()) {
+        constexpr size_t shm8 = conv3p_lds_bytes(NT, W, 8);
+        auto k8 = p.circular ? &k_conv3p<NT, W, true, false, 8> : &k_conv3p<NT, W, false, false, 8>;
+        static bool attr8[2] = {false, false};
+        if (!attr8[p.circular ? 1 : 0]) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(k8), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)shm8) != hipSuccess) {
+                set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", shm8);
+                return TCX_EHIP;
+            }
+            attr8[p.circular ? 1 : 0] = true;
+        }
+        hipLaunchKernelGGL(k8, dim3((p.M / 256) * p.n_nblk), dim3(512), shm8, st, p);
+        return check_launch("tcx_conv2d_h2(halo, pipelined, 8 waves)");
+    }
     if (!attr[p.circular ? 1 : 0]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)shm) != hipSuccess) {
@@ -745,7 +771,7 @@ bool halo_pipe() {
     return on;
 }
 // output pixels per workgroup tile of the selected variant
-int halo_tile() { return halo_nw() ? 32 * halo_nw() * halo_rt() : 256; }
+int halo_tile() { return halo_nw() ? 32 * halo_nw() * halo_rt() * (halo_pipe() && pnw8() ? 2 : 1) : 256; }
 
 }  // namespace
 
