@@ -20,8 +20,10 @@ Also reports, on one JSON line:
                  the peak of the MFMA it runs on — f16x3 split path (default): the 2.5 PFLOP/s dense
                  f16 MFMA peak / 3 MFMA products per fp32 multiply-add = 833.3; fp32 path
                  (--precision fp32): the 157.3 TFLOP/s fp32 MFMA peak (MI355X_MICROARCH.md).
-  cpu_baseline — the numpy oracle (a port of the reference's arithmetic) timed on this host's cores on a
-                 bounded sample (rank 0, N=1 only) and extrapolated per image to the 602-forward run.
+  fp32_path    — the same sampler with the fp32-MFMA convs (one lane), value + roofline, beside the f16x3 line.
+  cpu_baseline — the reference's CPU arithmetic (oracle/score_model_torch.py: torch CPU ops) on the same
+                 inputs at B=128, timed at 2 and 4 sampler steps on this host's cores (rank 0, N=1 only), the
+                 per-forward cost fitted and extrapolated to the 602-forward run.
 """
 from __future__ import annotations
 
@@ -53,30 +55,50 @@ TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 595.7e6}
 TRAFFIC_SOURCE = "rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE, profiles/r01_x_pmc_traffic.txt"
 
 
-def cpu_baseline(state_dict, B: int, n_steps: int, cfg: float, t_end: float) -> dict:
-    """Time the numpy oracle on a bounded sample and extrapolate to images/sec."""
-    import numpy as np
-    from oracle.score_model import ScoreUNet, VPSDE, sample_reverse_sde_euler_maruyama
+def _cpu_model() -> str:
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"] or [1])
-    except Exception:  # pragma: no cover
-        threads = os.cpu_count() or 1
-    o = ScoreUNet({k: v.detach().cpu().numpy() for k, v in state_dict.items()})
-    rng = np.random.default_rng(1234)
-    noise = rng.standard_normal((n_steps + 1, B, 1, 64, 64)).astype(np.float32)
-    y_cat = np.arange(B) % 4
-    y_cont = np.zeros((B, 4), np.float32)
-    y_cont[:, 1] = np.linspace(0, math.pi / 3, B)
-    t0 = time.perf_counter()
-    sample_reverse_sde_euler_maruyama(o, VPSDE(0.1, 30.0), y_cat, y_cont, noise, n_steps, cfg, t_end)
-    dt = time.perf_counter() - t0
-    n_fwd = 2 * n_steps + 2
-    per_img_fwd = dt / (n_fwd * B)
-    return {"value": 1.0 / (FWD_PER_IMG * per_img_fwd), "unit": "images/s", "cores": int(threads), "kind": "port",
-            "sample": f"numpy oracle, B={B}, {n_steps} reverse-SDE steps + final projection with CFG "
-                      f"({n_fwd} U-Net forwards of B={B}) in {dt:.1f}s, extrapolated per image to "
-                      f"{FWD_PER_IMG} forwards; {threads} BLAS threads"}
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:  # pragma: no cover
+        pass
+    return "unknown"
+
+
+def cpu_baseline(state_dict, B: int, steps_a: int, steps_b: int, cfg: float, t_end: float) -> dict:
+    """the reference's CPU arithmetic (oracle/score_model_torch.py: torch CPU ops,
+    the ATen kernels the reference's modules call) on the same synthetic inputs, B images, timed
+    at `steps_a` and `steps_b` reverse-SDE steps (+ the final projection); the per-forward cost is
+    fitted from the difference and extrapolated to the 602 forwards of the 300-step run."""
+    from oracle.score_model_torch import TorchScoreUNet, sample_reverse_sde
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    o = TorchScoreUNet({k: v.detach().cpu() for k, v in state_dict.items()})
+    y_cat = torch.arange(B) % 4
+    y_cont = torch.zeros(B, 4)
+    y_cont[:, 1] = torch.linspace(0, math.pi / 3, B)
+
+    def run(n):
+        gen = torch.Generator().manual_seed(1234)
+        t0 = time.perf_counter()
+        out = sample_reverse_sde(o, 0.1, 30.0, y_cat, y_cont, (B, 1, 64, 64), n, cfg, t_end, generator=gen)
+        assert bool(torch.isfinite(out).all())
+        return time.perf_counter() - t0
+
+    o(torch.zeros(2, 1, 64, 64), torch.full((2,), 0.5), y_cat[:2], y_cont[:2])  # warm the CPU kernels (untimed)
+    ta, tb = run(steps_a), run(steps_b)
+    torch.set_num_threads(prev)
+    fa, fb = 2 * steps_a + 2, 2 * steps_b + 2  # U-Net calls of batch B (CFG: 2 per step, 2 for the projection)
+    per_fwd = (tb - ta) / (fb - fa)
+    fixed = max(0.0, ta - per_fwd * fa)
+    sec_per_pass = fixed + per_fwd * FWD_PER_IMG  # the 300-step run = 602 U-Net calls of batch B
+    return {"value": round(B / sec_per_pass, 5), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu": _cpu_model(),
+            "sample": f"torch-CPU restatement of the reference arithmetic (oracle/score_model_torch.py), "
+                      f"B={B}, reverse SDE {steps_a} and {steps_b} steps + projection with CFG {cfg} "
+                      f"({fa} and {fb} U-Net calls of B={B}) in {ta:.1f}s / {tb:.1f}s; fit {per_fwd:.2f}s per call, "
+                      f"extrapolated to the {FWD_PER_IMG} calls of the 300-step run; torch threads {threads}"}
 
 
 def main() -> int:
@@ -92,13 +114,17 @@ def main() -> int:
     ap.add_argument("--img-size", type=int, default=64,
                     help="64 (the metric's config 2); 256 with --batch 64 = config 5's per-GPU share (512 over 8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=32)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-batch", type=int, default=128)
     ap.add_argument("--lanes", "--lanes-alt", dest="lanes", type=int, default=3,
                     help="concurrent sampling lanes of the timed region (tcx_set_sample_lanes, 1-4; images are "
                          "bit-identical for every value); the roofline pass after it always runs one lane")
     ap.add_argument("--precision", choices=["f16x3", "fp32"], default="f16x3",
                     help="conv arithmetic: f16x3 split MFMA (fp32-grade, default) or fp32 MFMA")
+    ap.add_argument("--fp32-passes", type=int, default=1,
+                    help="with the f16x3 headline: timed one-lane passes of the fp32-MFMA path reported beside it "
+                         "(`fp32_path`; 0 skips)")
+    ap.add_argument("--cpu-steps-a", type=int, default=2)
+    ap.add_argument("--cpu-steps-b", type=int, default=4)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -174,6 +200,32 @@ def main() -> int:
     out = _last_out[0]
     assert out is not None and bool(torch.isfinite(out).all()) and float(out.min()) >= 0.0 and float(out.max()) <= 1.0
 
+    # The fp32-MFMA path beside the f16x3 headline (same sampler, one lane, conv launches timed by
+    # HIP events as above): what the f16x3 split path buys at equal (fp32-grade) parity gates.
+    fp32_path = None
+    if args.precision == "f16x3" and args.fp32_passes > 0:
+        set_conv_precision("fp32")
+        L.tcx_set_sample_lanes(1)
+        run(-200)
+        torch.cuda.synchronize(device)
+        steps_saved = args.steps
+        args.steps = args.fp32_passes
+        L.tcx_prof_enable(1)
+        el32 = timed(lambda i: run(200 + i))
+        ms32, n32, fl32 = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
+        L.tcx_prof_read(ctypes.byref(ms32), ctypes.byref(n32), ctypes.byref(fl32))
+        L.tcx_prof_enable(0)
+        L.tcx_set_sample_lanes(prev_lanes)
+        set_conv_precision(args.precision)
+        ach32 = (fl32.value / max(1, n32.value)) / ((ms32.value / max(1, n32.value)) * 1e-3) / 1e12 if n32.value else 0.0
+        fp32_path = {"value": round(world * B * args.fp32_passes / el32, 4), "unit": "images/s", "lanes": 1,
+                     "passes": args.fp32_passes, "ms_per_step": round(el32 / args.fp32_passes * 1e3, 3),
+                     "roofline": {"bound": "mfma", "kernel": "k_conv (fp32-MFMA implicit GEMM, v_mfma_f32_32x32x2_f32)",
+                                  "achieved": round(ach32, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": round(ach32 / FP32_PEAK_TFLOPS, 4),
+                                  "avg_launch_ms": round(ms32.value / max(1, n32.value), 5)}}
+        args.steps = steps_saved
+
     if args.precision == "f16x3":
         kname = ("split-path convs: k_conv3p (3x3 halo), k_conv4s2h (4x4/s2 halo), k_conv<SPL> (1x1) — "
                  "f16x3, 3x v_mfma_f32_32x32x16_f16 per fp32 MAC; all conv launches of the pass")
@@ -219,8 +271,11 @@ def main() -> int:
         "one_lane": {"value": round(images / el1, 4), "unit": "images/s", "ms_per_step": round(el1 / args.steps * 1e3, 3),
                      "lanes_speedup": round(el1 / elapsed, 4)},
     }
+    if fp32_path is not None:
+        result["fp32_path"] = fp32_path
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(model.state_dict(), args.cpu_batch, args.cpu_steps, args.cfg, args.t_end)
+        result["cpu_baseline"] = cpu_baseline(model.state_dict(), args.cpu_batch, args.cpu_steps_a, args.cpu_steps_b,
+                                              args.cfg, args.t_end)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

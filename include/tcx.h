@@ -231,7 +231,8 @@ int tcx_set_sample_lanes(int lanes);
  *         1 reverse-SDE Euler-Maruyama update of x in place with noise z (sde_score_model.py:545-559);
  *         2 final projection x0 = clamp(((x - s*eps)/max(a,1e-6) + 1)/2) into eps_out (:562-569);
  *         3 Heun stage 1: drift d (-> eps_out) and x_e = x + d*dt (-> x2)   (:490-492, :426-449);
- *         4 Heun stage 2: x += 0.5*(d + d(x_e))*dt, d read from eps_out, x_e = x2 (:493).
+ *         4 Heun stage 2: x += 0.5*(d + d(x_e))*dt, d read from eps_out, x_e = x2 (:493);
+ *         5 as 2 but stops at x0_hat = (x - s*eps)/max(a,1e-6) (:566): no (x0+1)/2 map, no clamp.
  *   scal: device pointer to the current row of the per-step table.
  *   z: noise [B,H,W] for mode 1 (host-injected, parity mode) or NULL to draw it in-kernel from
  *   Philox4x32-10 keyed by (seed, step) (fast mode).  */
@@ -254,6 +255,19 @@ int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const fl
 int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
                    int H, int W, int n_steps, float guidance, const float* scal_table, void* ws,
                    size_t ws_bytes, void* stream);
+
+/* The two samplers with output flags.  TCX_SAMPLE_X0_HAT: x receives the unclamped projection
+ * x0_hat = (x - sigma*eps)/max(alpha,1e-6) (sde_score_model.py:500,566) instead of the clamped
+ * [0,1] image — the reference's last two lines (:503-504, :568-569) are then
+ * clamp((x0_hat + 1)/2, 0, 1).  flags = 0 is tcx_sde_sample / tcx_ode_sample. */
+#define TCX_SAMPLE_X0_HAT 1
+int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont,
+                      int B, int H, int W, int n_steps, float guidance, const float* scal_table,
+                      const float* noise, uint64_t seed, int flags, void* ws, size_t ws_bytes,
+                      void* stream);
+int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont,
+                      int B, int H, int W, int n_steps, float guidance, const float* scal_table,
+                      int flags, void* ws, size_t ws_bytes, void* stream);
 
 /* Standard normal draws from Philox4x32-10 (+ Box-Muller), keyed (seed, stream id). */
 int tcx_randn(float* out, size_t n, uint64_t seed, uint64_t stream_id, void* stream);

@@ -505,8 +505,15 @@ def main() -> int:
         np.savez_compressed(os.path.join(HERE, "trained32_state.npz"),
                             **{k: v.numpy() for k, v in sd.items()})
         print("  wrote trained32_state.npz")
-        gen_sampler("sde32_trained_300", "sde", 32, 4, 300, 1.5, 0.005, state_dict=sd, store_noise=False)
+        # (its 300-step reverse SDE saturated every pixel; replaced by sde96_trained_300 below)
         gen_sampler("ode32_trained_20", "ode", 32, 4, 20, 1.5, 0.005, state_dict=sd, store_noise=False)
+    if want("trained96"):
+        # the EMA weights of a 40-epoch run of the README recipe (README.md:104) through this repo's
+        # mirror train_sde_score_model.py on the MI355X (tools/gpu/recipe40.sh; loss curve in
+        # profiles/r02_a_recipe40_metrics.jsonl), loaded into the REFERENCE model here
+        sd = {k: torch.from_numpy(v) for k, v in np.load(os.path.join(HERE, "trained96_ema.npz")).items()}
+        gen_sampler("sde96_trained_300", "sde", 96, 8, 300, 1.5, 0.005, state_dict=sd, store_noise=False)
+        gen_sampler("ode96_trained_50", "ode", 96, 4, 50, 1.5, 0.005, state_dict=sd, store_noise=False)
     if want("loss"):
         gen_loss("loss16_b4")
     if want("vae"):

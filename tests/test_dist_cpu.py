@@ -124,3 +124,43 @@ def test_gloo_world2_bucketed_grad_allreduce_matches_flat():
         assert p.exitcode == 0
     for rank, ok, unchanged in res:
         assert ok and unchanged is True, (rank, ok, unchanged)
+
+
+def _presence_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        used = torch.nn.Parameter(torch.ones(4))
+        some = torch.nn.Parameter(torch.ones(3))    # gets a gradient on rank 0 only
+        never = torch.nn.Parameter(torch.ones(5))   # no rank produces a gradient
+        ar = BucketedGradAllReduce([used, some, never], bucket_mb=1e-6)  # one bucket per parameter
+        loss = (used * (rank + 1)).sum()
+        if rank == 0:
+            loss = loss + (some * 4.0).sum()
+        loss.backward()
+        ar.finish()
+        ok = (torch.allclose(used.grad, torch.full((4,), (1 + world) / 2))
+              and torch.allclose(some.grad, torch.full((3,), 4.0 / world)) and never.grad is None)
+        q.put((rank, ok, ""))
+    except Exception as e:  # report instead of leaving the parent waiting on the queue
+        q.put((rank, False, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_grad_presence():
+    """A parameter no rank produced a gradient for keeps grad None (Adam skips it, as in one
+    process); one produced on some ranks only is averaged with zeros (the global-batch mean)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_presence_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, err in res:
+        assert ok, (rank, err)

@@ -203,3 +203,56 @@ def test_oracle_ops_small():
     w2[0, 0, 0, 0] = 1.0  # reads (y-1, x-1) with wrap
     np.testing.assert_allclose(nn_np.conv2d(x, w2, None, padding=1, mode="circular")[:, 0],
                                np.roll(x[:, 0], (1, 1), axis=(1, 2)))
+
+
+# ---------------------------------------------------------------- torch-CPU restatement (bench cpu_baseline)
+@pytest.mark.parametrize("name,base,stored", [("unet16_b3", 16, True), ("unet96_b2", 96, False)])
+def test_torch_oracle_unet_forward(golden, name, base, stored):
+    """oracle/score_model_torch.py (the CPU baseline bench.py times) equals the reference forward."""
+    from oracle.score_model_torch import TorchScoreUNet
+    g = golden(name)
+    sd = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w/")} if stored else \
+        seeded_unet_sd(base)[0].state_dict()
+    o = TorchScoreUNet(sd)
+    t = torch.from_numpy(g["t"])
+    yc, yv = torch.from_numpy(g["y_cat"]), torch.from_numpy(g["y_cont"])
+    assert np.abs(o.maps(t, yc, yv).numpy() - g["maps"]).max() < 1e-6
+    eps = o(torch.from_numpy(g["x_t"]), t, yc, yv).numpy()
+    assert np.abs(eps - g["eps"]).max() < 1e-5
+
+
+def test_torch_oracle_sde_sampler(golden):
+    """Reverse SDE with draws from a CPU generator seeded like the reference's global RNG."""
+    from oracle.score_model_torch import TorchScoreUNet, sample_reverse_sde
+    g = golden("sde16_3step")
+    o = TorchScoreUNet(seeded_unet_sd(16)[0].state_dict())
+    kw = dict(y_cat=torch.from_numpy(g["y_cat"]), y_cont=torch.from_numpy(g["y_cont"]),
+              shape=tuple(g["noise"].shape[1:]), n_steps=int(g["steps"]), s=float(g["cfg"]), t_end=float(g["t_end"]))
+    gen = torch.Generator().manual_seed(int(g["noise_seed"]))
+    x0 = sample_reverse_sde(o, float(g["beta_min"]), float(g["beta_max"]), generator=gen, return_x0_hat=True,
+                            **kw).numpy()
+    ref = g["x0_unclamped"]
+    assert np.abs(x0 - ref).max() < 1e-4 * max(1.0, np.abs(ref).max())
+    gen = torch.Generator().manual_seed(int(g["noise_seed"]))
+    out = sample_reverse_sde(o, float(g["beta_min"]), float(g["beta_max"]), generator=gen, **kw).numpy()
+    assert np.abs(out - g["out"]).max() < 1e-4
+
+
+def test_torch_oracle_trained_sde300_one_image(golden):
+    """The metric's sampler on the genuinely trained fixture (tests/golden/trained96_ema.npz: EMA
+    weights of the README recipe run, profiles/r02_a_recipe40_metrics.jsonl) for image 0 of the
+    golden batch: the reference's draws regenerated from the seed and sliced; 602 forwards of one
+    image.  (At B = 8 the restatement reproduces the golden bit for bit, 0.0.)"""
+    from oracle.score_model_torch import TorchScoreUNet, sample_reverse_sde
+    from toycrystals_amd.models.sde_score_model import host_noise
+    g = golden("sde96_trained_300")
+    B, steps = int(g["B"]), int(g["steps"])
+    o = TorchScoreUNet({k: torch.from_numpy(v) for k, v in golden("trained96_ema").items()})
+    gen = torch.Generator().manual_seed(int(g["noise_seed"]))
+    noise = host_noise((B, 1, 64, 64), steps + 1, gen)[:, :1]
+    x0 = sample_reverse_sde(o, 0.1, 30.0, torch.from_numpy(g["y_cat"][:1]), torch.from_numpy(g["y_cont"][:1]),
+                            (1, 1, 64, 64), steps, float(g["cfg"]), float(g["t_end"]), return_x0_hat=True,
+                            noise=noise).numpy()
+    ref = g["x0_unclamped"][:1]
+    err = np.abs(x0 - ref).max()
+    assert err < 1e-5, err

@@ -743,13 +743,14 @@ int launch3h_w(const ConvParams& p, hipStream_t st) {
     return check_launch("tcx_conv2d_h2(halo)");
 }
 
-// variant: TCX_HALO_NW=8 (k_conv3h, 256-pixel tiles of 8 waves, one workgroup per CU), 4 (k_conv3h,
-// 128-pixel tiles, two workgroups per CU) or 0 (default: k_conv3w, 256-pixel tiles of 4 wide waves)
+// variant: TCX_HALO_NW=4 (default when unset: 128-pixel tiles, two workgroups per CU — k_conv3p, or
+// k_conv3h with TCX_HALO_PIPE=0), 8 (k_conv3h, 256-pixel tiles of 8 waves, one workgroup per CU) or
+// 0 (k_conv3w, 256-pixel tiles of 4 wide waves; slower, kept for A/B)
 int halo_nw() {
     static const int nw = [] {
         const char* e = getenv("TCX_HALO_NW");
-        const int v = e ? atoi(e) : 0;
-        return v == 8 ? 8 : (v == 4 ? 4 : 0);
+        const int v = e ? atoi(e) : 4;
+        return v == 8 ? 8 : (v == 0 ? 0 : 4);
     }();
     return nw;
 }

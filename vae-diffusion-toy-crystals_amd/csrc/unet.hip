@@ -447,12 +447,13 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
             const float drift = ((-0.5f * beta) * xv) - (beta * score);
             const float z = a.z ? a.z[i] : philox_normal(a.seed, a.step + 1, a.e0 + i);
             a.x_inout[i] = (xv + drift * dt) + (g * sq) * z;
-        } else if (a.mode == 2) {
-            // final projection (sde_score_model.py:562-569)
+        } else if (a.mode == 2 || a.mode == 5) {
+            // final projection (sde_score_model.py:562-569); mode 5 stops at x0_hat (:566), before
+            // the (x0 + 1) / 2 map and the clamp (parity reads of the unsaturated trajectory)
             const float sigma = a.scal[4], alpha = a.scal[7];
             const float x0 = (a.x[i] - sigma * eps) / fmaxf(alpha, 1e-6f);
             const float v = (x0 + 1.0f) * 0.5f;
-            a.eps_out[i] = fminf(fmaxf(v, 0.f), 1.f);
+            a.eps_out[i] = a.mode == 5 ? x0 : fminf(fmaxf(v, 0.f), 1.f);
         } else if (a.mode == 3) {
             // Heun stage 1: d = -0.5 b x - 0.5 b score; x_e = x + d dt (sde_score_model.py:444-449,490-491)
             const float dt = a.scal[2], beta = a.scal[3], sigma = a.scal[4];
@@ -874,9 +875,9 @@ int unet_eval_impl(const tcx_unet* net, const float* x, float* x2, const float* 
                    void* ws, size_t ws_bytes, hipStream_t st, size_t e_base) {
     TCX_TRY(validate(net, B, H, W));
     TCX_REQUIRE(x && t && y_cat && y_cont && ws, "tcx_unet_eval: null pointer");
-    TCX_REQUIRE(mode >= 0 && mode <= 4, "tcx_unet_eval: bad mode");
+    TCX_REQUIRE(mode >= 0 && mode <= 5, "tcx_unet_eval: bad mode");
     TCX_REQUIRE(mode == 0 || scal, "tcx_unet_eval: sampler modes need the step table row");
-    TCX_REQUIRE((mode != 0 && mode != 2 && mode != 3 && mode != 4) || eps_out, "tcx_unet_eval: eps_out needed");
+    TCX_REQUIRE(mode == 1 || eps_out, "tcx_unet_eval: eps_out needed");
     TCX_REQUIRE((mode != 1 && mode != 3 && mode != 4) || x_inout, "tcx_unet_eval: x_inout needed");
     TCX_REQUIRE(mode != 3 || x2, "tcx_unet_eval: Heun stage 1 needs x2");
     const int cfg = guidance > 0.f ? 1 : 0;
@@ -915,10 +916,12 @@ extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, con
                           x_inout, eps_out, ws, ws_bytes, (hipStream_t)stream, 0);
 }
 
-extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
-                              int W, int n_steps, float guidance, const float* scal_table, const float* noise,
-                              uint64_t seed, void* ws, size_t ws_bytes, void* stream) {
+extern "C" int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
+                                 int H, int W, int n_steps, float guidance, const float* scal_table, const float* noise,
+                                 uint64_t seed, int flags, void* ws, size_t ws_bytes, void* stream) {
     TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_sde_sample: bad args");
+    TCX_REQUIRE((flags & ~TCX_SAMPLE_X0_HAT) == 0, "tcx_sde_sample: unknown flags %d", flags);
+    const int fmode = (flags & TCX_SAMPLE_X0_HAT) ? 5 : 2;
     const size_t img = (size_t)B * H * W;
     const int L = std::min(lanes_setting(), B);
     const int rows = guidance > 0.f ? 2 * B : B;
@@ -943,7 +946,7 @@ extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_ca
                                            nullptr, wbase + l * lws, lws, ls->s[l], e));
                 } else {  // final projection -> image written over x
                     TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, y_cat + b0, y_cont + (size_t)b0 * net->y_cont_dim,
-                                           b1 - b0, H, W, guidance, 2, row, nullptr, seed, 0, nullptr, x + e,
+                                           b1 - b0, H, W, guidance, fmode, row, nullptr, seed, 0, nullptr, x + e,
                                            wbase + l * lws, lws, ls->s[l], e));
                 }
             }
@@ -962,14 +965,23 @@ extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_ca
     }
     // final projection -> image written over x
     const float* row = scal_table + (size_t)n_steps * TCX_SCAL;
-    return tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 2, row, nullptr, seed, 0, nullptr,
-                         x, ws, ws_bytes, stream);
+    return tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, fmode, row, nullptr, seed, 0,
+                         nullptr, x, ws, ws_bytes, stream);
 }
 
-extern "C" int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
-                              int W, int n_steps, float guidance, const float* scal_table, void* ws, size_t ws_bytes,
-                              void* stream) {
+extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
+                              int W, int n_steps, float guidance, const float* scal_table, const float* noise,
+                              uint64_t seed, void* ws, size_t ws_bytes, void* stream) {
+    return tcx_sde_sample_ex(net, x, y_cat, y_cont, B, H, W, n_steps, guidance, scal_table, noise, seed, 0, ws,
+                             ws_bytes, stream);
+}
+
+extern "C" int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
+                                 int H, int W, int n_steps, float guidance, const float* scal_table, int flags, void* ws,
+                                 size_t ws_bytes, void* stream) {
     TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_ode_sample: bad args");
+    TCX_REQUIRE((flags & ~TCX_SAMPLE_X0_HAT) == 0, "tcx_ode_sample: unknown flags %d", flags);
+    const int fmode = (flags & TCX_SAMPLE_X0_HAT) ? 5 : 2;
     // Scratch for d and x_e lives at the end of the workspace.
     const size_t img = (size_t)B * H * W;
     const size_t need = tcx_unet_workspace_size(net, guidance > 0.f ? 2 * B : B, H, W);
@@ -1003,7 +1015,7 @@ extern "C" int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_ca
                     TCX_TRY(unet_eval_impl(net, xe + e, nullptr, row + TCX_SCAL, 0, yc, yv, b1 - b0, H, W, guidance, 4,
                                            row, nullptr, 0, 0, x + e, d + e, w, lws, ls->s[l], e));
                 } else {
-                    TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, yc, yv, b1 - b0, H, W, guidance, 2, row,
+                    TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, yc, yv, b1 - b0, H, W, guidance, fmode, row,
                                            nullptr, 0, 0, nullptr, x + e, w, lws, ls->s[l], e));
                 }
             }
@@ -1023,8 +1035,14 @@ extern "C" int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_ca
                               d, ws, need, stream));
     }
     const float* row = scal_table + (size_t)n_steps * TCX_SCAL;
-    return tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 2, row, nullptr, 0, 0, nullptr, x,
-                         ws, need, stream);
+    return tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, fmode, row, nullptr, 0, 0, nullptr,
+                         x, ws, need, stream);
+}
+
+extern "C" int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
+                              int W, int n_steps, float guidance, const float* scal_table, void* ws, size_t ws_bytes,
+                              void* stream) {
+    return tcx_ode_sample_ex(net, x, y_cat, y_cont, B, H, W, n_steps, guidance, scal_table, 0, ws, ws_bytes, stream);
 }
 
 extern "C" int tcx_randn(float* out, size_t n, uint64_t seed, uint64_t stream_id, void* stream) {

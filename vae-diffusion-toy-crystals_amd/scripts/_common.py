@@ -45,3 +45,20 @@ def allreduce_scalar_mean(v: float, world: int, device) -> float:
     t = torch.tensor([v], dtype=torch.float64, device=device)
     dist.all_reduce(t)
     return float(t.item()) / world
+
+
+def broadcast_from_lead(tensors, world: int, device):
+    """Rank 0's list of CPU tensors on every rank (shapes and dtypes travel first); identity at
+    world 1.  Returned as CPU tensors."""
+    if world <= 1:
+        return tensors
+    meta = [None]
+    if dist.get_rank() == 0:
+        meta = [[(tuple(t.shape), t.dtype) for t in tensors]]
+    dist.broadcast_object_list(meta, src=0)
+    out = []
+    for i, (shape, dtype) in enumerate(meta[0]):
+        buf = tensors[i].to(device).contiguous() if dist.get_rank() == 0 else torch.empty(shape, dtype=dtype, device=device)
+        dist.broadcast(buf, src=0)
+        out.append(buf.cpu())
+    return out

@@ -97,6 +97,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--prior-ckpt", type=str, default="checkpoints/diffusion_prior_last.pt")
     p.add_argument("--resume", action="store_true")
     p.add_argument("--sample-only", action="store_true")
+    # additive (not in the reference): batch-DP draw semantics
+    p.add_argument("--global-draws", type=int, default=1, choices=[0, 1],
+                   help="1: every rank draws u/eps for the WHOLE global batch from one shared device generator and "
+                        "keeps its slice (N GPUs = 1 GPU); 0: per-rank draws of the local shard")
     return p
 
 
@@ -105,7 +109,7 @@ def main() -> int:
     rank, world, dp_dev = _common.init_dp()
     torch.manual_seed(args.seed)
     device = dp_dev if dp_dev is not None else _common.pick_device(args.device)
-    torch.cuda.manual_seed(args.seed + 7919 * rank)
+    torch.cuda.manual_seed(args.seed if args.global_draws else args.seed + 7919 * rank)
     lead = rank == 0
     for d in ("results", "checkpoints", "data"):
         os.makedirs(d, exist_ok=True)
@@ -115,26 +119,31 @@ def main() -> int:
     vae.eval()
     for p_ in vae.parameters():
         p_.requires_grad_(False)
-    if (not args.rebuild_latents) and os.path.exists(args.latent_cache):
-        obj = torch.load(args.latent_cache, map_location="cpu", weights_only=True)
-        z0, y_cat, y_cont = obj["z0"], obj["y_cat"], obj["y_cont"]
-        if "z_mean" in obj and "z_std" in obj:
-            z_mean, z_std = obj["z_mean"], obj["z_std"]
+    # Rank 0 alone loads or builds the latent set (and writes the cache); under torchrun the other
+    # ranks receive rank 0's tensors by broadcast, so every rank trains on the same latents even
+    # with --z-target sample (whose reparameterisation draws noise) and the encode runs once.
+    latents = None
+    if lead:
+        if (not args.rebuild_latents) and os.path.exists(args.latent_cache):
+            obj = torch.load(args.latent_cache, map_location="cpu", weights_only=True)
+            z0, y_cat, y_cont = obj["z0"], obj["y_cat"], obj["y_cont"]
+            if "z_mean" in obj and "z_std" in obj:
+                z_mean, z_std = obj["z_mean"], obj["z_std"]
+            else:
+                z_mean = z0.mean(dim=0, keepdim=True)
+                z_std = torch.clamp(z0.std(dim=0, keepdim=True), min=1e-6)
+            print(f"loaded latents: {args.latent_cache}  z0={tuple(z0.shape)}")
         else:
+            dl = DeviceBatches(ds, 512, device, shuffle=False, drop_last=False)
+            z0, y_cat, y_cont = build_latent_dataset(vae, dl, device=device, z_target=args.z_target,
+                                                     max_items=args.max_items)
             z_mean = z0.mean(dim=0, keepdim=True)
             z_std = torch.clamp(z0.std(dim=0, keepdim=True), min=1e-6)
-        if lead:
-            print(f"loaded latents: {args.latent_cache}  z0={tuple(z0.shape)}")
-    else:
-        dl = DeviceBatches(ds, 512, device, shuffle=False, drop_last=False)
-        z0, y_cat, y_cont = build_latent_dataset(vae, dl, device=device, z_target=args.z_target,
-                                                 max_items=args.max_items)
-        z_mean = z0.mean(dim=0, keepdim=True)
-        z_std = torch.clamp(z0.std(dim=0, keepdim=True), min=1e-6)
-        if lead:
             torch.save({"z0": z0, "y_cat": y_cat, "y_cont": y_cont, "z_mean": z_mean, "z_std": z_std},
                        args.latent_cache)
             print(f"saved latents: {args.latent_cache}  z0={tuple(z0.shape)}")
+        latents = [z0, y_cat, y_cont, z_mean, z_std]
+    z0, y_cat, y_cont, z_mean, z_std = _common.broadcast_from_lead(latents, world, device)
     z0n = ((z0 - z_mean) / z_std).to(device).contiguous()
     y_cat_d, y_cont_d = y_cat.to(device).contiguous(), y_cont.to(device).contiguous()
     prior = DiffusionPriorFiLM(z_dim=args.z_dim, n_types=args.n_types, y_cont_dim=args.y_cont_dim,
@@ -177,8 +186,13 @@ def main() -> int:
         for i in range(nb):
             idx = order[i * B + rank * per:i * B + (rank + 1) * per]
             z0b, ycb, yvb = z0n.index_select(0, idx), y_cat_d.index_select(0, idx), y_cont_d.index_select(0, idx)
-            u = torch.rand((per,), device=device)
-            eps = torch.randn_like(z0b)
+            if args.global_draws:  # reference order (:251-256) over the global batch, this rank's slice
+                sl = slice(rank * per, (rank + 1) * per)
+                u = torch.rand((B,), device=device)[sl].contiguous()
+                eps = torch.randn((B, args.z_dim), device=device)[sl].contiguous()
+            else:
+                u = torch.rand((per,), device=device)
+                eps = torch.randn_like(z0b)
             check(L.tcx_prior_qsample(ptr(z0b), ptr(eps), ptr(u), ptr(sched.sqrt_alpha_bars),
                                       ptr(sched.sqrt_one_minus_alpha_bars), args.T, per, args.z_dim, ptr(t), ptr(z_t),
                                       st), "tcx_prior_qsample")

@@ -7,7 +7,9 @@ Differences by design: batches come from a device-resident dataset (toycrystals_
 DeviceBatches: one HIP gather per batch) instead of a host DataLoader; the optimiser is the fused
 multi-tensor Adam (state_dict-compatible with torch.optim.Adam); under torchrun each rank trains
 on an equal slice of every global batch and gradients are averaged with one RCCL all-reduce
-(the mean of equal-shard means is the global mean, so the loss semantics are unchanged).
+(the mean of equal-shard means is the global mean, so the loss semantics are unchanged), and
+with --global-draws 1 (default) every rank draws the whole global batch's u/eps/drop from one
+shared device stream and keeps its slice, so an N-GPU run computes the 1-GPU run's step.
 """
 from __future__ import annotations
 
@@ -77,6 +79,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--cfg", type=float, default=0)
     p.add_argument("--t-end", type=float, default=1e-3)
     p.add_argument("--sample-from-ema", type=int, default=1, choices=[0, 1], help="If EMA enabled, save sample grids using EMA weights.")
+    # additive (not in the reference): batch-DP draw semantics
+    p.add_argument("--global-draws", type=int, default=1, choices=[0, 1],
+                   help="1: every rank draws u/eps/drop for the WHOLE global batch from the same device generator "
+                        "(reference order, sde_score_model.py:380-391) and keeps its slice, so an N-GPU run equals "
+                        "the 1-GPU run; 0: per-rank draws of the local shard only")
     return p
 
 
@@ -85,7 +92,8 @@ def main() -> int:
     rank, world, dp_dev = _common.init_dp()
     torch.manual_seed(args.seed)  # identical init on every rank
     device = dp_dev if dp_dev is not None else _common.pick_device(args.device)
-    torch.cuda.manual_seed(args.seed + 7919 * rank)  # per-rank draws (u, eps, dropout)
+    # global draws: one device stream shared by all ranks; else per-rank streams
+    torch.cuda.manual_seed(args.seed if args.global_draws else args.seed + 7919 * rank)
     if args.out_dir is None:
         args.out_dir = os.path.join("runs", "sde_score", _make_run_name(args))
     lead = rank == 0
@@ -136,8 +144,18 @@ def main() -> int:
         total = torch.zeros((), device=device, dtype=torch.float64)
         it = tqdm(dl, desc=f"epoch {epoch + 1:03d}/{args.epochs}", disable=not lead)
         for x0, y_cat, y_cont in it:
+            draws = None
+            if args.global_draws:
+                # the global batch's draws in the reference's order, this rank's slice (DeviceBatches
+                # yields rows [rank*per, (rank+1)*per) of every global batch)
+                Bg, per = args.batch_size, x0.shape[0]
+                u = torch.rand((Bg,), device=device)
+                eps = torch.randn((Bg,) + tuple(x0.shape[1:]), device=device)
+                drop = torch.rand((Bg,), device=device) if args.p_uncond > 0.0 else None
+                sl = slice(rank * per, (rank + 1) * per)
+                draws = (u[sl], eps[sl], drop[sl] if drop is not None else None)
             loss = diffusion_loss_eps(model=model, sde=sde, x0=x0, y_cat=y_cat, y_cont=y_cont,
-                                      p_uncond=args.p_uncond, t_power=args.t_power)
+                                      p_uncond=args.p_uncond, t_power=args.t_power, draws=draws)
             opt.zero_grad(set_to_none=True)
             loss.backward()
             grad_ar.finish()

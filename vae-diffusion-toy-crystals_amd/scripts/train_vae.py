@@ -147,6 +147,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--cond", dest="uncond", action="store_false", help="Train conditional VAE.")
     p.add_argument("--free-bits", type=float, default=0.05, help="Free bits threshold in nats per latent dim (0 disables).")
     p.set_defaults(uncond=False)
+    # additive (not in the reference): batch-DP draw semantics
+    p.add_argument("--global-draws", type=int, default=1, choices=[0, 1],
+                   help="1: every rank draws the reparameterisation eps and the condition-dropout mask for the "
+                        "WHOLE global batch from one shared device generator and keeps its slice (N GPUs = 1 GPU); "
+                        "0: per-rank draws of the local shard")
     return p
 
 
@@ -155,7 +160,7 @@ def main() -> int:
     rank, world, dp_dev = _common.init_dp()
     torch.manual_seed(args.seed)
     device = dp_dev if dp_dev is not None else _common.pick_device(args.device)
-    torch.cuda.manual_seed(args.seed + 7919 * rank)
+    torch.cuda.manual_seed(args.seed if args.global_draws else args.seed + 7919 * rank)
     lead = rank == 0
     os.makedirs("results", exist_ok=True)
     os.makedirs("checkpoints", exist_ok=True)
@@ -184,7 +189,16 @@ def main() -> int:
         model.train()
         tot = torch.zeros(4, device=device, dtype=torch.float64)
         for x, y_cat, y_cont in dl:
-            x_hat, mu, logvar = model(x) if args.uncond else model(x, y_cat, y_cont)
+            draws = None
+            if args.global_draws:
+                # reference order (vae.py:57-60 then :65-67): reparam eps, then the keep mask
+                Bg, per = args.batch_size, x.shape[0]
+                sl = slice(rank * per, (rank + 1) * per)
+                rep = torch.randn((Bg, args.z_dim), device=device)[sl]
+                keep = (torch.rand((Bg, 1), device=device)[sl]
+                        if (not args.uncond and args.cond_drop > 0.0) else None)
+                draws = (rep,) if args.uncond else (rep, keep)
+            x_hat, mu, logvar = model(x, draws=draws) if args.uncond else model(x, y_cat, y_cont, draws=draws)
             recon = TF.mse_loss(x_hat, x)
             kl_used, kl_raw = kl_stats(mu, logvar, free_bits=args.free_bits)
             beta = args.beta * min(1.0, (epoch + 1) / 5.0)

@@ -13,11 +13,6 @@ import os
 
 import torch  # noqa: F401  (must be loaded before libtcx: shared HIP runtime)
 
-# 3x3 halo-conv variant (csrc/conv3h.hip halo_nw): 4 = k_conv3h with two 128-pixel workgroups per
-# CU (the measured fastest, profiles/r01_s); 0 = the wide-wave k_conv3w, still work in progress
-# (its register demand spills to scratch). Read by libtcx at first use; an explicit setting wins.
-os.environ.setdefault("TCX_HALO_NW", "4")
-
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtcx.so")
 
@@ -29,6 +24,7 @@ c_u64 = ctypes.c_uint64
 c_ll = ctypes.c_longlong
 
 TCX_SCAL = 8
+TCX_SAMPLE_X0_HAT = 1  # tcx_{sde,ode}_sample_ex flag: return the unclamped x0_hat
 
 
 class TcxConv(ctypes.Structure):
@@ -93,6 +89,10 @@ _SIGS = {
                                c_fp, c_u64, c_fp, c_size, c_fp]),
     "tcx_ode_sample": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_float, c_fp,
                                c_fp, c_size, c_fp]),
+    "tcx_sde_sample_ex": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_float,
+                                  c_fp, c_fp, c_u64, c_int, c_fp, c_size, c_fp]),
+    "tcx_ode_sample_ex": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_float,
+                                  c_fp, c_int, c_fp, c_size, c_fp]),
     "tcx_randn": (c_int, [c_fp, c_size, c_u64, c_u64, c_fp]),
     "tcx_linear": (c_int, [c_fp, c_int, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_linear_workspace": (c_size, [c_int, c_int, c_int, c_int]),

@@ -83,13 +83,20 @@ class BucketedGradAllReduce:
 
     Parameters are grouped, in reverse registration order (roughly the order backward produces
     their gradients), into buckets of about `bucket_mb` MB.  A post-accumulate-grad hook per
-    parameter copies the fresh gradient into its bucket's flat buffer; when the last gradient of
-    a bucket has arrived, the bucket's all-reduce is launched asynchronously (RCCL runs it on its
-    own stream, ordered after the producing kernels) while the rest of the backward pass is still
-    being computed.  `finish()` waits for the outstanding buckets, divides by the world size and
-    points every `p.grad` at its slice of the averaged buffer.  Same result as `allreduce_grads_`
-    (one flat bucket after backward); the 412 MB of FiLM-prior gradients no longer serialise
-    behind the backward pass.
+    parameter copies the fresh gradient into its bucket's flat buffer; once a bucket is complete
+    AND every bucket before it has been launched, its all-reduce is launched asynchronously (RCCL
+    runs it on its own stream, ordered after the producing kernels) while the rest of the backward
+    pass is still being computed.  Launching strictly in bucket order keeps every rank's sequence
+    of collectives identical even if the ranks' graphs produce gradients in different orders.
+    `finish()` launches what is left, waits, divides by the world size and points every `p.grad`
+    at its slice of the averaged buffer.  Same result as `allreduce_grads_` (one flat bucket after
+    backward); the 412 MB of FiLM-prior gradients no longer serialise behind the backward pass.
+
+    Gradient presence: each bucket carries one extra slot per parameter (1 if this rank produced
+    a gradient for it, summed by the same all-reduce).  A parameter no rank produced a gradient for
+    keeps `p.grad = None` — as in a single-process run, where torch.optim.Adam (and the fused Adam)
+    then skips it; one that only some ranks produced is averaged with zeros from the others (the
+    global-batch mean).
 
     Usage per step: ``opt.zero_grad(set_to_none=True); loss.backward(); ar.finish(); opt.step()``.
     """
@@ -98,8 +105,8 @@ class BucketedGradAllReduce:
         self.group = group
         self.params = [p for p in params if p.requires_grad]
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
-        self.buckets = []  # [params], flat buffer, offsets
-        self.where = {}  # id(param) -> (bucket index, offset)
+        self.buckets = []  # (params, flat buffer incl. presence slots, n data elements)
+        self.where = {}  # id(param) -> (bucket index, offset, index within the bucket)
         cur, cur_bytes = [], 0
         for p in reversed(self.params):
             cur.append(p)
@@ -111,6 +118,7 @@ class BucketedGradAllReduce:
             self._add_bucket(cur)
         self.pending = [0] * len(self.buckets)
         self.works = [None] * len(self.buckets)
+        self.next_launch = 0
         self.hooks = []
         if self.world > 1:
             for p in self.params:
@@ -118,40 +126,62 @@ class BucketedGradAllReduce:
 
     def _add_bucket(self, ps) -> None:
         n = sum(p.numel() for p in ps)
-        flat = torch.empty(n, dtype=ps[0].dtype, device=ps[0].device)
+        flat = torch.zeros(n + len(ps), dtype=ps[0].dtype, device=ps[0].device)
         off = 0
         bi = len(self.buckets)
-        for p in ps:
-            self.where[id(p)] = (bi, off)
+        for j, p in enumerate(ps):
+            self.where[id(p)] = (bi, off, j)
             off += p.numel()
-        self.buckets.append((ps, flat))
+        self.buckets.append((ps, flat, n))
+
+    def _launch(self, bi) -> None:
+        self.works[bi] = dist.all_reduce(self.buckets[bi][1], group=self.group, async_op=True)
+
+    def _launch_ready(self) -> None:
+        while (self.next_launch < len(self.buckets)
+               and self.pending[self.next_launch] == len(self.buckets[self.next_launch][0])):
+            self._launch(self.next_launch)
+            self.next_launch += 1
 
     def _on_grad(self, p) -> None:
-        bi, off = self.where[id(p)]
-        ps, flat = self.buckets[bi]
+        bi, off, j = self.where[id(p)]
+        ps, flat, n = self.buckets[bi]
         flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
+        flat[n + j] = 1.0
         self.pending[bi] += 1
-        if self.pending[bi] == len(ps):
-            self.works[bi] = dist.all_reduce(flat, group=self.group, async_op=True)
+        self._launch_ready()
 
     def finish(self) -> None:
         if self.world <= 1:
             return
-        for bi, (ps, flat) in enumerate(self.buckets):
-            if self.works[bi] is None:  # a parameter without a gradient this step: zeros in its slot
-                for p in ps:
-                    if p.grad is None:
-                        bj, off = self.where[id(p)]
-                        flat[off:off + p.numel()].zero_()
-                self.works[bi] = dist.all_reduce(flat, group=self.group, async_op=True)
-        for bi, (ps, flat) in enumerate(self.buckets):
+        missing = set()
+        for bi in range(self.next_launch, len(self.buckets)):
+            ps, flat, n = self.buckets[bi]
+            for j, p in enumerate(ps):
+                if p.grad is None:  # no gradient on this rank: zeros in its slot, presence 0
+                    _, off, _ = self.where[id(p)]
+                    flat[off:off + p.numel()].zero_()
+                    flat[n + j] = 0.0
+                    missing.add(id(p))
+            self._launch(bi)
+        for bi, (ps, flat, n) in enumerate(self.buckets):
             self.works[bi].wait()
-            flat.div_(self.world)
+            flat[:n].div_(self.world)
+        # Only a parameter without a local gradient needs the global count (one host read, and
+        # none at all in the common step where every parameter got a gradient on this rank).
+        counts = {}
+        if missing:
+            for ps, flat, n in self.buckets:
+                c = flat[n:].cpu().tolist()
+                counts.update({id(p): c[j] for j, p in enumerate(ps) if id(p) in missing})
+        for bi, (ps, flat, n) in enumerate(self.buckets):
             for p in ps:
-                _, off = self.where[id(p)]
-                p.grad = flat[off:off + p.numel()].view_as(p)
+                _, off, _ = self.where[id(p)]
+                keep = id(p) not in missing or counts[id(p)] > 0
+                p.grad = flat[off:off + p.numel()].view_as(p) if keep else None
             self.pending[bi] = 0
             self.works[bi] = None
+        self.next_launch = 0
 
     def remove(self) -> None:
         for h in self.hooks:

@@ -26,7 +26,7 @@ import torch.nn as nn
 
 from .. import _lib
 from .. import functional as TF
-from .._lib import TCX_SCAL, TcxConv, TcxUnet, check, lib, ptr, require_gpu_tensor, stream_ptr
+from .._lib import TCX_SAMPLE_X0_HAT, TCX_SCAL, TcxConv, TcxUnet, check, lib, ptr, require_gpu_tensor, stream_ptr
 
 
 # =========================
@@ -494,7 +494,8 @@ def sample_reverse_sde_euler_maruyama(model: CondUNetTiny, sde: VPSDE, y_cat: to
                                       img_shape: Tuple[int, int, int, int], n_steps: int = 200,
                                       guidance_scale: float = 0.0, t_end: float = 1e-3, *,
                                       noise: Optional[torch.Tensor] = None,
-                                      seed: Optional[int] = None) -> torch.Tensor:
+                                      seed: Optional[int] = None,
+                                      return_x0_hat: bool = False) -> torch.Tensor:
     """Reverse-time SDE via Euler-Maruyama, t: 1 -> t_end (sde_score_model.py:507-569).
 
     The whole loop runs natively (tcx_sde_sample): per step ONE fused CFG-doubled U-Net
@@ -502,6 +503,8 @@ def sample_reverse_sde_euler_maruyama(model: CondUNetTiny, sde: VPSDE, y_cat: to
     Noise: `noise` [n_steps+1, B, 1, H, W] (x_T then one z per step, e.g. host_noise(...)) for
     bit-reproducible parity runs; otherwise x_T and z come from in-kernel Philox4x32-10 keyed by
     `seed` (default: drawn from torch's global CPU generator, so torch.manual_seed governs it).
+    `return_x0_hat=True` returns the projection x0_hat = (x - sigma eps)/max(alpha, 1e-6) of :566
+    itself, before the reference's (x0_hat + 1)/2 map and clamp (:568-569).
     """
     device, B, H, W, t_end, y_cat, y_cont = _sampler_prologue(model, y_cat, y_cont, img_shape, t_end)
     pk = model.tcx_pack(device)
@@ -519,14 +522,15 @@ def sample_reverse_sde_euler_maruyama(model: CondUNetTiny, sde: VPSDE, y_cat: to
         zs = noise[1:]
     g = float(guidance_scale) if guidance_scale > 0.0 else 0.0
     ws, nbytes = pk.workspace(2 * B if g > 0 else B, H, W)
+    flags = TCX_SAMPLE_X0_HAT if return_x0_hat else 0
 
     def launch():
         if noise is not None:
             x.copy_(noise[0].view_as(x))
         else:
             check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
-        check(L.tcx_sde_sample(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g,
-                               ptr(tab), ptr(zs) if zs is not None else None, seed, ptr(ws), nbytes, st),
+        check(L.tcx_sde_sample_ex(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g,
+                                  ptr(tab), ptr(zs) if zs is not None else None, seed, flags, ptr(ws), nbytes, st),
               "tcx_sde_sample")
     pk.run(H, W, launch)
     return x
@@ -537,8 +541,10 @@ def sample_probability_flow_ode(model: CondUNetTiny, sde: VPSDE, y_cat: torch.Te
                                 img_shape: Tuple[int, int, int, int], n_steps: int = 200,
                                 guidance_scale: float = 0.0, t_end: float = 1e-3, *,
                                 x_init: Optional[torch.Tensor] = None,
-                                seed: Optional[int] = None) -> torch.Tensor:
-    """Deterministic probability-flow ODE with Heun steps (sde_score_model.py:452-504)."""
+                                seed: Optional[int] = None,
+                                return_x0_hat: bool = False) -> torch.Tensor:
+    """Deterministic probability-flow ODE with Heun steps (sde_score_model.py:452-504).
+    `return_x0_hat=True`: the unclamped projection of :500 instead of the image of :503-504."""
     device, B, H, W, t_end, y_cat, y_cont = _sampler_prologue(model, y_cat, y_cont, img_shape, t_end)
     pk = model.tcx_pack(device)
     tab = step_table(sde, n_steps, t_end).to(device)
@@ -556,7 +562,8 @@ def sample_probability_flow_ode(model: CondUNetTiny, sde: VPSDE, y_cat: torch.Te
             x.copy_(x_init.to(device=device, dtype=torch.float32).view_as(x))
         else:
             check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
-        check(L.tcx_ode_sample(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g,
-                               ptr(tab), ptr(ws), nbytes, st), "tcx_ode_sample")
+        check(L.tcx_ode_sample_ex(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g,
+                                  ptr(tab), TCX_SAMPLE_X0_HAT if return_x0_hat else 0, ptr(ws), nbytes, st),
+              "tcx_ode_sample")
     pk.run(H, W, launch)
     return x
