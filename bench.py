@@ -51,8 +51,8 @@ SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 m
 # FETCH_SIZE x 2 (gfx950 reports half of 16-B/lane reads) + WRITE_SIZE, averaged over the k_conv<>
 # and k_conv3h<> launches of an evaluation.  A counter pass cannot run inside this process, so the
 # measured value is carried here with its source; it applies to the f16x3 path it was taken on.
-TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 595.7e6}
-TRAFFIC_SOURCE = "rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE, profiles/r01_x_pmc_traffic.txt"
+TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 500.5e6}
+TRAFFIC_SOURCE = "rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE over the default kernels (k_conv3p, k_conv4s2h, k_conv SPL), profiles/r02_b_pmc_traffic.txt"
 
 
 def _cpu_model() -> str:

@@ -143,6 +143,20 @@ int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, int H, int W
                   int stride, int pad, int circular, int act, double* gn_stats, unsigned* ovf,
                   void* stream);
 
+/* tcx_conv2d_h2 with a GroupNorm+SiLU prologue per source: a source whose pro_scale/pro_shift
+ * ([Bt][C] tables from tcx_gn_finalize) are given is read as FP32 and staged as
+ * h2(silu(x * scale[b][c] + shift[b][c])) — GroupNorm(+affine)+SiLU of the _ConvBlock
+ * (sde_score_model.py:103-107) feeding this conv, never written to memory; a source without
+ * tables is h2.  Only the 512-pixel 3x3 kernel takes prologues (3x3 stride 1 pad 1, W in
+ * {32, 64, 128, 256}, Ho*Wo % 512 == 0, Cin % 32 == 0, Cin <= 512, cout_pad % 96 == 0): other
+ * shapes return TCX_EINVAL when a table is passed. */
+int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
+                      const void* wh, const float* wscale, const float* bias, const float* bias_b,
+                      const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
+                      int stride, int pad, int circular, int act, double* gn_stats,
+                      const float* pro_scale1, const float* pro_shift1, const float* pro_scale2,
+                      const float* pro_shift2, unsigned* ovf, void* stream);
+
 /* tcx_gn_apply_tab with the output written as h2 (x == y allowed: in place). */
 int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale,
                         const float* shift, int silu, unsigned* ovf, void* stream);

@@ -1,7 +1,7 @@
 """GPU: the non-default split-path conv variants stay parity-green.
 
-The kernel variant is chosen once per process from the environment (csrc/conv3h.hip halo_nw /
-halo_rt / halo_pipe, csrc/conv4s2h.hip TCX_NO_DSHALO), so each variant runs in ONE child process
+The kernel variant is chosen once per process from the environment (csrc/conv3g.hip TCX_CONV3G,
+csrc/conv3h.hip halo_nw / halo_rt / halo_pipe, csrc/conv4s2h.hip TCX_NO_DSHALO), so each variant runs in ONE child process
 (sequential, one GPU process at a time besides this one) that checks the 3x3 and 4x4/s2 U-Net
 conv shapes against the fp64 numpy oracle at the fp32 gate (2e-5 of the output scale, as
 test_gpu_h2.py).  The default variants are covered by test_gpu_h2.py in this process."""
@@ -38,12 +38,13 @@ assert worst <= 2e-5, worst
 
 
 @pytest.mark.parametrize("env", [
-    {"TCX_HALO_PIPE": "0"},                       # unpipelined k_conv3h (4 waves, two workgroups per CU)
-    {"TCX_HALO_PNW": "8"},                        # k_conv3p with 8 waves, 256-pixel tiles
-    {"TCX_HALO_NW": "8"},                         # k_conv3h, 8 waves, grouped halo staging
-    {"TCX_HALO_NW": "4", "TCX_HALO_RT": "2"},     # k_conv3h, 64 pixels per wave
-    {"TCX_HALO_NW": "0"},                         # k_conv3w wide waves
-    {"TCX_NO_DSHALO": "1", "TCX_NO_HALO": "1"},   # every conv through the im2col kernel
+    {"TCX_CONV3G": "0"},                          # k_conv3p (the round-1 default) on every 3x3 row width
+    {"TCX_CONV3G": "0", "TCX_HALO_PIPE": "0"},    # unpipelined k_conv3h (4 waves, two workgroups per CU)
+    {"TCX_CONV3G": "0", "TCX_HALO_PNW": "8"},     # k_conv3p with 8 waves, 256-pixel tiles
+    {"TCX_CONV3G": "0", "TCX_HALO_NW": "8"},      # k_conv3h, 8 waves, grouped halo staging
+    {"TCX_CONV3G": "0", "TCX_HALO_NW": "4", "TCX_HALO_RT": "2"},  # k_conv3h, 64 pixels per wave
+    {"TCX_CONV3G": "0", "TCX_HALO_NW": "0"},      # k_conv3w wide waves
+    {"TCX_CONV3G": "0", "TCX_NO_DSHALO": "1", "TCX_NO_HALO": "1"},  # every conv through the im2col kernel
 ])
 def test_conv_variant_vs_oracle(env):
     e = dict(os.environ)

@@ -116,6 +116,101 @@ def test_conv_h2_vs_oracle(B, Ci, Co, H, ks, stride, circ):
     fp32_grade(run_conv_h2(x, w, b, stride, pad, circ), run_conv(x, w, b, stride, pad, circ), ref)
 
 
+def run_conv_h2_pro(x, w, b, circular, tabs, x2=None, tabs2=None, gn=False, out_h2=False, expect_ovf=0):
+    """tcx_conv2d_h2_pro: a source with tables (sc, sh [B][C]) is passed as FP32 and normalised +
+    SiLU'd + split in the conv's halo staging (k_conv3g); a source without tables is h2."""
+    B, C1, H, W = x.shape
+    C2 = 0 if x2 is None else x2.shape[1]
+    co, ci, ks, _ = w.shape
+    wh, ws, cpad, kpad = pack_h2(w)
+    y = torch.empty((B, H, W, co), device="cuda")
+    src = lambda t, tb: dev(nhwc(t)) if tb is not None else to_h2(dev(nhwc(t)))  # noqa: E731
+    xd = src(x, tabs)
+    x2d = src(x2, tabs2) if x2 is not None else None
+    tb = [dev(t) for t in tabs] if tabs is not None else [None, None]
+    tb2 = [dev(t) for t in tabs2] if tabs2 is not None else [None, None]
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    gnd = torch.zeros((B, H * W // 128, co, 2), dtype=torch.float64, device="cuda") if gn else None
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    chk(L().tcx_conv2d_h2_pro(xd.data_ptr(), p(x2d), B, 0, H, W, C1, C2, wh.data_ptr(), ws.data_ptr(),
+                              dev(b).data_ptr(), None, None, y.data_ptr(), int(out_h2), co, cpad, kpad, 3, 1, 1,
+                              int(circular), 0, p(gnd), p(tb[0]), p(tb[1]), p(tb2[0]), p(tb2[1]), ovf.data_ptr(), st()))
+    if out_h2:
+        y = from_h2(y)
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == expect_ovf
+    out = nchw(y.cpu().numpy())
+    return (out, gnd.cpu().numpy()) if gn else out
+
+
+def gn_silu_ref(x, tabs):
+    sc, sh = tabs
+    v = x * sc[:, :, None, None] + sh[:, :, None, None]
+    return v / (1.0 + np.exp(-v))
+
+
+def rand_tabs(B, C, seed):
+    g = np.random.default_rng(seed)
+    return (g.uniform(0.5, 2.0, (B, C)).astype(np.float32), g.standard_normal((B, C)).astype(np.float32))
+
+
+@pytest.mark.parametrize("B,Ci,Co,H,circ,two", [
+    (2, 96, 96, 64, True, False),    # up1_1 / down1_1 (64^2)
+    (2, 192, 192, 32, True, False),  # down2_1 (32^2)
+    (2, 96, 96, 32, True, False),    # up2_1
+    (1, 96, 96, 128, True, False),   # config 5's 128^2 rows
+    (2, 64, 96, 32, False, False),   # zero padding: the padded ring is 0 AFTER the transform
+    (2, 96, 96, 64, True, True),     # concat: source 1 h2, source 2 fp32 + tables
+])
+def test_conv_h2_gn_silu_prologue_vs_oracle(B, Ci, Co, H, circ, two):
+    """k_conv3g's GroupNorm+SiLU prologue: conv(silu(x*sc + sh)) against the fp64 oracle of the
+    same (SiLU in fp64), at the fp32 gate and within 2x the fp32-MFMA conv of the pre-normalised
+    input (the fp32 path applies the tables in a separate pass)."""
+    x = rng.standard_normal((B, Ci, H, H)) * 2.0
+    x2 = rng.standard_normal((B, Ci, H, H)) * 1.5 if two else None
+    w = rng.standard_normal((Co, Ci * (2 if two else 1), 3, 3)) / np.sqrt(Ci * 9)
+    b = rng.standard_normal(Co)
+    tabs = rand_tabs(B, Ci, 3)
+    mode = "circular" if circ else "zeros"
+    if two:
+        xin = np.concatenate([x, gn_silu_ref(x2.astype(np.float32).astype(np.float64), tabs)], 1)
+        got = run_conv_h2_pro(x, w, b, circ, None, x2=x2, tabs2=tabs)
+    else:
+        xin = gn_silu_ref(x.astype(np.float32).astype(np.float64), tabs)
+        got = run_conv_h2_pro(x, w, b, circ, tabs)
+    ref = nn_np.conv2d(xin, w, b, padding=1, mode=mode)
+    fp32 = run_conv(xin, w, b, 1, 1, circ)
+    fp32_grade(got, fp32, ref)
+
+
+def test_conv_h2_gn_prologue_gn_stats_and_range_flag():
+    """Prologue + fused GroupNorm partials of the output; a normalised value past the f16 range
+    raises the overflow flag (the evaluator then recomputes in fp32)."""
+    x = rng.standard_normal((2, 96, 64, 64))
+    w = rng.standard_normal((96, 96, 3, 3)) / 30
+    b = rng.standard_normal(96)
+    tabs = rand_tabs(2, 96, 5)
+    ref = nn_np.conv2d(gn_silu_ref(x.astype(np.float32).astype(np.float64), tabs), w, b, padding=1, mode="circular")
+    got, part = run_conv_h2_pro(x, w, b, True, tabs, gn=True)
+    close(got, ref)
+    s = part.sum(axis=1)
+    r = ref.reshape(2, 96, -1)
+    np.testing.assert_allclose(s[..., 0], r.sum(-1), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[..., 1], (r * r).sum(-1), rtol=1e-5, atol=1e-3)
+    big = x.copy()
+    big[1, 7, 9, 11] = 1e5  # silu(1e5 * sc + sh) > 65504
+    run_conv_h2_pro(big, w, b, True, tabs, expect_ovf=1)
+
+
+def test_conv_h2_pro_rejects_uncovered_shape():
+    """A prologue on a shape k_conv3g does not cover (16x16 rows) is an error, not a silent drop."""
+    from toycrystals_amd._lib import TcxError
+    x = rng.standard_normal((2, 96, 16, 16))
+    w = rng.standard_normal((96, 96, 3, 3)) / 30
+    with pytest.raises(TcxError, match="prologue"):
+        run_conv_h2_pro(x, w, np.zeros(96), True, rand_tabs(2, 96, 1))
+
+
 def test_conv_h2_concat_out_h2_gn_stats():
     """Two sources (the U-Net skip concat), h2 output, fused GroupNorm partials."""
     x1 = rng.standard_normal((2, 96, 32, 32))

@@ -59,7 +59,6 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 
 __device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
 // SiLU with the hardware exp2 / reciprocal (a few ulp; used in staged prologues)
-__device__ __forceinline__ float silu_fast(float v) { return __fdividef(v, 1.0f + __expf(-v)); }
 
 __device__ __forceinline__ int wrap_idx(int i, int n) {
     i = i < 0 ? i + n : i;

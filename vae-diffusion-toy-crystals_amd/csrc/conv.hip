@@ -288,10 +288,10 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
                 const int ch = dc.cb + lh * 16 + g * 4;
                 const float4 sc = *reinterpret_cast<const float4*>(&Tr[dc.tsel * PRO_MAXC + ch]);
                 const float4 sh = *reinterpret_cast<const float4*>(&Tr[(dc.tsel + 1) * PRO_MAXC + ch]);
-                fa.x = silu_fast(fmaf(fa.x, sc.x, sh.x));
-                fa.y = silu_fast(fmaf(fa.y, sc.y, sh.y));
-                fa.z = silu_fast(fmaf(fa.z, sc.z, sh.z));
-                fa.w = silu_fast(fmaf(fa.w, sc.w, sh.w));
+                fa.x = silu_f(fmaf(fa.x, sc.x, sh.x));
+                fa.y = silu_f(fmaf(fa.y, sc.y, sh.y));
+                fa.z = silu_f(fmaf(fa.z, sc.z, sh.z));
+                fa.w = silu_f(fmaf(fa.w, sc.w, sh.w));
             }
         }
     };
@@ -574,11 +574,12 @@ extern "C" int tcx_pack_conv_weight_h2(const float* wpk, void* wh, float* wscale
     return check_launch("tcx_pack_conv_weight_h2");
 }
 
-extern "C" int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
-                             const void* wh, const float* wscale, const float* bias, const float* bias_b,
-                             const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
-                             int stride, int pad, int circular, int act, double* gn_stats, unsigned* ovf,
-                             void* stream) {
+extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
+                                 const void* wh, const float* wscale, const float* bias, const float* bias_b,
+                                 const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
+                                 int stride, int pad, int circular, int act, double* gn_stats, const float* pro_scale1,
+                                 const float* pro_shift1, const float* pro_scale2, const float* pro_shift2,
+                                 unsigned* ovf, void* stream) {
     TCX_REQUIRE(x1 && wh && wscale && y, "tcx_conv2d_h2: null pointer");
     TCX_REQUIRE(Bt >= 0 && H > 0 && W > 0 && C1 > 0 && C2 >= 0 && Cout > 0, "tcx_conv2d_h2: bad shape");
     TCX_REQUIRE((C2 == 0) == (x2 == nullptr), "tcx_conv2d_h2: x2/C2 mismatch");
@@ -611,9 +612,26 @@ extern "C" int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, i
     TCX_REQUIRE(b1 < lim && b2 < lim && bw < lim, "tcx_conv2d_h2: operands must be < 2 GiB (32-bit buffer offsets)");
     p.bytes1 = (unsigned)b1; p.bytes2 = (unsigned)b2; p.bytesw = (unsigned)bw;
     p.wscale = wscale; p.out_h2 = out_h2; p.ovf = ovf;
+    TCX_REQUIRE(!pro_scale1 == !pro_shift1 && !pro_scale2 == !pro_shift2 && (C2 > 0 || !pro_scale2),
+                "tcx_conv2d_h2: prologue tables come in scale/shift pairs per source");
+    p.sc1 = pro_scale1; p.sh1 = pro_shift1; p.sc2 = pro_scale2; p.sh2 = pro_shift2;
+    if (conv3g_applies(p, cout_pad)) return launch_conv3g(p, cout_pad, (hipStream_t)stream);
+    TCX_REQUIRE(!pro_scale1 && !pro_scale2,
+                "tcx_conv2d_h2: the GroupNorm+SiLU prologue needs the 512-pixel 3x3 kernel (W in {32,64,128,256}, "
+                "Cin %% 32 == 0, Cout padded to 96k)");
     if (conv3h_applies(p, cout_pad)) return launch_conv3h(p, cout_pad, (hipStream_t)stream);
     if (conv4s2h_applies(p, cout_pad)) return launch_conv4s2h(p, cout_pad, (hipStream_t)stream);
     return launch_conv(p, cout_pad, 0, (hipStream_t)stream);
+}
+
+extern "C" int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
+                             const void* wh, const float* wscale, const float* bias, const float* bias_b,
+                             const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
+                             int stride, int pad, int circular, int act, double* gn_stats, unsigned* ovf,
+                             void* stream) {
+    return tcx_conv2d_h2_pro(x1, x2, Bt, bmod, H, W, C1, C2, wh, wscale, bias, bias_b, resid, y, out_h2, Cout,
+                             cout_pad, kpad, ks, stride, pad, circular, act, gn_stats, nullptr, nullptr, nullptr,
+                             nullptr, ovf, stream);
 }
 
 extern "C" int tcx_conv2d(const float* x1, const float* x2, int Bt, int bmod, int H, int W, int C1, int C2,

@@ -40,6 +40,12 @@ struct ConvParams {
 // Halo-staged 3x3 kernel (conv3h.hip): applicability test and launcher for tcx_conv2d_h2.
 bool conv3h_applies(const ConvParams& p, int cout_pad);
 int launch_conv3h(ConvParams& p, int cout_pad, hipStream_t st);
+// 512-pixel-tile 3x3 kernel with the GroupNorm+SiLU prologue (conv3g.hip): rows W >= 32.
+bool conv3g_applies(const ConvParams& p, int cout_pad);
+// true when a 3x3 stride-1 circular conv of an H x W image with Cin inputs runs on k_conv3g (and so
+// can take the GroupNorm+SiLU prologue of tcx_conv2d_h2_pro)
+bool conv3g_covers(int H, int W, int Cin, int cout_pad);
+int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st);
 // Halo-staged 4x4 stride-2 kernel (conv4s2h.hip): the U-Net downsamples on the split path.
 bool conv4s2h_applies(const ConvParams& p, int cout_pad);
 int launch_conv4s2h(ConvParams& p, int cout_pad, hipStream_t st);

@@ -14,6 +14,10 @@
 //              noise either host-injected or Philox4x32-10 in-kernel.
 #include "common.hpp"
 
+namespace tcx {
+bool conv3g_covers(int H, int W, int Cin, int cout_pad);  // conv3g.hip
+}
+
 #include <cmath>
 
 namespace tcx {
@@ -535,10 +539,11 @@ int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2
     const int HoWo = Ho * Wo;
     const bool fused = gn && HoWo % 128 == 0;
     if (h2.on) {
-        TCX_REQUIRE(cv.wh && cv.wscale && !sc1 && !sc2, "tcx_unet: split path needs packed h2 weights");
-        TCX_TRY(tcx_conv2d_h2(x1, x2, Bt, bmod, H, W, C1, C2, cv.wh, cv.wscale, cv.b, bias_b, resid, y, out_h2,
-                              cv.cout, cv.cout_pad, cv.kpad, cv.ks, stride, pad, 1, 0, fused ? gn : nullptr, h2.ovf,
-                              st));
+        // split path: sc/sh tables here are the GroupNorm+SiLU prologue of k_conv3g (fp32 source)
+        TCX_REQUIRE(cv.wh && cv.wscale, "tcx_unet: split path needs packed h2 weights");
+        TCX_TRY(tcx_conv2d_h2_pro(x1, x2, Bt, bmod, H, W, C1, C2, cv.wh, cv.wscale, cv.b, bias_b, resid, y, out_h2,
+                                  cv.cout, cv.cout_pad, cv.kpad, cv.ks, stride, pad, 1, 0, fused ? gn : nullptr, sc1,
+                                  sh1, sc2, sh2, h2.ovf, st));
     } else {
         TCX_TRY(tcx_conv2d(x1, x2, Bt, bmod, H, W, C1, C2, cv.w, cv.b, bias_b, resid, y, cv.cout, cv.cout_pad,
                            cv.kpad, cv.ks, stride, pad, 1, 0, 0, fused ? gn : nullptr, sc1, sh1, sc2, sh2, st));
@@ -625,6 +630,17 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         pro[4] = can(C2, 0, P.P2);
         pro[7] = can(C, 0, P.P1);
         pro[9] = can(C, 0, P.P0);
+    }
+    // Split path: a GroupNorm+SiLU whose only consumer is a 3x3 conv on k_conv3g (rows of 32/64/128
+    // pixels) is applied by that conv's halo staging from the fp32 tensor (tcx_conv2d_h2_pro), so the
+    // normalised tensor is never written: norms 0, 2, 7, 9 (down1.net.1, down2.net.1, up2.net.1,
+    // up1.net.1 feeding down1/down2/up2/up1 .net.3).  The skip tensors h1/h2 (norms 1, 3: read by a
+    // 4x4/s2 conv AND an up-path concat) and the 16x16 mid block keep the in-place h2 apply pass.
+    if (net->precision == 1) {
+        pro[0] = conv3g_covers(H, W, C, net->down1_1.cout_pad);
+        pro[2] = conv3g_covers(H1, W1, C2, net->down2_1.cout_pad);
+        pro[7] = conv3g_covers(H1, W1, C, net->up2_1.cout_pad);
+        pro[9] = conv3g_covers(H, W, C, net->up1_1.cout_pad);
     }
     auto SC = [&](int i) -> const float* { return pro[i] ? P.sc(i) : nullptr; };
     auto SH = [&](int i) -> const float* { return pro[i] ? P.sh(i) : nullptr; };

@@ -73,6 +73,9 @@ _SIGS = {
     "tcx_pack_conv_weight_h2": (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_fp]),
     "tcx_conv2d_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp, c_fp,
                               c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
+    "tcx_conv2d_h2_pro": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp,
+                                  c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp,
+                                  c_fp, c_fp, c_fp, c_fp, c_fp, c_fp]),
     "tcx_gn_apply_tab_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp, c_fp]),
     "tcx_upsample2x_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
     "tcx_attention_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),
