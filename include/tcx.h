@@ -143,15 +143,24 @@ int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, int H, int W
                   int stride, int pad, int circular, int act, double* gn_stats, unsigned* ovf,
                   void* stream);
 
-/* tcx_conv2d_h2 with a GroupNorm+SiLU prologue per source: a source whose pro_scale/pro_shift
+/* Fragment-ordered copy of a 3x3 h2 conv weight ([cout_pad][9 Cin], cout_pad % 96 == 0, Cin % 32 ==
+ * 0) for the 3x3 kernel k_conv3g, which loads its B fragments straight from it (one coalesced 1 KB
+ * load per wave and fragment, no LDS staging): wf[cout_pad/96][9 Cin/16][3][hi, lo][64][16 B].
+ * Same byte size as wh (tcx_conv_weight_h2_frag_bytes). */
+size_t tcx_conv_weight_h2_frag_bytes(int cout_pad, int Cin);
+int tcx_pack_conv_weight_h2_frag(const void* wh, void* wf, int cout_pad, int kpad, int Cin, void* stream);
+
+/* tcx_conv2d_h2 with the fragment-ordered weights (wfrag, or NULL) and a GroupNorm+SiLU prologue per
+ * source: a source whose pro_scale/pro_shift
  * ([Bt][C] tables from tcx_gn_finalize) are given is read as FP32 and staged as
  * h2(silu(x * scale[b][c] + shift[b][c])) — GroupNorm(+affine)+SiLU of the _ConvBlock
  * (sde_score_model.py:103-107) feeding this conv, never written to memory; a source without
- * tables is h2.  Only the 512-pixel 3x3 kernel takes prologues (3x3 stride 1 pad 1, W in
- * {32, 64, 128, 256}, Ho*Wo % 512 == 0, Cin % 32 == 0, Cin <= 512, cout_pad % 96 == 0): other
- * shapes return TCX_EINVAL when a table is passed. */
+ * tables is h2.  Only k_conv3g takes prologues (wfrag given; 3x3 stride 1 pad 1, W in {32, 64,
+ * 128}, Cin % 32 == 0, Cin <= 384, cout_pad % 96 == 0): otherwise a table is TCX_EINVAL.  Without
+ * wfrag the call is tcx_conv2d_h2. */
 int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
-                      const void* wh, const float* wscale, const float* bias, const float* bias_b,
+                      const void* wh, const void* wfrag, const float* wscale, const float* bias,
+                      const float* bias_b,
                       const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
                       int stride, int pad, int circular, int act, double* gn_stats,
                       const float* pro_scale1, const float* pro_shift1, const float* pro_scale2,
@@ -196,6 +205,7 @@ typedef struct tcx_conv {
     int cin, cout, ks, kpad, cout_pad;
     const void* wh;       /* h2 split of w (tcx_pack_conv_weight_h2), or NULL */
     const float* wscale;  /* device float: inverse power-of-two scale of wh */
+    const void* whf;      /* fragment-ordered copy of wh (tcx_pack_conv_weight_h2_frag), or NULL */
 } tcx_conv;
 
 /* Every pointer refers to device memory prepared by the host mirror of CondUNetTiny

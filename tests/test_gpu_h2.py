@@ -58,7 +58,20 @@ def pack_h2(w):
     return wh, ws, cpad, kpad
 
 
-def run_conv_h2(x, w, b, stride, pad, circular, x2=None, act=0, resid=None, bmod=0, gn=False, Bt=None, out_h2=False):
+def pack_frag(wh, cpad, kpad, cin):
+    """Fragment-ordered copy for k_conv3g (None where it does not apply: the call then runs k_conv3p)."""
+    nb = int(L().tcx_conv_weight_h2_frag_bytes(cpad, cin))
+    if not nb or kpad != 9 * cin:
+        return None
+    wf = torch.empty(nb // 4, device="cuda")
+    chk(L().tcx_pack_conv_weight_h2_frag(wh.data_ptr(), wf.data_ptr(), cpad, kpad, cin, st()))
+    return wf
+
+
+def run_conv_h2(x, w, b, stride, pad, circular, x2=None, act=0, resid=None, bmod=0, gn=False, Bt=None, out_h2=False,
+                frag=True):
+    """frag=True passes the fragment-ordered weights (3x3 convs k_conv3g covers run on it; the rest,
+    and frag=False, on k_conv3p / k_conv4s2h / the im2col kernel)."""
     B, C1, H, W = x.shape
     C2 = 0 if x2 is None else x2.shape[1]
     Bt = Bt or B
@@ -72,11 +85,13 @@ def run_conv_h2(x, w, b, stride, pad, circular, x2=None, act=0, resid=None, bmod
     rd = dev(nhwc(resid)) if resid is not None else None
     gnd = torch.zeros((Bt, -(-Ho * Wo // 128), co, 2), dtype=torch.float64, device="cuda") if gn else None
     ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
-    chk(L().tcx_conv2d_h2(xd.data_ptr(), x2d.data_ptr() if x2d is not None else None, Bt, bmod, H, W, C1, C2,
-                          wh.data_ptr(), ws.data_ptr(), bd.data_ptr() if bd is not None else None, None,
-                          rd.data_ptr() if rd is not None else None, y.data_ptr(), int(out_h2), co, cpad, kpad, ks,
-                          stride, pad, int(circular), act, gnd.data_ptr() if gnd is not None else None,
-                          ovf.data_ptr(), st()))
+    wf = pack_frag(wh, cpad, kpad, C1 + C2) if (frag and ks == 3) else None
+    chk(L().tcx_conv2d_h2_pro(xd.data_ptr(), x2d.data_ptr() if x2d is not None else None, Bt, bmod, H, W, C1, C2,
+                              wh.data_ptr(), wf.data_ptr() if wf is not None else None, ws.data_ptr(),
+                              bd.data_ptr() if bd is not None else None, None,
+                              rd.data_ptr() if rd is not None else None, y.data_ptr(), int(out_h2), co, cpad, kpad, ks,
+                              stride, pad, int(circular), act, gnd.data_ptr() if gnd is not None else None,
+                              None, None, None, None, ovf.data_ptr(), st()))
     if out_h2:
         y = from_h2(y)
     torch.cuda.synchronize()
@@ -107,13 +122,16 @@ def fp32_grade(got, fp32, ref):
     (3, 64, 192, 32, 4, 2, False),  # zero padding, two column blocks
     (1, 32, 96, 128, 4, 2, True),   # Wo = 64 (the 256^2 config's ds2)
 ])
-def test_conv_h2_vs_oracle(B, Ci, Co, H, ks, stride, circ):
+@pytest.mark.parametrize("frag", [True, False], ids=["conv3g", "conv3p"])
+def test_conv_h2_vs_oracle(B, Ci, Co, H, ks, stride, circ, frag):
+    """frag: with the fragment-ordered weights the covered 3x3 shapes run on k_conv3g, without
+    them on k_conv3p (both kernels are live: k_conv3p serves 16x16 rows and the training path)."""
     x = rng.standard_normal((B, Ci, H, H))
     w = rng.standard_normal((Co, Ci, ks, ks)) / np.sqrt(Ci * ks * ks)
     b = rng.standard_normal(Co)
     pad = 0 if ks == 1 else 1
     ref = nn_np.conv2d(x, w, b, stride=stride, padding=pad, mode="circular" if circ else "zeros")
-    fp32_grade(run_conv_h2(x, w, b, stride, pad, circ), run_conv(x, w, b, stride, pad, circ), ref)
+    fp32_grade(run_conv_h2(x, w, b, stride, pad, circ, frag=frag), run_conv(x, w, b, stride, pad, circ), ref)
 
 
 def run_conv_h2_pro(x, w, b, circular, tabs, x2=None, tabs2=None, gn=False, out_h2=False, expect_ovf=0):
@@ -132,7 +150,8 @@ def run_conv_h2_pro(x, w, b, circular, tabs, x2=None, tabs2=None, gn=False, out_
     p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     gnd = torch.zeros((B, H * W // 128, co, 2), dtype=torch.float64, device="cuda") if gn else None
     ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
-    chk(L().tcx_conv2d_h2_pro(xd.data_ptr(), p(x2d), B, 0, H, W, C1, C2, wh.data_ptr(), ws.data_ptr(),
+    wf = pack_frag(wh, cpad, kpad, C1 + C2)
+    chk(L().tcx_conv2d_h2_pro(xd.data_ptr(), p(x2d), B, 0, H, W, C1, C2, wh.data_ptr(), p(wf), ws.data_ptr(),
                               dev(b).data_ptr(), None, None, y.data_ptr(), int(out_h2), co, cpad, kpad, 3, 1, 1,
                               int(circular), 0, p(gnd), p(tb[0]), p(tb[1]), p(tb2[0]), p(tb2[1]), ovf.data_ptr(), st()))
     if out_h2:

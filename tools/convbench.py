@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-layer micro-benchmark of libtcx's implicit-GEMM conv at the U-Net's shapes (Bt=256).
 Prints µs and algorithmic TFLOP/s per layer (HIP events, median of N reps).
-H2=1: the f16x3 split conv (tcx_conv2d_h2) over h2 operands instead of the fp32-MFMA conv."""
+H2=1: the f16x3 split conv (tcx_conv2d_h2) over h2 operands instead of the fp32-MFMA conv; with PRO=1
+the single-source 3x3 layers at W >= 32 read fp32 + GroupNorm tables (k_conv3g's prologue).
+LAYER=name selects one layer, REPS the repetitions; TCX_CONV3G=0 selects k_conv3p for the 3x3 layers."""
 import ctypes, os, sys, statistics
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "vae-diffusion-toy-crystals_amd"))
@@ -50,16 +52,27 @@ def bench(name, H, C1, C2, Co, ks, s, pad, ups, reps=20, gn=True):
             o = torch.empty_like(t)
             check(L.tcx_f32_to_h2(t.data_ptr(), o.data_ptr(), t.numel(), None, st))
             return o
-        x1 = h2(x1)
+        # PRO=1 (H2 mode): source 1 stays fp32 and k_conv3g applies GroupNorm+SiLU tables while staging
+        h2pro = os.environ.get("PRO", "0") == "1" and ks == 3 and s == 1 and C2 == 0 and H >= 32
+        hp = [t.data_ptr() for t in tabs[:2]] if (h2pro and use_pro) else [None, None]
+        if hp[0] is None:
+            x1 = h2(x1)
         x2 = h2(x2) if x2 is not None else None
         wh = torch.empty_like(wpk)
         ws = torch.empty(4, device="cuda")
         check(L.tcx_pack_conv_weight_h2(wpk.data_ptr(), wh.data_ptr(), ws.data_ptr(), cpad, kpad, st))
 
+        nfb = int(L.tcx_conv_weight_h2_frag_bytes(cpad, Cin)) if (ks == 3 and os.environ.get("TCX_CONV3G", "1") != "0") else 0
+        wf = torch.empty(max(nfb // 4, 4), device="cuda")
+        if nfb:
+            check(L.tcx_pack_conv_weight_h2_frag(wh.data_ptr(), wf.data_ptr(), cpad, kpad, Cin, st))
+        wfp = wf.data_ptr() if nfb else None
+
         def run():
-            check(L.tcx_conv2d_h2(x1.data_ptr(), x2.data_ptr() if x2 is not None else None, Bt, 0, H, H, C1, C2,
-                                  wh.data_ptr(), ws.data_ptr(), b.data_ptr(), None, None, y.data_ptr(), 0, Co, cpad,
-                                  kpad, ks, s, pad, 1, 0, g.data_ptr() if g is not None else None, None, st))
+            check(L.tcx_conv2d_h2_pro(x1.data_ptr(), x2.data_ptr() if x2 is not None else None, Bt, 0, H, H, C1, C2,
+                                      wh.data_ptr(), wfp, ws.data_ptr(), b.data_ptr(), None, None, y.data_ptr(), 0, Co,
+                                      cpad, kpad, ks, s, pad, 1, 0, g.data_ptr() if g is not None else None, hp[0],
+                                      hp[1], None, None, None, st))
     else:
       def run():
         check(L.tcx_conv2d(x1.data_ptr(), x2.data_ptr() if x2 is not None else None, Bt, 0, H, H, C1, C2,

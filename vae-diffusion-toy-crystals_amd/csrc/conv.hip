@@ -575,7 +575,8 @@ extern "C" int tcx_pack_conv_weight_h2(const float* wpk, void* wh, float* wscale
 }
 
 extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
-                                 const void* wh, const float* wscale, const float* bias, const float* bias_b,
+                                 const void* wh, const void* wfrag, const float* wscale, const float* bias,
+                                 const float* bias_b,
                                  const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
                                  int stride, int pad, int circular, int act, double* gn_stats, const float* pro_scale1,
                                  const float* pro_shift1, const float* pro_scale2, const float* pro_shift2,
@@ -615,10 +616,12 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
     TCX_REQUIRE(!pro_scale1 == !pro_shift1 && !pro_scale2 == !pro_shift2 && (C2 > 0 || !pro_scale2),
                 "tcx_conv2d_h2: prologue tables come in scale/shift pairs per source");
     p.sc1 = pro_scale1; p.sh1 = pro_shift1; p.sc2 = pro_scale2; p.sh2 = pro_shift2;
+    p.wf = wfrag;
     if (conv3g_applies(p, cout_pad)) return launch_conv3g(p, cout_pad, (hipStream_t)stream);
     TCX_REQUIRE(!pro_scale1 && !pro_scale2,
-                "tcx_conv2d_h2: the GroupNorm+SiLU prologue needs the 512-pixel 3x3 kernel (W in {32,64,128,256}, "
-                "Cin %% 32 == 0, Cout padded to 96k)");
+                "tcx_conv2d_h2: the GroupNorm+SiLU prologue needs k_conv3g: the fragment-ordered weights "
+                "(tcx_pack_conv_weight_h2_frag) and a 3x3 stride-1 conv with W in {32, 64, 128}, Cin %% 32 == 0, "
+                "Cin <= 384, Cout padded to 96k");
     if (conv3h_applies(p, cout_pad)) return launch_conv3h(p, cout_pad, (hipStream_t)stream);
     if (conv4s2h_applies(p, cout_pad)) return launch_conv4s2h(p, cout_pad, (hipStream_t)stream);
     return launch_conv(p, cout_pad, 0, (hipStream_t)stream);
@@ -629,7 +632,7 @@ extern "C" int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, i
                              const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
                              int stride, int pad, int circular, int act, double* gn_stats, unsigned* ovf,
                              void* stream) {
-    return tcx_conv2d_h2_pro(x1, x2, Bt, bmod, H, W, C1, C2, wh, wscale, bias, bias_b, resid, y, out_h2, Cout,
+    return tcx_conv2d_h2_pro(x1, x2, Bt, bmod, H, W, C1, C2, wh, nullptr, wscale, bias, bias_b, resid, y, out_h2, Cout,
                              cout_pad, kpad, ks, stride, pad, circular, act, gn_stats, nullptr, nullptr, nullptr,
                              nullptr, ovf, stream);
 }

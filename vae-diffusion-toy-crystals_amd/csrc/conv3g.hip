@@ -1,21 +1,26 @@
 // k_conv3g: the 3x3 stride-1 circular conv of the U-Net rows W >= 32 (every _ConvBlock conv and
-// us*_conv at 64^2 / 32^2, and the 128^2 / 256^2 rows of config 5: /root/reference/src/toycrystals/
+// us*_conv at 64^2 / 32^2, and the 128^2 rows of config 5: /root/reference/src/toycrystals/
 // models/sde_score_model.py:102,105,218,222) on the f16x3 split path, with the preceding
 // GroupNorm + SiLU (:103-107) applied while the input halo is staged.
 //
-// Why a new tiling (k_conv3p, conv3h.hip, stays for 16^2): k_conv3p's 128-pixel x 96-channel tile
-// re-reads the whole weight chunk from LDS per wave per 32 pixels, and stages the 12 KB weight chunk
-// of every tap with ds_write_b128 for only 128 pixels: its LDS traffic is ~0.8 of the MFMA time
-// (PMC r01_bh: MFMA busy 48 % at 64^2).  Here 8 waves each own 64 pixels (two
-// 32-row blocks) x 96 channels (a 512-pixel tile = whole rows), so every B fragment read from LDS
-// feeds two MFMAs, and the input-channel chunk is 16 deep: per tap the weight chunk is 6 KB for 512
-// pixels (1/8 of k_conv3p's staging per FLOP) and each wave issues 18 MFMAs per 10 ds_read_b128
-// (k_conv3p: 9 per 8).  Two waves per SIMD, one 512-thread workgroup per CU.
+// Why a new kernel (k_conv3p, conv3h.hip, stays for 16^2 and for callers without the fragment-
+// ordered weights): k_conv3p stages every tap's weight chunk through LDS and so needs a workgroup
+// barrier per tap (18 MFMAs per wave); its MFMA pipe is busy 45-48 % (PMC r01_bh, r02_f), the rest
+// mostly waves parked at those barriers with both waves of a SIMD in the same phase.  Here:
+//  * each wave owns 64 pixels (two 32-row blocks) x 96 channels, so a B fragment feeds two MFMAs;
+//  * the input-channel chunk is 16 deep and B fragments come straight from global memory (L1/L2:
+//    the 6 KB of a tap are read by every wave of the CU) in a fragment-ordered copy of the weights
+//    (tcx_pack_conv_weight_h2_frag: one coalesced 1 KB dwordx4 load per wave per fragment), loaded
+//    one tap ahead into the second of two register sets — no weight staging, no weight barrier;
+//  * only the halo is in LDS, double-buffered: halo j+1 is staged during taps 2-5 of chunk j, so
+//    a chunk of 9 taps (162 MFMAs per wave) needs 2 barriers (after taps 1 and 6) instead of 9.
+// NW = 4 waves (256-pixel tiles, two workgroups per CU) for rows of 32/64 pixels, NW = 8
+// (512-pixel tiles, one per CU) at 128.
 //
 // LDS: two halo buffers [(TR+2)*(W+2)][20 floats] (16 channels h2 = 64 B per pixel + 16 B pad: the
 // 80-B pixel stride makes the ds_read_b128 of 32 consecutive pixels conflict free for every tap
-// offset), weights [2][96][20 floats], GroupNorm tables [2][Cin] of the tile's image: 124 KB at
-// W = 64, 143 KB at W = 128 (W = 256 would not fit: those rows stay on the im2col kernel).
+// offset) and the GroupNorm tables [2][Cin] of the tile's image: 66 KB at W = 64 (two per CU),
+// 128 KB at W = 128.  (W = 256 would not fit: those rows stay on the im2col kernel.)
 //
 // Prologue: a source may be h2 (copied) or fp32 + a per-(image, channel) GroupNorm scale/shift table
 // (tcx_gn_finalize): x -> silu(x*sc + sh) is computed per 8-channel unit two taps after its load and
@@ -25,32 +30,34 @@
 // rounded to the 22-bit h2 split right after, so the difference to expf/IEEE division is below the
 // split's own rounding (h2.hpp).
 //
-// Pipeline per tap t of chunk j (c = 9j + t; B set S = c & 1 in registers, A0 = tap t's row block 0;
-// halo j in buffer j & 1, halo j+1 filled into the other buffer during taps 0..UPT+1):
-//   read A1(t) | 9 MFMAs (row block 0) | read A0(t+1), B(t+1) into set S^1 | 9 MFMAs (row block 1) |
-//   [t < UPT: load halo unit t of j+1]  [2 <= t < UPT+2: GN+SiLU+split and store unit t-2]
-//   store weights c+2 | barrier | load weights c+4
-// The weights of chunk c+2 go into LDS buffer c & 1, whose data (chunk c) every wave read into
-// registers before the previous barrier; halo buffer (j+1) & 1 was last read (taps 8 of chunk j-1)
-// before the last barrier of chunk j-1, and is complete before the barrier of tap 5 (UPT <= 4),
-// ahead of its first read (A0 of tap 0 of chunk j+1, read during tap 8).
+// Per tap t of chunk j (c = 9j + t; B set S = c & 1 holds B(c); A0 = row block 0 of tap t):
+//   load B(c+1) -> set S^1 | read A1(t) | 9 MFMAs (row block 0) | read A0(t+1) | 9 MFMAs (row block 1)
+//   [t < UPT: load halo unit t of j+1] [2 <= t < UPT+2: GN+SiLU+split, store unit t-2 into the other
+//   halo buffer] [t == 1, t == 6: barrier]
+// The other halo buffer held halo j-1, last read during tap 7 of chunk j-1 (the A fragments of tap
+// 8 are read one tap early), before the barrier after tap 1 of chunk j; its stores end at tap 5,
+// before the barrier after tap 6; its first read is A0 of tap 0 of chunk j+1, during tap 8.
 #include "conv_common.hpp"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace tcx {
 namespace {
 
-constexpr int G_PXF = 20;   // floats per staged pixel / weight row: 16 channels h2 (64 B) + 16 B pad
+constexpr int G_PXF = 20;   // floats per staged halo pixel: 16 channels h2 (64 B) + 16 B pad
 constexpr int G_KC = 16;    // input channels per chunk
-constexpr int G_TP = 512;   // output pixels per tile
 constexpr int G_NT = 3;     // 32-channel accumulator tiles per wave (96 output channels)
 
-__host__ __device__ constexpr int g_npx(int W) { return (G_TP / W + 2) * (W + 2); }
-__host__ __device__ constexpr int g_units(int W) { return (2 * g_npx(W) + 511) / 512; }  // 8-ch units per thread
+// NW waves of 64 pixels: tile TP = 64 NW output pixels = whole rows
+__host__ __device__ constexpr int g_tp(int NW) { return 64 * NW; }
+__host__ __device__ constexpr int g_npx(int W, int NW) { return (g_tp(NW) / W + 2) * (W + 2); }
+__host__ __device__ constexpr int g_units(int W, int NW) { return (2 * g_npx(W, NW) + 64 * NW - 1) / (64 * NW); }
+// NW = 4 (two workgroups per CU) for rows of 32/64 pixels, NW = 8 (one per CU) for 128
+__host__ __device__ constexpr int g_nw(int W) { return W >= 128 ? 8 : 4; }
 
-constexpr size_t conv3g_lds_bytes(int W, int Cin) {
-    return ((size_t)2 * g_npx(W) * G_PXF + 2 * 96 * G_PXF + 2 * (size_t)Cin) * sizeof(float);
+constexpr size_t conv3g_lds_bytes(int W, int NW, int Cin) {
+    return ((size_t)2 * g_npx(W, NW) * G_PXF + 2 * (size_t)Cin) * sizeof(float);
 }
 
 __device__ __forceinline__ float silu_split_src(float v, float sc, float sh) {
@@ -72,27 +79,26 @@ __device__ __forceinline__ void split8(const float (&v)[8], float4& hi, float4& 
     lo = make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), __uint_as_float(l[2]), __uint_as_float(l[3]));
 }
 
-template <int W, bool CIRC>
-__global__ __launch_bounds__(512, 2) void k_conv3g(ConvParams p) {
-    constexpr int NW = 8, RT = 2, NT = G_NT, BN = 32 * NT, NTHR = 512;
+template <int W, int NW, bool CIRC>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
+    constexpr int RT = 2, NT = G_NT, BN = 32 * NT, NTHR = 64 * NW;
+    constexpr int TP = g_tp(NW);
     constexpr int W2 = W + 2;
-    constexpr int NPX = g_npx(W);
+    constexpr int NPX = g_npx(W, NW);
     constexpr int NU = 2 * NPX;        // 8-channel halo units per chunk
-    constexpr int UPT = g_units(W);
+    constexpr int UPT = g_units(W, NW);
     constexpr int HBUF = NPX * G_PXF;
-    constexpr int WBUF = BN * G_PXF;
-    constexpr int WPC = BN * 4;        // 16-B weight pieces per chunk (384)
+    static_assert(UPT <= 4, "halo units per thread: stores must finish by tap 5");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* const Hs = sm;                   // [2][NPX][PXF]
-    float* const Bs = sm + 2 * HBUF;        // [2][BN][PXF]
-    float* const Ts = Bs + 2 * WBUF;        // [2][Cin]: scale, shift of this tile's image
+    float* const Ts = sm + 2 * HBUF;        // [2][Cin]: scale, shift of this tile's image
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int mblk = tile / p.n_nblk;
     const int nblk = tile - mblk * p.n_nblk;
-    const int m0 = mblk * G_TP, n0 = nblk * BN;
+    const int m0 = mblk * TP, n0 = nblk * BN;
     const int b = m0 / p.HoWo;
     const int r0 = (m0 - b * p.HoWo) / W;
     const int bs = p.bmod > 0 ? b % p.bmod : b;
@@ -104,7 +110,7 @@ __global__ __launch_bounds__(512, 2) void k_conv3g(ConvParams p) {
 
     const __amdgpu_buffer_rsrc_t r1 = mk_rsrc(p.x1, p.bytes1);
     const __amdgpu_buffer_rsrc_t r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
-    const __amdgpu_buffer_rsrc_t rw = mk_rsrc(p.w, p.bytesw);
+    const __amdgpu_buffer_rsrc_t rw = mk_rsrc(reinterpret_cast<const float*>(p.wf), p.bytesw);
 
     // ---- GroupNorm tables of this tile's image (concatenated channel order)
     if (gn1 || gn2) {
@@ -119,13 +125,14 @@ __global__ __launch_bounds__(512, 2) void k_conv3g(ConvParams p) {
         }
     }
 
-    // ---- halo plan: unit u = tid + 512 i -> halo pixel u >> 1, 8-channel group u & 1
+    // ---- halo plan: unit u = tid + NTHR i -> halo pixel u % NPX, 8-channel group u / NPX (eight
+    // consecutive lanes store eight consecutive 80-B pixel slots: conflict-free ds_write_b128)
     const int rowb = p.C1 * 4;  // bytes per source pixel (C2 == C1 when there are two sources)
     int hoff[UPT];              // source byte offset of the unit (kOOB: zero padding)
 #pragma unroll
     for (int i = 0; i < UPT; ++i) {
         const int u = tid + NTHR * i;
-        const int hp = u >> 1;
+        const int hp = u < NPX ? u : u - NPX;
         hoff[i] = kOOB;
         if (u < NU) {
             const int hr = hp / W2, hc = hp - hr * W2;
@@ -137,10 +144,12 @@ __global__ __launch_bounds__(512, 2) void k_conv3g(ConvParams p) {
             } else {
                 ok = y >= 0 && y < H && x >= 0 && x < W;
             }
-            hoff[i] = ok ? ((bs * H + y) * W + x) * rowb + (u & 1) * 32 : kOOB;
+            hoff[i] = ok ? ((bs * H + y) * W + x) * rowb + (u < NPX ? 0 : 32) : kOOB;
         }
     }
-    static_assert(UPT <= 4, "halo units per thread: stores must finish by tap 5");
+    // Every vector-memory load is unconditional (after the last chunk the loads re-read valid bytes
+    // that are never used): a load under a branch makes hipcc's wait counting fall back to
+    // vmcnt(0), which would drain the halo loads in flight.
     float4 hv[UPT][2];  // unit i of the next halo (loaded at tap i, stored at tap i+2)
     auto src_of = [&](int j, __amdgpu_buffer_rsrc_t& rs, int& cc) {
         const int ci0 = j * G_KC;
@@ -163,7 +172,7 @@ __global__ __launch_bounds__(512, 2) void k_conv3g(ConvParams p) {
         __amdgpu_buffer_rsrc_t rs;
         int cc;
         if (src_of(j, rs, cc)) {
-            const int c = j * G_KC + (u & 1) * 8;
+            const int c = j * G_KC + (u < NPX ? 0 : 8);
             const float4 s0 = *reinterpret_cast<const float4*>(&Ts[c]);
             const float4 s1v = *reinterpret_cast<const float4*>(&Ts[c + 4]);
             const float4 h0 = *reinterpret_cast<const float4*>(&Ts[Cin + c]);
@@ -180,31 +189,18 @@ __global__ __launch_bounds__(512, 2) void k_conv3g(ConvParams p) {
             split8(v, hv[i][0], hv[i][1], bad);
             h2_flag(p.ovf, bad);
         }
-        float* d = &Hs[buf * HBUF + (u >> 1) * G_PXF + (u & 1) * 8];
+        float* d = &Hs[buf * HBUF + (u < NPX ? u * G_PXF : (u - NPX) * G_PXF + 8)];
         *reinterpret_cast<float4*>(d) = hv[i][0];
         *reinterpret_cast<float4*>(d + 4) = hv[i][1];
     };
-    // ---- weight chunk c = 9 j + t: rows n0..n0+95, packed k = t*Cin + 16 j (4 pieces of 16 B)
-    const bool wthr = tid < WPC;
-    const int woff = ((n0 + (tid >> 2)) * p.kpad) * 4 + (tid & 3) * 16;
-    const int wdst = (tid >> 2) * G_PXF + (tid & 3) * 4;
-    float4 wr[2];
-    auto w_load = [&](int c, float4& r) {
-        const int j = c / 9, t = c - 9 * j;
-        if (wthr) r = bld4(rw, woff, (t * Cin + j * G_KC) * 4);
-    };
-    auto w_store = [&](int buf, const float4& r) {
-        if (wthr) *reinterpret_cast<float4*>(&Bs[buf * WBUF + wdst]) = r;
-    };
 
-    // ---- fragments
+    // ---- fragments.  B: fragment-ordered weights [nblk][chunk c][n][hi, lo][lane][16 B]
     int abase[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
         const int mloc = (wv * RT + rt) * 32 + li;
         abase[rt] = ((mloc / W) * W2 + (mloc % W)) * G_PXF + lh * 8;
     }
-    const int bbase = li * G_PXF + lh * 8;
     f32x16 acc[RT][NT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
@@ -217,12 +213,14 @@ __global__ __launch_bounds__(512, 2) void k_conv3g(ConvParams p) {
         a_h[rt] = __builtin_bit_cast(h8, ld4(A));
         a_l[rt] = __builtin_bit_cast(h8, ld4(A + 4));
     };
-    auto rd_b = [&](int s, int buf) {
-        const float* B = &Bs[buf * WBUF + bbase];
+    const int bl = lane * 16;
+    auto ld_b = [&](int s, int c) {
+        c = c < nch ? c : nch - 1;
+        const int cb = ((nblk * nch + c) * NT) * 2048;  // NT fragments of [2][64][16 B]
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-            b_h[s][n] = __builtin_bit_cast(h8, ld4(B + n * 32 * G_PXF));
-            b_l[s][n] = __builtin_bit_cast(h8, ld4(B + n * 32 * G_PXF + 4));
+            b_h[s][n] = __builtin_bit_cast(h8, bld4(rw, bl, cb + n * 2048));
+            b_l[s][n] = __builtin_bit_cast(h8, bld4(rw, bl, cb + n * 2048 + 1024));
         }
     };
     auto mf = [&](int rt, int s) {
@@ -237,51 +235,41 @@ __global__ __launch_bounds__(512, 2) void k_conv3g(ConvParams p) {
             acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[rt], b_h[s][n], acc[rt][n], 0, 0, 0);
     };
 
-    // ---- prologue: tables, halo 0 and weight chunks 0 and 1 in LDS; chunks 2, 3 in flight
+    // ---- prologue: tables, halo 0 in LDS; B(0) in registers
     if (gn1 || gn2) __syncthreads();  // Ts before the first transform
 #pragma unroll
     for (int i = 0; i < UPT; ++i) unit_load(0, i);
-    w_load(0, wr[0]);
-    w_load(1, wr[1]);
+    ld_b(0, 0);
 #pragma unroll
     for (int i = 0; i < UPT; ++i) unit_store(0, i, 0);
-    w_store(0, wr[0]);
-    w_store(1, wr[1]);
-    w_load(2, wr[0]);
-    w_load(3, wr[1]);
     __syncthreads();
     rd_a(0, 0, 0);
-    rd_b(0, 0);
 
-    // one tap: T compile-time tap index, S the register set of B(c) (c & 1), HB halo buffer of chunk j
+    // one tap: T compile-time tap index, S the register set of B(c) (c & 1), HBc halo buffer of chunk j
     auto iter = [&](int j, auto T, auto S, auto HBc) {
         constexpr int t = decltype(T)::value;
         constexpr int s = decltype(S)::value;
         constexpr int hb = decltype(HBc)::value;
         const int c = 9 * j + t;
         const bool more = j + 1 < cpt;
-        if (t != 8) rd_a(1, t, hb);  // A1(8) was read at the end of tap 7
+        ld_b(s ^ 1, c + 1);
+        if (t != 8) rd_a(1, t, hb);  // A1(8) was read during tap 7
         __builtin_amdgcn_sched_barrier(0);
         mf(0, s);
         __builtin_amdgcn_sched_barrier(0);
         if (c + 1 < nch) {
             if (t == 8) rd_a(0, 0, hb ^ 1);
             else rd_a(0, t + 1, hb);
-            rd_b(s ^ 1, (c + 1) & 1);
         }
         __builtin_amdgcn_sched_barrier(0);
         mf(1, s);
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
-        if constexpr (t < UPT) {
-            if (more) unit_load(j + 1, t);
-        }
+        if constexpr (t < UPT) unit_load(more ? j + 1 : j, t);  // (not stored after the last chunk)
         if constexpr (t >= 2 && t < UPT + 2) {
             if (more) unit_store(j + 1, t - 2, hb ^ 1);
         }
-        if (c + 2 < nch) w_store(c & 1, wr[s]);
-        __syncthreads();
-        if (c + 4 < nch) w_load(c + 4, wr[s]);
+        if (t == 1 || t == 6) __syncthreads();
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
@@ -312,22 +300,46 @@ __global__ __launch_bounds__(512, 2) void k_conv3g(ConvParams p) {
     }
 }
 
+// Fragment-ordered copy of h2 conv weights for k_conv3g: wf[nblk][c = 9 j + t][n][hi, lo][lane][16 B]
+// = the 8 hi (or lo) halves of weight row 96 nblk + 32 n + (lane & 31), packed k = t Cin + 16 j +
+// 8 (lane >> 5) (h2 group of 8 channels: [8 hi][8 lo] = 32 B at byte 4 k of the row).
+__global__ void k_pack_frag(const char* __restrict__ wh, char* __restrict__ wf, int kpad, int Cin, int nblk_n) {
+    const int cpt = Cin / G_KC, nch = 9 * cpt;
+    const size_t n16 = (size_t)nblk_n * nch * G_NT * 2 * 64;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(i & 63);
+        size_t q = i >> 6;
+        const int hl = (int)(q & 1);
+        q >>= 1;
+        const int n = (int)(q % G_NT);
+        q /= G_NT;
+        const int c = (int)(q % nch);
+        const int nb = (int)(q / nch);
+        const int j = c / 9, t = c - 9 * j;
+        const int row = nb * 96 + n * 32 + (lane & 31);
+        const int k = t * Cin + j * G_KC + 8 * (lane >> 5);
+        *reinterpret_cast<float4*>(wf + i * 16) =
+            *reinterpret_cast<const float4*>(wh + ((size_t)row * kpad + k) * 4 + hl * 16);
+    }
+}
+
 template <int W>
 int launch3g(const ConvParams& p, hipStream_t st) {
-    const size_t shm = conv3g_lds_bytes(W, p.Cin);
+    constexpr int NW = g_nw(W);
+    const size_t shm = conv3g_lds_bytes(W, NW, p.Cin);
     static bool attr[2] = {false, false};
-    auto kc = p.circular ? &k_conv3g<W, true> : &k_conv3g<W, false>;
+    auto kc = p.circular ? &k_conv3g<W, NW, true> : &k_conv3g<W, NW, false>;
     if (!attr[p.circular ? 1 : 0]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)conv3g_lds_bytes(W, 512)) != hipSuccess) {
-            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3g_lds_bytes(W, 512));
+                                (int)conv3g_lds_bytes(W, NW, 384)) != hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3g_lds_bytes(W, NW, 384));
             return TCX_EHIP;
         }
         attr[p.circular ? 1 : 0] = true;
     }
-    const int grid = (p.M / G_TP) * p.n_nblk;
-    hipLaunchKernelGGL(kc, dim3(grid), dim3(512), shm, st, p);
-    return check_launch("tcx_conv2d_h2(halo 512)");
+    const int grid = (p.M / g_tp(NW)) * p.n_nblk;
+    hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * NW), shm, st, p);
+    return check_launch("tcx_conv2d_h2(halo 3g)");
 }
 
 }  // namespace
@@ -342,17 +354,15 @@ bool conv3g_enabled() {
 }
 
 bool conv3g_covers(int H, int W, int Cin, int cout_pad) {
-    return conv3g_enabled() && (W == 32 || W == 64 || W == 128) && H % (G_TP / W) == 0 && (H * W) % G_TP == 0 &&
-           Cin % 32 == 0 && Cin <= 512 && cout_pad % 96 == 0;
+    if (!conv3g_enabled() || !(W == 32 || W == 64 || W == 128)) return false;
+    const int tp = g_tp(g_nw(W));
+    return H % (tp / W) == 0 && (H * W) % tp == 0 && Cin % 32 == 0 && Cin <= 384 && cout_pad % 96 == 0;
 }
 
 bool conv3g_applies(const ConvParams& p, int cout_pad) {
-    if (!conv3g_enabled()) return false;
-    const bool wok = p.W == 32 || p.W == 64 || p.W == 128;
-    return wok && p.ks == 3 && p.stride == 1 && p.pad_y == 1 && p.pad_x == 1 && p.Hi == p.H && p.Wi == p.W &&
-           p.H % (G_TP / p.W) == 0 && p.HoWo % G_TP == 0 && cout_pad % 96 == 0 && p.Cin % 32 == 0 &&
-           p.Cin <= 512 && p.C1 % G_KC == 0 && (p.C2 == 0 || p.C2 == p.C1) && p.kpad == 9 * p.Cin && p.osy == 1 &&
-           p.osx == 1;
+    return p.wf != nullptr && conv3g_covers(p.H, p.W, p.Cin, cout_pad) && p.ks == 3 && p.stride == 1 && p.pad_y == 1 && p.pad_x == 1 &&
+           p.Hi == p.H && p.Wi == p.W && p.C1 % G_KC == 0 && (p.C2 == 0 || p.C2 == p.C1) && p.kpad == 9 * p.Cin &&
+           p.osy == 1 && p.osx == 1;
 }
 
 int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st) {
@@ -368,3 +378,20 @@ int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st) {
 }
 
 }  // namespace tcx
+
+using namespace tcx;
+
+extern "C" size_t tcx_conv_weight_h2_frag_bytes(int cout_pad, int Cin) {
+    return (cout_pad % 96 == 0 && Cin % 32 == 0) ? (size_t)cout_pad * 9 * Cin * 4 : 0;
+}
+
+extern "C" int tcx_pack_conv_weight_h2_frag(const void* wh, void* wf, int cout_pad, int kpad, int Cin, void* stream) {
+    TCX_REQUIRE(wh && wf && cout_pad > 0 && cout_pad % 96 == 0 && Cin > 0 && Cin % 32 == 0 && kpad == 9 * Cin,
+                "tcx_pack_conv_weight_h2_frag: needs a 3x3 h2 weight with cout_pad %% 96 == 0, Cin %% 32 == 0");
+    TCX_REQUIRE(aligned16(wh) && aligned16(wf), "tcx_pack_conv_weight_h2_frag: 16-B alignment");
+    const size_t n16 = (size_t)cout_pad * 9 * Cin * 4 / 16;
+    const int blocks = (int)std::min<size_t>((n16 + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_pack_frag, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const char*)wh, (char*)wf, kpad,
+                       Cin, cout_pad / 96);
+    return check_launch("tcx_pack_conv_weight_h2_frag");
+}

@@ -35,6 +35,8 @@ struct ConvParams {
     const float* wscale;
     int out_h2;
     unsigned* ovf;
+    // fragment-ordered copy of the h2 weights (tcx_pack_conv_weight_h2_frag) or null: k_conv3g only
+    const void* wf;
 };
 
 // Halo-staged 3x3 kernel (conv3h.hip): applicability test and launcher for tcx_conv2d_h2.

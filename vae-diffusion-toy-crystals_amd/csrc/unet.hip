@@ -541,7 +541,7 @@ int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2
     if (h2.on) {
         // split path: sc/sh tables here are the GroupNorm+SiLU prologue of k_conv3g (fp32 source)
         TCX_REQUIRE(cv.wh && cv.wscale, "tcx_unet: split path needs packed h2 weights");
-        TCX_TRY(tcx_conv2d_h2_pro(x1, x2, Bt, bmod, H, W, C1, C2, cv.wh, cv.wscale, cv.b, bias_b, resid, y, out_h2,
+        TCX_TRY(tcx_conv2d_h2_pro(x1, x2, Bt, bmod, H, W, C1, C2, cv.wh, cv.whf, cv.wscale, cv.b, bias_b, resid, y, out_h2,
                                   cv.cout, cv.cout_pad, cv.kpad, cv.ks, stride, pad, 1, 0, fused ? gn : nullptr, sc1,
                                   sh1, sc2, sh2, h2.ovf, st));
     } else {
@@ -637,10 +637,10 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // up1.net.1 feeding down1/down2/up2/up1 .net.3).  The skip tensors h1/h2 (norms 1, 3: read by a
     // 4x4/s2 conv AND an up-path concat) and the 16x16 mid block keep the in-place h2 apply pass.
     if (net->precision == 1) {
-        pro[0] = conv3g_covers(H, W, C, net->down1_1.cout_pad);
-        pro[2] = conv3g_covers(H1, W1, C2, net->down2_1.cout_pad);
-        pro[7] = conv3g_covers(H1, W1, C, net->up2_1.cout_pad);
-        pro[9] = conv3g_covers(H, W, C, net->up1_1.cout_pad);
+        pro[0] = net->down1_1.whf && conv3g_covers(H, W, C, net->down1_1.cout_pad);
+        pro[2] = net->down2_1.whf && conv3g_covers(H1, W1, C2, net->down2_1.cout_pad);
+        pro[7] = net->up2_1.whf && conv3g_covers(H1, W1, C, net->up2_1.cout_pad);
+        pro[9] = net->up1_1.whf && conv3g_covers(H, W, C, net->up1_1.cout_pad);
     }
     auto SC = [&](int i) -> const float* { return pro[i] ? P.sc(i) : nullptr; };
     auto SH = [&](int i) -> const float* { return pro[i] ? P.sh(i) : nullptr; };

@@ -29,7 +29,7 @@ TCX_SAMPLE_X0_HAT = 1  # tcx_{sde,ode}_sample_ex flag: return the unclamped x0_h
 
 class TcxConv(ctypes.Structure):
     _fields_ = [("w", c_fp), ("b", c_fp), ("cin", c_int), ("cout", c_int), ("ks", c_int), ("kpad", c_int),
-                ("cout_pad", c_int), ("wh", c_fp), ("wscale", c_fp)]
+                ("cout_pad", c_int), ("wh", c_fp), ("wscale", c_fp), ("whf", c_fp)]
 
 
 _CONV_NAMES = ["down1_0", "down1_1", "ds1", "down2_0", "down2_1", "ds2", "mid_0", "mid_1", "qkv", "proj", "us2",
@@ -74,8 +74,10 @@ _SIGS = {
     "tcx_conv2d_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp, c_fp,
                               c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
     "tcx_conv2d_h2_pro": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp,
-                                  c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp,
-                                  c_fp, c_fp, c_fp, c_fp, c_fp, c_fp]),
+                                  c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp]),
+    "tcx_conv_weight_h2_frag_bytes": (c_size, [c_int, c_int]),
+    "tcx_pack_conv_weight_h2_frag": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp]),
     "tcx_gn_apply_tab_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp, c_fp]),
     "tcx_upsample2x_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
     "tcx_attention_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),

@@ -153,14 +153,21 @@ class _UNetPack:
             check(L.tcx_pack_conv_weight(w.data_ptr(), wpk.data_ptr(), cout, cin, ks, cpad, kpad, st),
                   "pack conv weight")
             self.keep.extend([w, wpk])
-            wh = whs = None
+            wh = whs = whf = None
             if self.split_ok:
                 wh = torch.empty((cpad, kpad), device=device, dtype=torch.float32)  # h2: 4 B per element
                 whs = torch.empty(4, device=device, dtype=torch.float32)
                 check(L.tcx_pack_conv_weight_h2(wpk.data_ptr(), wh.data_ptr(), whs.data_ptr(), cpad, kpad, st),
                       "pack conv weight h2")
                 self.keep.extend([wh, whs])
-            return TcxConv(wpk.data_ptr(), dev(m.bias), cin, cout, ks, kpad, cpad, ptr(wh), ptr(whs))
+                # fragment-ordered copy for the 3x3 kernel k_conv3g (its B fragments load straight from it)
+                nfb = int(L.tcx_conv_weight_h2_frag_bytes(cpad, cin)) if ks == 3 and kpad == 9 * cin else 0
+                if nfb:
+                    whf = torch.empty(nfb // 4, device=device, dtype=torch.float32)
+                    check(L.tcx_pack_conv_weight_h2_frag(wh.data_ptr(), whf.data_ptr(), cpad, kpad, cin, st),
+                          "pack conv weight h2 frag")
+                    self.keep.append(whf)
+            return TcxConv(wpk.data_ptr(), dev(m.bias), cin, cout, ks, kpad, cpad, ptr(wh), ptr(whs), ptr(whf))
 
         w0 = model.down1.net[0].weight.detach()
         net.down1_0 = conv(model.down1.net[0], w0[:, :1])
