@@ -181,30 +181,49 @@ def test_trained_sde300_vs_reference(golden, prec, monkeypatch):
     weights and draws (tests/golden/make_goldens.py trained96).  98.5 % of the golden image's
     pixels are unsaturated, so the clamped image and x0_hat both see the whole trajectory.
 
-    Discrimination (printed): the same run with one step-table scalar perturbed by 1e-5 relative."""
+    Noise floor: the fp32 reference itself differs from the fp64 trajectory of the same draws by
+    3.0e-5 relative on x0_hat (tests/golden/sde96_trained_300_fp64.npz, make_fp64_floor.py); this
+    path is gated at 1e-4 against BOTH.  A single step-table scalar perturbed by 1e-5 moves x0_hat
+    by at most ~2e-5 (printed), below that floor: no gate can see it.  Discrimination: alpha(t_end)
+    scaled by 1 + 2e-4 (a ~2e-4 change of x0_hat, ~7x the floor) must fail the gate."""
     import toycrystals_amd.models.sde_score_model as S
     from toycrystals_amd.models.sde_score_model import host_noise
     g = golden("sde96_trained_300")
+    f64 = golden("sde96_trained_300_fp64")["x0_fp64"]
     m = unet(96, golden("trained96_ema"))
     B, steps = int(g["B"]), int(g["steps"])
     torch.manual_seed(int(g["noise_seed"]))
     noise = host_noise((B, 1, 64, 64), steps + 1).cuda()
     out, x0 = run_sde(m, g, noise, (B, 1, 64, 64))
     check_sampler_outputs(f"sde96_trained_300 ({prec})", out, x0, g)
+    e64 = rel_err(x0, f64)
+    print(f"  x0_hat rel err vs the fp64 trajectory {e64:.3e} (fp32 reference vs fp64: "
+          f"{rel_err(g['x0_unclamped'], f64):.3e})")
+    assert e64 < 1e-4
     base = S.step_table
+
+    def perturbed_run(row, col, f):
+        def tab_fn(sde, n, t_end):
+            tab = base(sde, n, t_end).clone()
+            tab[row, col] *= 1.0 + f
+            return tab
+
+        monkeypatch.setattr(S, "step_table", tab_fn)
+        try:
+            return run_sde(m, g, noise, (B, 1, 64, 64))[1]
+        finally:
+            monkeypatch.setattr(S, "step_table", base)
+
     for row, col, what in ((steps, 7, "alpha(t_end), final projection"), (steps, 4, "sigma(t_end)"),
                            (steps - 1, 3, "beta, last EM step"), (steps // 2, 3, "beta, step 150"),
                            (0, 4, "sigma(1), first step")):
-        def perturbed(sde, n, t_end, row=row, col=col):
-            tab = base(sde, n, t_end).clone()
-            tab[row, col] *= 1.0 + 1e-5
-            return tab
-
-        monkeypatch.setattr(S, "step_table", perturbed)
-        _, x0p = run_sde(m, g, noise, (B, 1, 64, 64))
+        x0p = perturbed_run(row, col, 1e-5)
         print(f"  {what} x (1 + 1e-5): x0_hat rel err vs reference {rel_err(x0p, g['x0_unclamped']):.3e}, "
               f"vs unperturbed {rel_err(x0p, x0):.3e}")
-    monkeypatch.setattr(S, "step_table", base)
+    x0p = perturbed_run(steps, 7, 2e-4)
+    perr = rel_err(x0p, g["x0_unclamped"])
+    print(f"  alpha(t_end) x (1 + 2e-4): x0_hat rel err vs reference {perr:.3e} (must exceed the 1e-4 gate)")
+    assert perr > 1e-4
 
 
 def test_trained_ode50_vs_reference(golden, prec):

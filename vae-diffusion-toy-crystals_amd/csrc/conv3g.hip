@@ -79,7 +79,9 @@ __device__ __forceinline__ void split8(const float (&v)[8], float4& hi, float4& 
     lo = make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), __uint_as_float(l[2]), __uint_as_float(l[3]));
 }
 
-template <int W, int NW, bool CIRC>
+// PRO: 0 = every source h2; 1 = every source fp32 + GroupNorm table (the transform is branch-free
+// and interleaved with the MFMAs of its tap); 2 = per-source at run time (mixed concat sources)
+template <int W, int NW, bool CIRC, int PRO>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
     constexpr int RT = 2, NT = G_NT, BN = 32 * NT, NTHR = 64 * NW;
     constexpr int TP = g_tp(NW);
@@ -106,14 +108,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
     const int Cin = p.Cin;
     const int cpt = Cin / G_KC;        // chunks (even: Cin % 32 == 0)
     const int nch = 9 * cpt;
-    const bool gn1 = p.sc1 != nullptr, gn2 = p.sc2 != nullptr;
+    const bool gn1 = PRO == 1 || (PRO == 2 && p.sc1 != nullptr);
+    const bool gn2 = PRO == 1 || (PRO == 2 && p.sc2 != nullptr);
 
     const __amdgpu_buffer_rsrc_t r1 = mk_rsrc(p.x1, p.bytes1);
     const __amdgpu_buffer_rsrc_t r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
     const __amdgpu_buffer_rsrc_t rw = mk_rsrc(reinterpret_cast<const float*>(p.wf), p.bytesw);
 
     // ---- GroupNorm tables of this tile's image (concatenated channel order)
-    if (gn1 || gn2) {
+    if (PRO != 0 && (gn1 || gn2)) {
         for (int c = tid; c < Cin; c += NTHR) {
             const bool s1 = c < p.C1;
             const float* sc = s1 ? p.sc1 : p.sc2;
@@ -165,30 +168,34 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
         hv[i][0] = bld4(rs, hoff[i], cc);
         hv[i][1] = bld4(rs, hoff[i], cc + 16);
     };
-    // fp32 source with a GroupNorm table: silu(x*sc+sh) -> h2 (zero padding stays 0); then LDS
-    auto unit_store = [&](int j, int i, int buf) {
-        const int u = tid + NTHR * i;
-        if (!((i + 1) * NTHR <= NU || u < NU)) return;
+    // fp32 source with a GroupNorm table: silu(x*sc+sh) -> h2 in registers (zero padding stays 0)
+    auto unit_transform = [&](int j, int i) {
+        if constexpr (PRO == 0) return;
         __amdgpu_buffer_rsrc_t rs;
         int cc;
-        if (src_of(j, rs, cc)) {
-            const int c = j * G_KC + (u < NPX ? 0 : 8);
-            const float4 s0 = *reinterpret_cast<const float4*>(&Ts[c]);
-            const float4 s1v = *reinterpret_cast<const float4*>(&Ts[c + 4]);
-            const float4 h0 = *reinterpret_cast<const float4*>(&Ts[Cin + c]);
-            const float4 h1 = *reinterpret_cast<const float4*>(&Ts[Cin + c + 4]);
-            float v[8] = {silu_split_src(hv[i][0].x, s0.x, h0.x), silu_split_src(hv[i][0].y, s0.y, h0.y),
-                          silu_split_src(hv[i][0].z, s0.z, h0.z), silu_split_src(hv[i][0].w, s0.w, h0.w),
-                          silu_split_src(hv[i][1].x, s1v.x, h1.x), silu_split_src(hv[i][1].y, s1v.y, h1.y),
-                          silu_split_src(hv[i][1].z, s1v.z, h1.z), silu_split_src(hv[i][1].w, s1v.w, h1.w)};
-            if (!CIRC && hoff[i] == kOOB) {
+        const bool gn = src_of(j, rs, cc);
+        if (PRO == 2 && !gn) return;
+        const int u = tid + NTHR * i;
+        const int c = j * G_KC + (u < NPX ? 0 : 8);
+        const float4 s0 = *reinterpret_cast<const float4*>(&Ts[c]);
+        const float4 s1v = *reinterpret_cast<const float4*>(&Ts[c + 4]);
+        const float4 h0 = *reinterpret_cast<const float4*>(&Ts[Cin + c]);
+        const float4 h1 = *reinterpret_cast<const float4*>(&Ts[Cin + c + 4]);
+        float v[8] = {silu_split_src(hv[i][0].x, s0.x, h0.x), silu_split_src(hv[i][0].y, s0.y, h0.y),
+                      silu_split_src(hv[i][0].z, s0.z, h0.z), silu_split_src(hv[i][0].w, s0.w, h0.w),
+                      silu_split_src(hv[i][1].x, s1v.x, h1.x), silu_split_src(hv[i][1].y, s1v.y, h1.y),
+                      silu_split_src(hv[i][1].z, s1v.z, h1.z), silu_split_src(hv[i][1].w, s1v.w, h1.w)};
+        if (!CIRC && hoff[i] == kOOB) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] = 0.f;
-            }
-            bool bad = false;
-            split8(v, hv[i][0], hv[i][1], bad);
-            h2_flag(p.ovf, bad);
+            for (int k = 0; k < 8; ++k) v[k] = 0.f;
         }
+        bool bad = false;
+        split8(v, hv[i][0], hv[i][1], bad);
+        h2_flag(p.ovf, bad);
+    };
+    auto unit_write = [&](int i, int buf) {
+        const int u = tid + NTHR * i;
+        if (!((i + 1) * NTHR <= NU || u < NU)) return;
         float* d = &Hs[buf * HBUF + (u < NPX ? u * G_PXF : (u - NPX) * G_PXF + 8)];
         *reinterpret_cast<float4*>(d) = hv[i][0];
         *reinterpret_cast<float4*>(d + 4) = hv[i][1];
@@ -235,13 +242,56 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
             acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[rt], b_h[s][n], acc[rt][n], 0, 0, 0);
     };
 
+    // row-block-1 MFMAs of B set s with the GN+SiLU(+split) of halo unit i placed one value per gap
+    auto mf1_transform = [&](int j, int i, int s) {
+        const int u = tid + NTHR * i;
+        const int c = j * G_KC + (u < NPX ? 0 : 8);
+        const float4 s0 = *reinterpret_cast<const float4*>(&Ts[c]);
+        const float4 s1v = *reinterpret_cast<const float4*>(&Ts[c + 4]);
+        const float4 h0 = *reinterpret_cast<const float4*>(&Ts[Cin + c]);
+        const float4 h1 = *reinterpret_cast<const float4*>(&Ts[Cin + c + 4]);
+        const float xs[8] = {hv[i][0].x, hv[i][0].y, hv[i][0].z, hv[i][0].w, hv[i][1].x, hv[i][1].y, hv[i][1].z,
+                             hv[i][1].w};
+        const float scs[8] = {s0.x, s0.y, s0.z, s0.w, s1v.x, s1v.y, s1v.z, s1v.w};
+        const float shs[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        unsigned sp[8];  // (lo << 16) | hi of each value
+        bool bad = false;
+        const bool zero = !CIRC && hoff[i] == kOOB;  // zero padding: the normalised ring is 0
+        const h8* As[3] = {&a_h[1], &a_l[1], &a_h[1]};
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int g = k / 3, n = k - 3 * (k / 3);
+            const h8& bb = g == 0 ? b_l[s][n] : b_h[s][n];
+            acc[1][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*As[g], bb, acc[1][n], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (k < 8) {
+                float v = silu_split_src(xs[k], scs[k], shs[k]);
+                v = zero ? 0.f : v;
+                bad = bad || h2_bad(v);
+                sp[k] = split1(v);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        unsigned h[4], l[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            h[k] = (sp[2 * k] & 0xffffu) | (sp[2 * k + 1] << 16);
+            l[k] = (sp[2 * k] >> 16) | (sp[2 * k + 1] & 0xffff0000u);
+        }
+        hv[i][0] = make_float4(__uint_as_float(h[0]), __uint_as_float(h[1]), __uint_as_float(h[2]), __uint_as_float(h[3]));
+        hv[i][1] = make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), __uint_as_float(l[2]), __uint_as_float(l[3]));
+        h2_flag(p.ovf, bad);
+    };
     // ---- prologue: tables, halo 0 in LDS; B(0) in registers
     if (gn1 || gn2) __syncthreads();  // Ts before the first transform
 #pragma unroll
     for (int i = 0; i < UPT; ++i) unit_load(0, i);
     ld_b(0, 0);
 #pragma unroll
-    for (int i = 0; i < UPT; ++i) unit_store(0, i, 0);
+    for (int i = 0; i < UPT; ++i) {
+        unit_transform(0, i);
+        unit_write(i, 0);
+    }
     __syncthreads();
     rd_a(0, 0, 0);
 
@@ -262,12 +312,23 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
             else rd_a(0, t + 1, hb);
         }
         __builtin_amdgcn_sched_barrier(0);
-        mf(1, s);
+        constexpr bool st = t >= 2 && t < UPT + 2;  // this tap stores halo unit t - 2 of chunk j+1
+        if constexpr (st && PRO == 1) {
+            // GN+SiLU of the unit's 8 values interleaved one per MFMA gap with the row-block-1
+            // MFMAs (~10 VALU per gap, under the ~5 issue slots x 2 waves an MFMA gap hides:
+            // MI355X_MICROARCH.md issue costs), the h2 split after the last one
+            mf1_transform(more ? j + 1 : j, t - 2, s);
+        } else {
+            mf(1, s);
+        }
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
         if constexpr (t < UPT) unit_load(more ? j + 1 : j, t);  // (not stored after the last chunk)
-        if constexpr (t >= 2 && t < UPT + 2) {
-            if (more) unit_store(j + 1, t - 2, hb ^ 1);
+        if constexpr (st) {
+            // unconditional (after the last chunk the other buffer is dead): a branch here lets hipcc
+            // sink the interleaved split of mf1_transform out of the MFMA gaps into it
+            if constexpr (PRO == 2) unit_transform(more ? j + 1 : j, t - 2);
+            unit_write(t - 2, hb ^ 1);
         }
         if (t == 1 || t == 6) __syncthreads();
     };
@@ -327,15 +388,21 @@ template <int W>
 int launch3g(const ConvParams& p, hipStream_t st) {
     constexpr int NW = g_nw(W);
     const size_t shm = conv3g_lds_bytes(W, NW, p.Cin);
-    static bool attr[2] = {false, false};
-    auto kc = p.circular ? &k_conv3g<W, NW, true> : &k_conv3g<W, NW, false>;
-    if (!attr[p.circular ? 1 : 0]) {
+    static bool attr[6] = {false, false, false, false, false, false};
+    const bool has1 = p.sc1 != nullptr, has2 = p.C2 > 0 && p.sc2 != nullptr;
+    const int pro = !has1 && !has2 ? 0 : ((has1 && (p.C2 == 0 || has2)) ? 1 : 2);
+    using K = void (*)(ConvParams);
+    const K ks[6] = {&k_conv3g<W, NW, false, 0>, &k_conv3g<W, NW, false, 1>, &k_conv3g<W, NW, false, 2>,
+                     &k_conv3g<W, NW, true, 0>, &k_conv3g<W, NW, true, 1>, &k_conv3g<W, NW, true, 2>};
+    const int ki = (p.circular ? 3 : 0) + pro;
+    const K kc = ks[ki];
+    if (!attr[ki]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)conv3g_lds_bytes(W, NW, 384)) != hipSuccess) {
             set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3g_lds_bytes(W, NW, 384));
             return TCX_EHIP;
         }
-        attr[p.circular ? 1 : 0] = true;
+        attr[ki] = true;
     }
     const int grid = (p.M / g_tp(NW)) * p.n_nblk;
     hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * NW), shm, st, p);
