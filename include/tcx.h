@@ -321,6 +321,65 @@ int tcx_linear_ws(const float* x1, int K1, const float* x2, int K2, const float*
 int tcx_layernorm_film(const float* x, float* y, int M, int Wd, const float* ln_w,
                        const float* ln_b, const float* gb, int ld_gb, float eps, void* stream);
 
+/* A packed nn.Linear: w = weight [n][k] packed by tcx_pack_conv_weight(ks=1) to [npad][kpad]
+ * (npad >= 16*ceil(n/16), kpad % 4 == 0), b = bias [n]. */
+typedef struct tcx_linear_w {
+    const float* w;
+    const float* b;
+    int n, k, npad, kpad;
+    /* optional f16x3 pack (tcx_pack_linear_h2) or NULL: rows scaled by 1/winv[n], h2 storage */
+    const void* wh;
+    const float* winv;
+} tcx_linear_w;
+
+/* f16x3 pack of an nn.Linear weight [n][k]: each row scaled by an exact power of two (its max |w|
+ * into [2^14, 2^15)), split into h2 storage [ceil16(n)][ceil32(k)/8][2][8] f16 (hi, lo; see the f16x3
+ * section); winv [ceil16(n)] receives the inverse scales.  tcx_linear_h2_bytes gives wh's size. */
+size_t tcx_linear_h2_bytes(int n, int k);
+int tcx_pack_linear_h2(const float* w, int n, int k, void* wh, float* winv, void* stream);
+
+/* DiffusionPriorFiLM (diffusion_prior.py:57-127) as packed device weights.  fc1 / fc2 / norm_w /
+ * norm_b are HOST arrays of n_blocks entries (device pointers inside); cond_all is the n_blocks
+ * FiLM `cond` linears stacked along N ([n_blocks*2W][2W], input [t_feat | y_feat]). */
+typedef struct tcx_prior {
+    int z_dim, n_types, y_cont_dim, t_emb_dim, width, n_blocks, y_cat_emb_dim;
+    float ln_eps;
+    const float* temb_freqs; /* [t_emb_dim/2]: exp(-linspace(0, ln 1e4, half)) (:11-25) */
+    const float* y_cat_emb;  /* [n_types][y_cat_emb_dim] */
+    tcx_linear_w t_mlp0, t_mlp2, y_cont0, y_cont2, y_fuse0, y_fuse2, in_proj, cond_all, out_proj;
+    const tcx_linear_w* fc1;
+    const tcx_linear_w* fc2;
+    const float* const* norm_w;
+    const float* const* norm_b;
+    const float* out_norm_w;
+    const float* out_norm_b;
+} tcx_prior;
+
+/* Diagnostics: copy the skinny-linear kernel's per-workgroup timestamps (written only when the
+ * environment sets TCX_SK_VAR with bit 64): [n][2 waves][5] s_memrealtime ticks (100 MHz) at entry,
+ * after the first k block, after the last MFMA, after the barrier, at exit.  Returns n copied. */
+int tcx_skinny_stamps(unsigned long long* out, int n_workgroups);
+
+/* Scratch bytes for tcx_prior_forward (n_steps = 0) or tcx_prior_ddim_sample (n_steps > 0). */
+size_t tcx_prior_workspace(const tcx_prior* net, int B, int n_steps);
+/* eps_pred = DiffusionPriorFiLM.forward(z_t, t, y_cat, y_cont) (diffusion_prior.py:108-127), eval mode.
+ * B <= 64 runs the skinny path (each weight streamed once, LayerNorm+FiLM fused into the residual
+ * reduce); larger B the tiled GEMMs.  ovf: NULL = fp32 products throughout; a device word (zeroed by
+ * the caller) = fc1 / fc2 / out_proj on f16x3 MFMA when their h2 packs are present and B <= 64,
+ * *ovf != 0 afterwards if an activation left the f16 range (re-run with ovf = NULL). */
+int tcx_prior_forward(const tcx_prior* net, const float* z_t, const int64_t* t, const int64_t* y_cat,
+                      const float* y_cont, int B, float* eps_out, unsigned* ovf, void* ws, size_t ws_bytes,
+                      void* stream);
+/* DiffusionSchedule.ddim_sample, eta = 0 (diffusion_prior.py:203-252): z [B][z_dim] holds x_T on entry
+ * and z0_pred on return.  ts / abar_t / abar_prev are HOST arrays of n_steps entries (the rounded,
+ * de-duplicated timestep grid and alpha_bar at t_i and t_{i+1}).  Loop invariants are hoisted: the
+ * y branch and the y half of every FiLM projection once per call, the t branch and the t half for
+ * all n_steps timesteps in one batched GEMM (the same sums, split over K at the [t_feat | y_feat]
+ * boundary); the DDIM update is fused into the output projection's reduce. */
+int tcx_prior_ddim_sample(const tcx_prior* net, const int64_t* y_cat, const float* y_cont, int B,
+                          const int64_t* ts, const float* abar_t, const float* abar_prev, int n_steps, float* z,
+                          unsigned* ovf, void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------ training path (backward)
  * The reference trains with torch autograd (loss.backward(), scripts/train_*.py); these are the
  * native kernels behind the package's autograd Functions.  Activations NHWC fp32 contiguous. */

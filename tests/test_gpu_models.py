@@ -360,11 +360,16 @@ def test_prior_vs_reference(golden, name, width, stored):
     m = m.cuda().eval()
     eps = m(cu(g["z_t"]), cu(g["t"]), cu(g["y_cat"]), cu(g["y_cont"]))
     assert eps.requires_grad  # autograd training chain
-    assert rel_err(eps.detach().cpu().numpy(), g["eps"]) < 2e-4  # t=999 sinusoid phase ~1e-4 (oracle test)
-    with torch.no_grad():  # fused evaluator
+    e_train = rel_err(eps.detach().cpu().numpy(), g["eps"])
+    with torch.no_grad():  # fused evaluator (skinny-M fp32 MFMA linears at B = 5)
         eps = m(cu(g["z_t"]), cu(g["t"]), cu(g["y_cat"]), cu(g["y_cont"])).cpu().numpy()
-    assert rel_err(eps, g["eps"]) < 2e-4
+    e_eval = rel_err(eps, g["eps"])
     sch = DiffusionSchedule.linear(1000, 1e-4, 0.05, torch.device("cuda"))
     z0 = sch.ddim_sample(m, cu(g["y_cat"]), cu(g["y_cont"]), n_steps=int(g["ddim_steps"]),
                          z_init=cu(g["ddim_z_init"])).cpu().numpy()
-    assert rel_err(z0, g["ddim_z0"]) < 2e-4
+    e_ddim = rel_err(z0, g["ddim_z0"])
+    print(f"{name}: forward (autograd) {e_train:.2e}, forward (fused) {e_eval:.2e}, DDIM-{int(g['ddim_steps'])} "
+          f"{e_ddim:.2e} relative")
+    # the U-Net's gate: the frequency table is the reference's own torch.linspace (diffusion_prior.py:30-35
+    # of the package), so the t = 999 sinusoid matches to rounding
+    assert e_train < 2e-5 and e_eval < 2e-5 and e_ddim < 2e-5

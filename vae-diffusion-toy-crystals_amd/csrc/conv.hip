@@ -764,7 +764,9 @@ extern "C" int tcx_linear(const float* x1, int K1, const float* x2, int K2, cons
     p.x1 = x1; p.x2 = x2; p.C1 = K1; p.C2 = K2; p.Cin = K;
     p.bmod = 0; p.H = 1; p.W = 1; p.Hi = 1; p.Wi = 1; p.Ho = 1; p.Wo = 1; p.HoWo = 1; p.M = M;
     p.w = wpk; p.bias = b; p.bias_b = nullptr; p.resid = resid; p.y = y;
-    p.Cout = N; p.kpad = kpad; p.nchunks = kpad / BK;
+    // chunks cover K only: a caller may pass a column window of a wider packed weight (row stride
+    // kpad, e.g. one half of the prior's FiLM projection), whose columns past K are not padding
+    p.Cout = N; p.kpad = kpad; p.nchunks = cdiv(K, BK);
     p.ks = 1; p.stride = 1; p.pad_y = 0; p.pad_x = 0; p.circular = 0;
     p.Hy = 1; p.Wy = 1; p.osy = 1; p.ooy = 0; p.osx = 1; p.oox = 0; p.act = act; p.gn = nullptr; p.nsplit = 1;
     const bool vec_ok = (K1 % 4 == 0) && (K2 % 4 == 0) && aligned16(x1) && (!x2 || aligned16(x2));

@@ -14,6 +14,7 @@
 // buffering.  Operands whose reduction dimension is not the contiguous one are loaded as float4
 // along the contiguous dimension and transposed on the LDS store.
 #include "common.hpp"
+#include "skinny.hpp"
 
 namespace tcx {
 namespace {
@@ -542,7 +543,7 @@ extern "C" int tcx_gemm_ws(int M, int N, int K, float alpha, const float* A, lon
                      sa_lo, sb_hi, sb_lo, sc_hi, sc_lo, ws, ws_bytes, (hipStream_t)stream);
 }
 
-// ---------------------------------------------------------------- skinny linears (split-K)
+// ---------------------------------------------------------------- linears (split-K / skinny)
 namespace tcx {
 namespace {
 
@@ -577,7 +578,9 @@ bool linear_wants_split(int M, int N, int K1, int K2, const float* x1, const flo
 }  // namespace tcx
 
 extern "C" size_t tcx_linear_workspace(int M, int N, int K1, int K2) {
-    if (M <= 0 || N <= 0 || K1 <= 0 || K2 < 0 || !linear_wants_split(M, N, K1, K2, nullptr, nullptr)) return 0;
+    if (M <= 0 || N <= 0 || K1 <= 0 || K2 < 0) return 0;
+    if (skinny_ok(M, N, K1, K2)) return skinny_part_floats(skinny_plan(K1, K2), M, N) * sizeof(float);
+    if (!linear_wants_split(M, N, K1, K2, nullptr, nullptr)) return 0;
     const LinPlan lp = linear_plan(M, N, K1, K2);
     return (size_t)(lp.s1 + lp.s2) * M * N * sizeof(float);
 }
@@ -587,6 +590,15 @@ extern "C" int tcx_linear_ws(const float* x1, int K1, const float* x2, int K2, c
                              size_t ws_bytes, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const size_t need = tcx_linear_workspace(M, N, K1, K2);
+    if (need > 0 && ws && ws_bytes >= need && skinny_ok(M, N, K1, K2) && aligned16(wpk) && aligned16(x1) &&
+        (!x2 || aligned16(x2)) && kpad % 4 == 0 && npad >= 16 * cdiv(N, 16)) {
+        // M <= 64: each weight streamed once, fixed-order reduce with the epilogue (skinny.hip)
+        TCX_REQUIRE(x1 && y && N > 0 && (K2 == 0) == (x2 == nullptr) && kpad >= K1 + K2 && act >= 0 && act <= 3,
+                    "tcx_linear_ws: bad args");
+        SkEpi e;
+        e.b = b; e.resid = resid; e.act = act; e.y = y;
+        return skinny_linear(x1, K1, K1, x2, K2, K2, wpk, kpad, M, N, static_cast<float*>(ws), e, st);
+    }
     if (need == 0 || !ws || ws_bytes < need || !linear_wants_split(M, N, K1, K2, x1, x2) || !aligned16(wpk))
         return tcx_linear(x1, K1, x2, K2, wpk, b, resid, y, M, N, npad, kpad, act, stream);
     TCX_REQUIRE(x1 && wpk && y && M >= 0 && N > 0 && K1 > 0 && K2 >= 0 && (K2 == 0) == (x2 == nullptr),

@@ -46,6 +46,22 @@ class TcxUnet(ctypes.Structure):
                 + [("precision", c_int), ("h2_ovf", c_fp)])
 
 
+class TcxLinearW(ctypes.Structure):
+    _fields_ = [("w", c_fp), ("b", c_fp), ("n", c_int), ("k", c_int), ("npad", c_int), ("kpad", c_int),
+                ("wh", c_fp), ("winv", c_fp)]
+
+
+class TcxPrior(ctypes.Structure):
+    _fields_ = ([(n, c_int) for n in ("z_dim", "n_types", "y_cont_dim", "t_emb_dim", "width", "n_blocks",
+                                      "y_cat_emb_dim")]
+                + [("ln_eps", c_float), ("temb_freqs", c_fp), ("y_cat_emb", c_fp)]
+                + [(n, TcxLinearW) for n in ("t_mlp0", "t_mlp2", "y_cont0", "y_cont2", "y_fuse0", "y_fuse2",
+                                             "in_proj", "cond_all", "out_proj")]
+                + [("fc1", ctypes.POINTER(TcxLinearW)), ("fc2", ctypes.POINTER(TcxLinearW)),
+                   ("norm_w", ctypes.POINTER(c_fp)), ("norm_b", ctypes.POINTER(c_fp)),
+                   ("out_norm_w", c_fp), ("out_norm_b", c_fp)])
+
+
 class TcxAdamTensor(ctypes.Structure):
     _fields_ = [("p", c_fp), ("g", c_fp), ("m", c_fp), ("v", c_fp), ("n", c_ll)]
 
@@ -104,6 +120,15 @@ _SIGS = {
     "tcx_linear_ws": (c_int, [c_fp, c_int, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp,
                               c_size, c_fp]),
     "tcx_layernorm_film": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_float, c_fp]),
+    "tcx_skinny_stamps": (c_int, [c_fp, c_int]),
+    "tcx_prior_workspace": (c_size, [ctypes.POINTER(TcxPrior), c_int, c_int]),
+    "tcx_prior_forward": (c_int, [ctypes.POINTER(TcxPrior), c_fp, c_fp, c_fp, c_fp, c_int, c_fp, c_fp, c_fp, c_size,
+                                  c_fp]),
+    "tcx_prior_ddim_sample": (c_int, [ctypes.POINTER(TcxPrior), c_fp, c_fp, c_int, ctypes.POINTER(c_ll),
+                                      ctypes.POINTER(c_float), ctypes.POINTER(c_float), c_int, c_fp, c_fp, c_fp,
+                                      c_size, c_fp]),
+    "tcx_linear_h2_bytes": (c_size, [c_int, c_int]),
+    "tcx_pack_linear_h2": (c_int, [c_fp, c_int, c_int, c_fp, c_fp, c_fp]),
     # training path
     "tcx_gemm": (c_int, [c_int, c_int, c_int, c_float, c_fp, c_ll, c_ll, c_fp, c_ll, c_ll, c_float, c_fp, c_ll, c_ll,
                          c_fp, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_fp]),

@@ -1,20 +1,25 @@
 """MI355X-native drop-in for toycrystals.models.diffusion_prior (FiLM-MLP latent prior).
 
 Mirrors /root/reference/src/toycrystals/models/diffusion_prior.py (names, signatures,
-state_dict keys, seeded init).  The forward runs in libtcx as fp32-MFMA GEMMs:
+state_dict keys, seeded init).  The eval forward is ONE native call, tcx_prior_forward
+(csrc/prior.hip), over fp32-MFMA linears:
   t_mlp / y_cont_mlp / y_fuse      Linear+SiLU epilogue, Linear          (:80-104)
   all n_blocks FiLM `cond` linears ONE [B,2W] x [2W, n_blocks*2W] GEMM  (:47, cond shared)
-  per block LN+FiLM (tcx_layernorm_film), fc1+SiLU, fc2 + residual epilogue (:49-54)
+  per block LN+FiLM, fc1+SiLU, fc2 + residual                          (:49-54)
   out LayerNorm, out_proj                                              (:125-126)
-The integer-t sinusoid (:11-25), the y_cat row gather, q_sample and the DDIM update run in
-libtcx kernels too (tcx_prior_temb / tcx_embedding_fwd / tcx_q_sample / tcx_ddim_step).
+At B <= 64 (the DDIM's latents) each weight is streamed once by the skinny kernels
+(csrc/skinny.hip) and every LayerNorm+FiLM is fused into the preceding residual reduce.
+DiffusionSchedule.ddim_sample on this model is ONE native call too (tcx_prior_ddim_sample),
+with the step-invariant y branch and the FiLM projections of all timesteps hoisted out of the loop.
 Training: with autograd on, the same forward runs as a chain of libtcx autograd Functions
 (functional.py): GEMM linears, per-block LayerNorm+FiLM with its fused backward, residual
 added in the fc2 GEMM (beta = 1).
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -22,7 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import functional as TF
-from .._lib import check, lib, ptr, require_gpu_tensor, stream_ptr
+from .._lib import TcxLinearW, TcxPrior, c_fp, c_ll, check, lib, ptr, require_gpu_tensor, stream_ptr
 
 _FREQS = {}
 
@@ -87,14 +92,21 @@ class _PriorPack:
             self.keep.append(t)
             return t
 
-        def lin(w, b):
+        def lin(w, b, h2=False):
+            """packed fp32 weight [npad][kpad]; h2: + the f16x3 pack (tcx_pack_linear_h2, K % 32 == 0)"""
             w = dev(w)
             n, k = w.shape
             npad, kpad = _round_up(n, 32), _round_up(k, 32)
             wpk = torch.empty((npad, kpad), device=device, dtype=torch.float32)
             check(L.tcx_pack_conv_weight(ptr(w), ptr(wpk), n, k, 1, npad, kpad, st), "pack linear")
             self.keep.append(wpk)
-            return (wpk, n, npad, kpad, k, dev(b))
+            wh = winv = None
+            if h2 and k % 32 == 0:
+                wh = torch.empty(int(L.tcx_linear_h2_bytes(n, k)), device=device, dtype=torch.uint8)
+                winv = torch.empty((n + 15) // 16 * 16, device=device, dtype=torch.float32)
+                check(L.tcx_pack_linear_h2(ptr(w), n, k, ptr(wh), ptr(winv), st), "pack linear h2")
+                self.keep += [wh, winv]
+            return (wpk, n, npad, kpad, k, dev(b), wh, winv)
 
         def seq(s):
             return lin(s[0].weight, s[0].bias), lin(s[2].weight, s[2].bias)
@@ -106,24 +118,50 @@ class _PriorPack:
         self.in_proj = lin(m.in_proj.weight, m.in_proj.bias)
         blocks = list(m.blocks)
         self.cond_all = lin(torch.cat([b.cond.weight for b in blocks], 0), torch.cat([b.cond.bias for b in blocks], 0))
-        self.blocks = [(dev(b.norm.weight), dev(b.norm.bias), lin(b.fc1.weight, b.fc1.bias),
-                        lin(b.fc2.weight, b.fc2.bias)) for b in blocks]
+        self.blocks = [(dev(b.norm.weight), dev(b.norm.bias), lin(b.fc1.weight, b.fc1.bias, h2=True),
+                        lin(b.fc2.weight, b.fc2.bias, h2=True)) for b in blocks]
         self.out_norm = (dev(m.out_norm.weight), dev(m.out_norm.bias))
-        self.out_proj = lin(m.out_proj.weight, m.out_proj.bias)
+        self.out_proj = lin(m.out_proj.weight, m.out_proj.bias, h2=True)
+        self.freqs = _temb_freqs(m.t_emb_dim, device)
+        self.net = self._net(m)
+
+    @staticmethod
+    def _lw(packed) -> TcxLinearW:
+        wpk, n, npad, kpad, k, b, wh, winv = packed
+        return TcxLinearW(wpk.data_ptr(), b.data_ptr(), n, k, npad, kpad, ptr(wh), ptr(winv))
+
+    def _net(self, m) -> TcxPrior:
+        nb = len(self.blocks)
+        self.fc1 = (TcxLinearW * nb)(*[self._lw(b[2]) for b in self.blocks])
+        self.fc2 = (TcxLinearW * nb)(*[self._lw(b[3]) for b in self.blocks])
+        self.norm_w = (c_fp * nb)(*[b[0].data_ptr() for b in self.blocks])
+        self.norm_b = (c_fp * nb)(*[b[1].data_ptr() for b in self.blocks])
+        return TcxPrior(
+            z_dim=m.z_dim, n_types=m.n_types, y_cont_dim=m.y_cont_dim, t_emb_dim=m.t_emb_dim, width=m.width,
+            n_blocks=nb, y_cat_emb_dim=self.y_cat_emb.shape[1], ln_eps=float(m.out_norm.eps),
+            temb_freqs=self.freqs.data_ptr(), y_cat_emb=self.y_cat_emb.data_ptr(),
+            t_mlp0=self._lw(self.t_mlp[0]), t_mlp2=self._lw(self.t_mlp[1]), y_cont0=self._lw(self.y_cont_mlp[0]),
+            y_cont2=self._lw(self.y_cont_mlp[1]), y_fuse0=self._lw(self.y_fuse[0]), y_fuse2=self._lw(self.y_fuse[1]),
+            in_proj=self._lw(self.in_proj), cond_all=self._lw(self.cond_all), out_proj=self._lw(self.out_proj),
+            fc1=self.fc1, fc2=self.fc2, norm_w=self.norm_w, norm_b=self.norm_b,
+            out_norm_w=self.out_norm[0].data_ptr(), out_norm_b=self.out_norm[1].data_ptr())
 
 
-def _lin(x1, x2, packed, act, resid=None, out=None):
-    wpk, n, npad, kpad, k, b = packed
-    M, K1 = x1.shape
-    K2 = x2.shape[1] if x2 is not None else 0
-    assert K1 + K2 == k, (K1, K2, k)
-    y = out if out is not None else torch.empty((M, n), device=x1.device, dtype=torch.float32)
-    # skinny batches (DDIM over 36 samples) split K over the chip (tcx_linear_ws scratch)
-    nb = int(lib().tcx_linear_workspace(M, n, K1, K2))
-    ws = TF._ws(x1.device, nb) if nb else None
-    check(lib().tcx_linear_ws(ptr(x1), K1, ptr(x2), K2, ptr(wpk), ptr(b), ptr(resid), ptr(y), M, n, npad, kpad, act,
-                              ptr(ws), nb, stream_ptr(x1.device)), "tcx_linear")
-    return y
+# "f16x3" (default): fc1 / fc2 / out_proj of the native eval forward and DDIM at B <= 64 on split-f16
+# MFMA products (csrc/skinny.hip, ~2^-21 relative per product, fp32 accumulation); "fp32": f32 MFMA.
+PRIOR_PRECISION = os.environ.get("TCX_PRIOR_PRECISION", "f16x3")
+
+
+def _run_h2_or_fp32(run, device) -> None:
+    """run(ovf) with an overflow word for the f16x3 path; if an activation left the f16 range (the
+    word is set; one host read per call) run again in fp32 (ovf = None)."""
+    if PRIOR_PRECISION != "f16x3":
+        run(None)
+        return
+    ovf = torch.zeros(1, dtype=torch.int32, device=device)
+    run(ovf)
+    if int(ovf.item()) != 0:
+        run(None)
 
 
 class DiffusionPriorFiLM(nn.Module):
@@ -183,32 +221,26 @@ class DiffusionPriorFiLM(nn.Module):
         return TF.linear(hn, self.out_proj)
 
     def _forward_eval(self, z_t, t, y_cat, y_cont):
-        pk = self._tcx(z_t.device)
-        st = stream_ptr(z_t.device)
-        W = self.width
-        te = _temb_dev(t, self.t_emb_dim)
-        t_feat = _lin(_lin(te, None, pk.t_mlp[0], act=3), None, pk.t_mlp[1], act=0)
-        yc = _lin(_lin(y_cont.to(torch.float32).contiguous(), None, pk.y_cont_mlp[0], act=3), None,
-                  pk.y_cont_mlp[1], act=0)
-        yci = y_cat.to(torch.int64).contiguous()
-        ycat_feat = torch.empty((yci.shape[0], pk.y_cat_emb.shape[1]), device=z_t.device, dtype=torch.float32)
-        check(lib().tcx_embedding_fwd(ptr(yci), ptr(pk.y_cat_emb), yci.shape[0], pk.y_cat_emb.shape[1],
-                                      ptr(ycat_feat), st), "tcx_embedding_fwd")
-        y_feat = _lin(_lin(ycat_feat, yc, pk.y_fuse[0], act=3), None, pk.y_fuse[1], act=0)
-        gb_all = _lin(t_feat, y_feat, pk.cond_all, act=0)  # [B, n_blocks*2W]
-        h = _lin(z_t.to(torch.float32).contiguous(), None, pk.in_proj, act=0)
-        B = h.shape[0]
-        hn = torch.empty_like(h)
+        """tcx_prior_forward (csrc/prior.hip): the whole eval forward in one native call."""
+        dev = z_t.device
+        pk = self._tcx(dev)
+        B = int(z_t.shape[0])
+        out = torch.empty((B, self.z_dim), device=dev, dtype=torch.float32)
+        if B == 0:
+            return out
+        z = z_t.to(torch.float32).contiguous()
+        tt = t.to(device=dev, dtype=torch.int64).reshape(-1).expand(B).contiguous()
+        yc = y_cat.to(device=dev, dtype=torch.int64).contiguous()
+        yv = y_cont.to(device=dev, dtype=torch.float32).contiguous()
         L = lib()
-        for i, (lw, lb, fc1, fc2) in enumerate(pk.blocks):
-            gb = gb_all[:, i * 2 * W:]
-            check(L.tcx_layernorm_film(ptr(h), ptr(hn), B, W, ptr(lw), ptr(lb), gb.data_ptr(), gb_all.shape[1],
-                                       1e-5, st), "layernorm_film")
-            a = _lin(hn, None, fc1, act=3)
-            h = _lin(a, None, fc2, act=0, resid=h)
-        check(L.tcx_layernorm_film(ptr(h), ptr(hn), B, W, ptr(pk.out_norm[0]), ptr(pk.out_norm[1]), None, 0, 1e-5,
-                                   st), "layernorm")
-        return _lin(hn, None, pk.out_proj, act=0)
+        nb = int(L.tcx_prior_workspace(ctypes.byref(pk.net), B, 0))
+        ws = TF._ws(dev, nb)
+
+        def run(ovf):
+            check(L.tcx_prior_forward(ctypes.byref(pk.net), ptr(z), ptr(tt), ptr(yc), ptr(yv), B, ptr(out), ptr(ovf),
+                                      ptr(ws), nb, stream_ptr(dev)), "tcx_prior_forward")
+        _run_h2_or_fp32(run, dev)
+        return out
 
 
 @dataclass(frozen=True)
@@ -257,6 +289,27 @@ class DiffusionSchedule:
         n = len(ts)
         abar = self.alpha_bars.detach().float().cpu()
         st = stream_ptr(device)
+        if isinstance(model, DiffusionPriorFiLM) and z.is_cuda:
+            if n > 1 and eta != 0.0:
+                raise NotImplementedError("eta != 0 not implemented in this minimal version")
+            # one native call: tcx_prior_ddim_sample (csrc/prior.hip)
+            pk = model._tcx(device)
+            a_t = [float(abar[ts[i]]) for i in range(n)]
+            a_p = [float(abar[ts[i + 1]]) if i + 1 < n else 1.0 for i in range(n)]
+            yci = y_cat.to(device=device, dtype=torch.int64).contiguous()
+            ycv = y_cont.to(device=device, dtype=torch.float32).contiguous()
+            L = lib()
+            nb = int(L.tcx_prior_workspace(ctypes.byref(pk.net), B, n))
+            ws = TF._ws(device, nb)
+            z_init = z.clone()
+
+            def run(ovf):
+                z.copy_(z_init)
+                check(L.tcx_prior_ddim_sample(ctypes.byref(pk.net), ptr(yci), ptr(ycv), B, (c_ll * n)(*ts),
+                                              (ctypes.c_float * n)(*a_t), (ctypes.c_float * n)(*a_p), n, ptr(z),
+                                              ptr(ovf), ptr(ws), nb, st), "tcx_prior_ddim_sample")
+            _run_h2_or_fp32(run, device)
+            return z
         for i in range(n):
             t = torch.full((B,), ts[i], device=device, dtype=torch.int64)
             eps_pred = model(z, t, y_cat, y_cont).contiguous()
