@@ -51,8 +51,9 @@ SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 m
 # FETCH_SIZE x 2 (gfx950 reports half of 16-B/lane reads) + WRITE_SIZE, averaged over the k_conv<>
 # and k_conv3h<> launches of an evaluation.  A counter pass cannot run inside this process, so the
 # measured value is carried here with its source; it applies to the f16x3 path it was taken on.
-TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 500.5e6}
-TRAFFIC_SOURCE = "rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE over the default kernels (k_conv3p, k_conv4s2h, k_conv SPL), profiles/r02_b_pmc_traffic.txt"
+TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 504.0e6}
+TRAFFIC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE over the default kernels (k_conv3g 32/64 with and "
+                  "without the GN+SiLU prologue, k_conv3p 16, k_conv4s2h, k_conv SPL), profiles/r02_x_pmc_traffic.txt")
 
 
 def _cpu_model() -> str:
@@ -227,8 +228,9 @@ def main() -> int:
         args.steps = steps_saved
 
     if args.precision == "f16x3":
-        kname = ("split-path convs: k_conv3p (3x3 halo), k_conv4s2h (4x4/s2 halo), k_conv<SPL> (1x1) — "
-                 "f16x3, 3x v_mfma_f32_32x32x16_f16 per fp32 MAC; all conv launches of the pass")
+        kname = ("split-path convs: k_conv3g (3x3 halo, 32/64-px rows, GN+SiLU prologue), k_conv3p (16-px rows), "
+                 "k_conv4s2h (4x4/s2 halo), k_conv<SPL> (1x1) — f16x3, 3 f16 MFMAs per fp32 MAC; all conv launches "
+                 "of the pass")
         peak = F16_PEAK_TFLOPS / SPLIT_PRODUCTS
         peak_basis = "2500 TFLOP/s dense f16 MFMA / 3 products per fp32 MAC; achieved in fp32-equivalent FLOPs"
     else:

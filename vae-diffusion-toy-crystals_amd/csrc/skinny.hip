@@ -52,8 +52,7 @@ struct SkArgs {
     int kpad, M, N;
     float* part;   // S > 1: partial planes
     int direct;    // S == 1: apply e here
-    int var;       // benchmark knobs (TCX_SK_VAR): 1 rotate K slices, 2/8 skip activation/weight loads, 4 skip MFMA,
-                   // 64 timestamps
+    int var;       // TCX_SK_VAR: bit 1 rotate the K slices (default on), bit 64 timestamps (diagnostics)
     SkEpi e;
 };
 
@@ -83,7 +82,7 @@ __global__ __launch_bounds__(512) void k_skinny(SkArgs a) {
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
         const int kc = min(kw0 + 16 * u, K - 16);
-        wf[u] = *reinterpret_cast<const float4*>(a.var & 8 ? sk_zero4 : wr + kc);
+        wf[u] = *reinterpret_cast<const float4*>(wr + kc);
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
@@ -93,7 +92,7 @@ __global__ __launch_bounds__(512) void k_skinny(SkArgs a) {
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
             const float* xp = a.x + (size_t)min(16 * t + r, a.M - 1) * a.ldx + kc + 4 * q;
-            xf[u][t] = *reinterpret_cast<const float4*>(live && !(a.var & 2) ? xp : sk_zero4);
+            xf[u][t] = *reinterpret_cast<const float4*>(live ? xp : sk_zero4);
         }
     }
     // keep every load above in flight before the first MFMA (left alone, the scheduler trades
@@ -102,12 +101,7 @@ __global__ __launch_bounds__(512) void k_skinny(SkArgs a) {
     f32x4 acc[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (a.var & 4) {  // benchmark knob: loads only
-#pragma unroll
-        for (int u = 0; u < NB; ++u)
-#pragma unroll
-            for (int t = 0; t < MT; ++t) acc[t][0] += xf[u][t].x + wf[u].y;
-    } else {
+    {
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
 #pragma unroll
