@@ -119,7 +119,7 @@ def main() -> int:
     ap.add_argument("--lanes", "--lanes-alt", dest="lanes", type=int, default=3,
                     help="concurrent sampling lanes of the timed region (tcx_set_sample_lanes, 1-4; images are "
                          "bit-identical for every value); the roofline pass after it always runs one lane")
-    ap.add_argument("--precision", choices=["f16x3", "fp32"], default="f16x3",
+    ap.add_argument("--precision", choices=["f16x3", "fp32", "bf16"], default="f16x3",
                     help="conv arithmetic: f16x3 split MFMA (fp32-grade, default) or fp32 MFMA")
     ap.add_argument("--fp32-passes", type=int, default=1,
                     help="with the f16x3 headline: timed one-lane passes of the fp32-MFMA path reported beside it "
@@ -233,6 +233,11 @@ def main() -> int:
                  "of the pass")
         peak = F16_PEAK_TFLOPS / SPLIT_PRODUCTS
         peak_basis = "2500 TFLOP/s dense f16 MFMA / 3 products per fp32 MAC; achieved in fp32-equivalent FLOPs"
+    elif args.precision == "bf16":
+        kname = ("bf16 single-product convs (config 5): k_conv3g, k_conv4s2h, k_conv<SPL=2> — one "
+                 "v_mfma_f32_32x32x16_bf16 per MAC; all conv launches of the pass")
+        peak = F16_PEAK_TFLOPS
+        peak_basis = "2500 TFLOP/s dense bf16 MFMA"
     else:
         kname = "k_conv (fp32-MFMA implicit-GEMM conv, v_mfma_f32_32x32x2_f32)"
         peak = FP32_PEAK_TFLOPS
@@ -253,7 +258,8 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32" if args.precision == "fp32" else "fp32 (f16x3 split MFMA, fp32-grade)",
+        "dtype": {"fp32": "fp32", "bf16": "bf16 (single-product MFMA, fp32 accumulation)"}.get(
+            args.precision, "fp32 (f16x3 split MFMA, fp32-grade)"),
         "data": "synthetic (y_cat=i%4, theta=linspace(0,pi/3,B); random-init weights seed 0; Philox noise)",
         "config": {"workload": f"reverse-SDE {args.n_steps} steps, CFG {args.cfg}, t_end {args.t_end}, "
                                f"CondUNetTiny(base_ch={args.base_ch}) {S}x{S}, batch {B}/GPU",

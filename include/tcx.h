@@ -150,6 +150,18 @@ int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, int H, int W
 size_t tcx_conv_weight_h2_frag_bytes(int cout_pad, int Cin);
 int tcx_pack_conv_weight_h2_frag(const void* wh, void* wf, int cout_pad, int kpad, int Cin, void* stream);
 
+/* ------------------------------------------------------------------ bf16 single-product path
+ * Config 5 (256x256, "bf16 MFMA conv-as-GEMM", BASELINE.json configs[4]): the same record layout as
+ * h2 with bf16 halves (hi = bf16(v), lo = bf16(v - hi)); every product is ONE
+ * v_mfma_f32_32x32x16_bf16 of the hi halves (fp32 accumulation), weights unscaled (*wscale = 1).
+ * The evaluator selects it with tcx_unet.precision = 2; tcx_conv2d_h2_pro with bf16 = 1. */
+int tcx_pack_conv_weight_bf16(const float* wpk, void* wh, float* wscale, int cout_pad, int kpad, void* stream);
+int tcx_gn_apply_tab_bf16(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift,
+                          int silu, void* stream);
+int tcx_upsample2x_bf16(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
+                        const float* shift, void* stream);
+int tcx_attention_split_bf16(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream);
+
 /* tcx_conv2d_h2 with the fragment-ordered weights (wfrag, or NULL) and a GroupNorm+SiLU prologue per
  * source: a source whose pro_scale/pro_shift
  * ([Bt][C] tables from tcx_gn_finalize) are given is read as FP32 and staged as
@@ -164,7 +176,7 @@ int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmod, int H, i
                       const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
                       int stride, int pad, int circular, int act, double* gn_stats,
                       const float* pro_scale1, const float* pro_shift1, const float* pro_scale2,
-                      const float* pro_shift2, unsigned* ovf, void* stream);
+                      const float* pro_shift2, int bf16, unsigned* ovf, void* stream);
 
 /* tcx_gn_apply_tab with the output written as h2 (x == y allowed: in place). */
 int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale,
@@ -228,7 +240,8 @@ typedef struct tcx_unet {
     const float* gn_b[11];
     /* 0: fp32 MFMA convs; 1: f16x3 split convs over h2 activations (needs base_ch % 32 == 0 and
      * every conv's wh/wscale); h2_ovf: device word raised when an activation leaves the f16 range
-     * (the host re-runs the evaluation in fp32) */
+     * (the host re-runs the evaluation in fp32); 2: bf16 single-product convs and attention over bf16
+     * records (wh/whf/wscale then hold the tcx_pack_conv_weight_bf16 packs; (H/4)*(W/4) % 256 == 0) */
     int precision;
     unsigned* h2_ovf;
 } tcx_unet;

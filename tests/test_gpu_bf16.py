@@ -1,0 +1,184 @@
+"""GPU: the bf16 single-product path (config 5's "bf16 MFMA conv-as-GEMM", BASELINE.json configs[4]).
+
+Records hold bf16 halves (hi = bf16(v), lo = bf16(v - hi)); every product is ONE
+v_mfma_f32_32x32x16_bf16 of the hi halves with fp32 accumulation.  Checks:
+  * the writers produce exactly torch's round-to-nearest-even bf16 of the value (hi) and of the
+    residual (lo);
+  * each bf16 kernel (k_conv3g at 32/64/128-pixel rows with and without the GroupNorm+SiLU prologue,
+    the im2col kernel, k_conv4s2h, the split attention) against a float64 reference computed on the
+    SAME bf16-rounded operands: then only the fp32 accumulation differs (5e-6 of the output scale);
+    the attention additionally rounds P and its output to bf16 (1e-2);
+  * the whole U-Net forward at 64² and 256² against the reference's fp32 goldens: bf16 operands
+    carry 8 significant bits, so the stated gate is 3e-2 of the output scale (observed printed).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nn_np
+
+from test_gpu_ops import L, chk, dev, nchw, nhwc, pack, st
+
+pytestmark = pytest.mark.gpu
+
+rng = np.random.default_rng(11)
+
+
+def bf(a):
+    """round to bf16 (nearest even) and back, as torch does on the CPU"""
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16).float().numpy()
+
+
+def to_bf16_records(t):
+    """fp32 NHWC [.., C] -> bf16 records via the GroupNorm-apply writer with scale 1, shift 0, no SiLU"""
+    B = t.shape[0]
+    C = t.shape[-1]
+    HW = t.numel() // (B * C)
+    one = torch.ones(B, C, device="cuda")
+    zero = torch.zeros(B, C, device="cuda")
+    y = torch.empty_like(t)
+    chk(L().tcx_gn_apply_tab_bf16(t.data_ptr(), y.data_ptr(), B, HW, C, one.data_ptr(), zero.data_ptr(), 0, st()))
+    return y
+
+
+def decode(rec):
+    """bf16 records [.., C] -> (hi, lo) float32 arrays [.., C]"""
+    u = rec.contiguous().view(torch.int32).cpu().numpy().view(np.uint16)
+    C = rec.shape[-1]
+    g = u.reshape(-1, C // 8, 2, 8)
+    hi = (g[:, :, 0, :].astype(np.uint32) << 16).view(np.float32).reshape(rec.shape)
+    lo = (g[:, :, 1, :].astype(np.uint32) << 16).view(np.float32).reshape(rec.shape)
+    return hi, lo
+
+
+def test_bf16_writer_is_round_to_nearest_even():
+    v = (rng.standard_normal((2, 8, 8, 32)) * 10.0 ** rng.uniform(-6, 6, (2, 8, 8, 32))).astype(np.float32)
+    hi, lo = decode(to_bf16_records(dev(v)))
+    assert np.array_equal(hi, bf(v))
+    assert np.array_equal(lo, bf(v - bf(v)))
+
+
+def pack_bf16(w):
+    wpk, cpad, kpad = pack(w)
+    wh = torch.empty_like(wpk)
+    ws = torch.empty(4, device="cuda")
+    chk(L().tcx_pack_conv_weight_bf16(wpk.data_ptr(), wh.data_ptr(), ws.data_ptr(), cpad, kpad, st()))
+    return wh, ws, cpad, kpad
+
+
+def pack_frag(wh, cpad, kpad, cin):
+    nb = int(L().tcx_conv_weight_h2_frag_bytes(cpad, cin))
+    if not nb or kpad != 9 * cin:
+        return None
+    wf = torch.empty(nb // 4, device="cuda")
+    chk(L().tcx_pack_conv_weight_h2_frag(wh.data_ptr(), wf.data_ptr(), cpad, kpad, cin, st()))
+    return wf
+
+
+def run_conv_bf16(x, w, b, stride, pad, x2=None, frag=True, tabs=None):
+    """tabs: (scale, shift) [B][C] for a GroupNorm+SiLU prologue on x (fp32 source, k_conv3g only)"""
+    B, C1, H, W = x.shape
+    C2 = 0 if x2 is None else x2.shape[1]
+    co, ci, ks, _ = w.shape
+    wh, ws, cpad, kpad = pack_bf16(w)
+    Ho, Wo = (H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1
+    y = torch.empty((B, Ho, Wo, co), device="cuda")
+    xd = dev(nhwc(x)) if tabs is not None else to_bf16_records(dev(nhwc(x)))
+    x2d = to_bf16_records(dev(nhwc(x2))) if x2 is not None else None
+    wf = pack_frag(wh, cpad, kpad, C1 + C2) if (frag and ks == 3) else None
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    sc, sh = (dev(tabs[0]), dev(tabs[1])) if tabs is not None else (None, None)
+    chk(L().tcx_conv2d_h2_pro(xd.data_ptr(), p(x2d), B, 0, H, W, C1, C2, wh.data_ptr(), p(wf), ws.data_ptr(),
+                              dev(b).data_ptr(), None, None, y.data_ptr(), 0, co, cpad, kpad, ks, stride, pad, 1, 0,
+                              None, p(sc), p(sh), None, None, 1, None, st()))
+    return nchw(y.cpu().numpy())
+
+
+def conv_ref(x, w, b, stride, pad):
+    return nn_np.conv2d(x.astype(np.float64), w.astype(np.float64), b.astype(np.float64), stride, pad,
+                        mode="circular")
+
+
+@pytest.mark.parametrize("B,C1,C2,H,co,ks,stride,frag", [
+    (2, 96, 0, 64, 96, 3, 1, True),      # k_conv3g, 64-px rows
+    (2, 96, 96, 32, 96, 3, 1, True),     # k_conv3g, two sources, 32-px rows
+    (1, 96, 0, 128, 96, 3, 1, True),     # k_conv3g, 128-px rows
+    (2, 64, 0, 16, 64, 3, 1, True),      # 16-px rows: the im2col kernel (no bf16 k_conv3p)
+    (2, 96, 0, 64, 96, 4, 2, False),     # k_conv4s2h (ds1 at 64 -> 32)
+    (2, 192, 0, 16, 576, 1, 1, False),   # 1x1 (qkv): the im2col kernel
+])
+def test_bf16_convs_vs_float64_on_rounded_operands(B, C1, C2, H, co, ks, stride, frag):
+    pad = 1 if ks in (3, 4) else 0
+    x = rng.standard_normal((B, C1, H, H)).astype(np.float32)
+    x2 = rng.standard_normal((B, C2, H, H)).astype(np.float32) if C2 else None
+    w = (rng.standard_normal((co, C1 + C2, ks, ks)) / np.sqrt((C1 + C2) * ks * ks)).astype(np.float32)
+    b = rng.standard_normal(co).astype(np.float32)
+    y = run_conv_bf16(x, w, b, stride, pad, x2=x2, frag=frag)
+    xin = bf(x) if x2 is None else np.concatenate([bf(x), bf(x2)], axis=1)
+    ref = conv_ref(xin, bf(w), b, stride, pad)
+    err = float(np.abs(y - ref).max()) / max(1.0, float(np.abs(ref).max()))
+    print(f"bf16 conv B={B} C={C1}+{C2} {H}² co={co} k={ks} s={stride}: {err:.2e} vs float64 on bf16 operands")
+    assert err < 5e-6
+
+
+def test_bf16_conv3g_gn_prologue_vs_float64():
+    """the prologue applies silu(x*scale+shift) in fp32 and rounds the result to bf16 in registers"""
+    B, C, H = 2, 96, 64
+    x = rng.standard_normal((B, C, H, H)).astype(np.float32)
+    sc = (0.5 + rng.random((B, C))).astype(np.float32)
+    sh = rng.standard_normal((B, C)).astype(np.float32) * 0.2
+    w = (rng.standard_normal((C, C, 3, 3)) / np.sqrt(9 * C)).astype(np.float32)
+    b = rng.standard_normal(C).astype(np.float32)
+    y = run_conv_bf16(x, w, b, 1, 1, tabs=(sc, sh))
+    z = x * sc[:, :, None, None] + sh[:, :, None, None]
+    a = z / (1.0 + np.exp(-z.astype(np.float64)))
+    ref = conv_ref(bf(a.astype(np.float32)), bf(w), b, 1, 1)
+    err = float(np.abs(y - ref).max()) / max(1.0, float(np.abs(ref).max()))
+    print(f"bf16 conv3g with the GN+SiLU prologue: {err:.2e}")
+    # the kernel's SiLU (hardware exp2 / rcp) may round to the neighbouring bf16 value: 2^-8 of one input
+    assert err < 2e-3
+
+
+def test_bf16_attention_split_vs_float64():
+    Bt, N, C, heads = 2, 256, 192, 4
+    D = C // heads
+    qkv = (rng.standard_normal((Bt, N, 3 * C)) * 0.5).astype(np.float32)
+    rec = to_bf16_records(dev(qkv))
+    out = torch.empty(Bt, N, C, device="cuda")
+    chk(L().tcx_attention_split_bf16(rec.data_ptr(), out.data_ptr(), Bt, N, C, heads, st()))
+    hi, _ = decode(out)
+    qb = bf(qkv).astype(np.float64)
+    q, k, v = qb[..., :C], qb[..., C:2 * C], qb[..., 2 * C:]
+    ref = np.empty((Bt, N, C))
+    for b in range(Bt):
+        for h in range(heads):
+            sl = slice(h * D, (h + 1) * D)
+            s = q[b, :, sl] @ k[b, :, sl].T / np.sqrt(D)
+            p = np.exp(s - s.max(1, keepdims=True))
+            ref[b, :, sl] = (p / p.sum(1, keepdims=True)) @ v[b, :, sl]
+    err = float(np.abs(hi - ref).max()) / max(1.0, float(np.abs(ref).max()))
+    print(f"bf16 split attention (P rounded to bf16, output as bf16): {err:.2e}")
+    assert err < 1e-2
+
+
+@pytest.mark.parametrize("name", ["unet96_b2", "unet96_b2_h256"])
+def test_bf16_unet_forward_vs_reference(golden, name):
+    """the whole evaluator in bf16 against the reference's fp32 forward: stated gate 3e-2 of the scale"""
+    from toycrystals_amd import _lib
+    from test_gpu_models import cu, rel_err, unet
+    g = golden(name)
+    m = unet(96)
+    old = _lib.conv_precision()
+    try:
+        _lib.set_conv_precision("bf16")
+        with torch.no_grad():
+            e_bf = m(cu(g["x_t"]), cu(g["t"]), cu(g["y_cat"]), cu(g["y_cont"])).cpu().numpy()
+        _lib.set_conv_precision("f16x3")
+        with torch.no_grad():
+            e_h2 = m(cu(g["x_t"]), cu(g["t"]), cu(g["y_cat"]), cu(g["y_cont"])).cpu().numpy()
+    finally:
+        _lib.set_conv_precision(old)
+    e1, e2 = rel_err(e_bf, g["eps"]), rel_err(e_h2, g["eps"])
+    print(f"{name}: bf16 {e1:.2e}, f16x3 {e2:.2e} of the output scale vs the reference fp32 forward")
+    assert e2 < 2e-5
+    assert e1 < 3e-2 and e1 > 10 * e2  # really the bf16 path (8-bit operands), within its gate

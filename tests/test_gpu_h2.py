@@ -91,7 +91,7 @@ def run_conv_h2(x, w, b, stride, pad, circular, x2=None, act=0, resid=None, bmod
                               bd.data_ptr() if bd is not None else None, None,
                               rd.data_ptr() if rd is not None else None, y.data_ptr(), int(out_h2), co, cpad, kpad, ks,
                               stride, pad, int(circular), act, gnd.data_ptr() if gnd is not None else None,
-                              None, None, None, None, ovf.data_ptr(), st()))
+                              None, None, None, None, 0, ovf.data_ptr(), st()))
     if out_h2:
         y = from_h2(y)
     torch.cuda.synchronize()
@@ -153,7 +153,8 @@ def run_conv_h2_pro(x, w, b, circular, tabs, x2=None, tabs2=None, gn=False, out_
     wf = pack_frag(wh, cpad, kpad, C1 + C2)
     chk(L().tcx_conv2d_h2_pro(xd.data_ptr(), p(x2d), B, 0, H, W, C1, C2, wh.data_ptr(), p(wf), ws.data_ptr(),
                               dev(b).data_ptr(), None, None, y.data_ptr(), int(out_h2), co, cpad, kpad, 3, 1, 1,
-                              int(circular), 0, p(gnd), p(tb[0]), p(tb[1]), p(tb2[0]), p(tb2[1]), ovf.data_ptr(), st()))
+                              int(circular), 0, p(gnd), p(tb[0]), p(tb[1]), p(tb2[0]), p(tb2[1]), 0, ovf.data_ptr(),
+                              st()))
     if out_h2:
         y = from_h2(y)
     torch.cuda.synchronize()

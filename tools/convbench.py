@@ -72,7 +72,7 @@ def bench(name, H, C1, C2, Co, ks, s, pad, ups, reps=20, gn=True):
             check(L.tcx_conv2d_h2_pro(x1.data_ptr(), x2.data_ptr() if x2 is not None else None, Bt, 0, H, H, C1, C2,
                                       wh.data_ptr(), wfp, ws.data_ptr(), b.data_ptr(), None, None, y.data_ptr(), 0, Co,
                                       cpad, kpad, ks, s, pad, 1, 0, g.data_ptr() if g is not None else None, hp[0],
-                                      hp[1], None, None, None, st))
+                                      hp[1], None, None, 0, None, st))
     else:
       def run():
         check(L.tcx_conv2d(x1.data_ptr(), x2.data_ptr() if x2 is not None else None, Bt, 0, H, H, C1, C2,

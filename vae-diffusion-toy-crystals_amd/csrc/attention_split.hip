@@ -81,7 +81,8 @@ _Pragma("unroll") \
         } \
     } while (0)
 
-template <int D>
+// BF: bf16 records (h2.hpp), one v_mfma_f32_32x32x16_bf16 (hi x hi) per product, P in bf16
+template <int D, bool BF>
 __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict__ qkv, char* __restrict__ out, int N,
                                                          int C, float scale) {
     static_assert(D % 16 == 0 && D <= 64, "split attention: head dim multiple of 16, <= 64");
@@ -154,6 +155,11 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
 #pragma unroll
             for (int s = 0; s < DS; ++s) {
                 const h8 kh = *reinterpret_cast<const h8*>(kr + (2 * s + lh) * 32);
+                if constexpr (BF) {
+                    sacc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, kh),
+                                                                      __builtin_bit_cast(bf8, qh[s]), sacc[n], 0, 0, 0);
+                    continue;
+                }
                 const h8 kl = *reinterpret_cast<const h8*>(kr + (2 * s + lh) * 32 + 16);
                 sacc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[s], sacc[n], 0, 0, 0);
                 sacc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[s], sacc[n], 0, 0, 0);
@@ -182,6 +188,23 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
         for (int n = 0; n < NST; ++n) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
+                const int c0 = (n * 32 + 16 * s + 8 * lh) >> 1;
+                if constexpr (BF) {
+                    bf8 pb;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float v = __builtin_amdgcn_exp2f(fmaf(sacc[n][8 * s + e], scale2, mb));
+                        lt += v;
+                        pb[e] = (__bf16)v;
+                    }
+#pragma unroll
+                    for (int t = 0; t < DT; ++t) {
+                        const h8 vh = *reinterpret_cast<const h8*>(&Vh[(t * 32 + li) * VSW + c0]);
+                        oacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, vh), pb, oacc[t], 0,
+                                                                          0, 0);
+                    }
+                    continue;
+                }
                 h8 ph, pl;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
@@ -191,7 +214,6 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
                     ph[e] = hh;
                     pl[e] = (_Float16)(v - (float)hh);
                 }
-                const int c0 = (n * 32 + 16 * s + 8 * lh) >> 1;
 #pragma unroll
                 for (int t = 0; t < DT; ++t) {
                     const h8 vh = *reinterpret_cast<const h8*>(&Vh[(t * 32 + li) * VSW + c0]);
@@ -216,26 +238,26 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
             if (d < D) {
                 const float4 v = make_float4(oacc[t][4 * i] * inv, oacc[t][4 * i + 1] * inv, oacc[t][4 * i + 2] * inv,
                                              oacc[t][4 * i + 3] * inv);
-                store4_h2(out, ((size_t)b * N + q) * C * 4, (h * D + d) >> 2, v);
+                store4_h2x(out, ((size_t)b * N + q) * C * 4, (h * D + d) >> 2, v, BF);
             }
         }
 }
 
-template <int D>
+template <int D, bool BF>
 int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
     const float scale = (float)(1.0 / std::sqrt((double)D));
     constexpr int DP = (D + 31) / 32 * 32;
     constexpr size_t shm = 2 * ((size_t)128 * (D * 4 + 16) + 2 * (size_t)DP * (128 / 2 + 4) * 4);
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D, BF>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) {
             set_error("tcx_attention_split: cannot enable %zu B of dynamic LDS", shm);
             return TCX_EHIP;
         }
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_attention_split<D>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
+    hipLaunchKernelGGL((k_attention_split<D, BF>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
                        (char*)out, N, C, scale);
     return check_launch("tcx_attention_split");
 }
@@ -248,19 +270,33 @@ int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hi
 
 using namespace tcx;
 
-extern "C" int tcx_attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream) {
+namespace tcx {
+int attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads, int bf, hipStream_t st) {
     TCX_REQUIRE(qkv && out && heads > 0 && C % heads == 0, "tcx_attention_split: bad args");
     TCX_REQUIRE(N > 0 && N % 256 == 0, "tcx_attention_split: needs N %% 256 == 0");
     TCX_REQUIRE(aligned16(qkv) && aligned16(out), "tcx_attention_split: pointers must be 16-B aligned");
     if (Bt == 0) return TCX_OK;
-    hipStream_t st = (hipStream_t)stream;
+#define TCX_ATT_D(D_)                                                                        \
+    case D_:                                                                                 \
+        return bf ? launch_split<D_, true>(qkv, out, Bt, N, C, heads, st)                   \
+                  : launch_split<D_, false>(qkv, out, Bt, N, C, heads, st);
     switch (C / heads) {
-        case 16: return launch_split<16>(qkv, out, Bt, N, C, heads, st);
-        case 32: return launch_split<32>(qkv, out, Bt, N, C, heads, st);
-        case 48: return launch_split<48>(qkv, out, Bt, N, C, heads, st);
-        case 64: return launch_split<64>(qkv, out, Bt, N, C, heads, st);
+        TCX_ATT_D(16)
+        TCX_ATT_D(32)
+        TCX_ATT_D(48)
+        TCX_ATT_D(64)
         default:
             set_error("tcx_attention_split: head dim %d unsupported (16, 32, 48, 64)", C / heads);
             return TCX_EUNSUP;
     }
+#undef TCX_ATT_D
+}
+}  // namespace tcx
+
+extern "C" int tcx_attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream) {
+    return attention_split(qkv, out, Bt, N, C, heads, 0, (hipStream_t)stream);
+}
+
+extern "C" int tcx_attention_split_bf16(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream) {
+    return attention_split(qkv, out, Bt, N, C, heads, 1, (hipStream_t)stream);
 }

@@ -33,7 +33,7 @@ namespace {
 // SPL: the f16x3 split path (h2.hpp): MODE 3 staging unchanged (4 bytes per element either
 //      way); per 32-deep chunk two k16 steps, lane half h of step s owns the 8-channel group
 //      2s + h = one hi and one lo b128 read per operand; 3 MFMA 32x32x16 f16 per accumulator.
-template <int NT, int MODE, bool CIRC, bool PRO, bool SPL = false>
+template <int NT, int MODE, bool CIRC, bool PRO, int SPL = 0>  // SPL: 0 fp32, 1 f16x3, 2 bf16 (one product)
 __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     static_assert(!SPL || (MODE == 3 && !PRO), "split path: MODE 3 staging only, no prologue");
     constexpr int BN = 32 * NT;
@@ -321,6 +321,13 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
             }
         };
         auto mf = [&](const h8& ah, const h8& al, const h8 (&bh)[NT], const h8 (&bl)[NT]) {
+            if constexpr (SPL == 2) {  // bf16: hi x hi only
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, ah),
+                                                                     __builtin_bit_cast(bf8, bh[n]), acc[n], 0, 0, 0);
+                return;
+            }
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[n], acc[n], 0, 0, 0);
 #pragma unroll
@@ -423,7 +430,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     }
     }  // !SPL
 
-    conv_epilogue<NT, SPL, 4>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(&As[0][0]));
+    conv_epilogue<NT, (SPL != 0), 4>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(&As[0][0]));
 }
 
 template <int NT>
@@ -435,9 +442,14 @@ int launch_nt(const ConvParams& p, int mode, hipStream_t st) {
                      p.ks * p.ks <= MAXTAP && p.kpad == p.ks * p.ks * p.Cin && p.Hi == p.H && p.Wi == p.W &&
                      p.bytes1 && (p.C2 == 0 || p.bytes2) && p.bytesw;
     const bool pro = p.sc1 || p.sc2;
-    if (p.wscale) {  // f16x3 split path, validated by the caller: uni
-        if (p.circular) hipLaunchKernelGGL((k_conv<NT, 3, true, false, true>), grid, block, 0, st, p);
-        else hipLaunchKernelGGL((k_conv<NT, 3, false, false, true>), grid, block, 0, st, p);
+    if (p.wscale) {  // split path (f16x3, or bf16 single product), validated by the caller: uni
+        if (p.bf) {
+            if (p.circular) hipLaunchKernelGGL((k_conv<NT, 3, true, false, 2>), grid, block, 0, st, p);
+            else hipLaunchKernelGGL((k_conv<NT, 3, false, false, 2>), grid, block, 0, st, p);
+        } else {
+            if (p.circular) hipLaunchKernelGGL((k_conv<NT, 3, true, false, 1>), grid, block, 0, st, p);
+            else hipLaunchKernelGGL((k_conv<NT, 3, false, false, 1>), grid, block, 0, st, p);
+        }
         return check_launch("tcx_conv2d_h2");
     }
     if (pro) {  // validated by the caller: uni && circular
@@ -532,8 +544,9 @@ __global__ void k_pack_conv_dgrad(const float* __restrict__ w, float* __restrict
 // fp32 packed weight [cout_pad][kpad] -> h2 split [cout_pad][kpad/8][2][8] f16 of w * 2^e, with
 // e chosen from max|w| so the largest scaled weight lies in [2^13, 2^14) (lo halves normal);
 // *wscale = 2^-e.  One workgroup: max-reduce, then split.
+// bf != 0: the bf16 single-product form — unscaled (bf16 has the fp32 range), *wscale = 1.
 __global__ __launch_bounds__(1024) void k_pack_h2(const float* __restrict__ wpk, char* __restrict__ wh,
-                                                  float* __restrict__ wscale, size_t n) {
+                                                  float* __restrict__ wscale, size_t n, int bf) {
     __shared__ float red[16];
     const int tid = threadIdx.x;
     float m = 0.f;
@@ -546,7 +559,7 @@ __global__ __launch_bounds__(1024) void k_pack_h2(const float* __restrict__ wpk,
         for (int w = 0; w < 16; ++w) mx = fmaxf(mx, red[w]);
         int k = 0;
         if (mx > 0.f && mx < INFINITY) (void)frexpf(mx, &k);  // mx < 2^k
-        int e = 14 - k;
+        int e = bf ? 0 : 14 - k;
         e = e < -100 ? -100 : (e > 100 ? 100 : e);
         red[0] = ldexpf(1.f, e);
         wscale[0] = ldexpf(1.f, -e);
@@ -556,7 +569,7 @@ __global__ __launch_bounds__(1024) void k_pack_h2(const float* __restrict__ wpk,
     for (size_t g = tid; g < n / 4; g += 1024) {
         float4 v = reinterpret_cast<const float4*>(wpk)[g];
         v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
-        store4_h2(wh, (g >> 1) * 32, (int)(g & 1), v);
+        store4_h2x(wh, (g >> 1) * 32, (int)(g & 1), v, bf != 0);
     }
 }
 
@@ -570,8 +583,17 @@ extern "C" int tcx_pack_conv_weight_h2(const float* wpk, void* wh, float* wscale
     TCX_REQUIRE(wpk && wh && wscale && cout_pad > 0 && kpad > 0 && kpad % BK == 0 && aligned16(wpk) && aligned16(wh),
                 "tcx_pack_conv_weight_h2: bad args");
     hipLaunchKernelGGL(k_pack_h2, dim3(1), dim3(1024), 0, (hipStream_t)stream, wpk, (char*)wh, wscale,
-                       (size_t)cout_pad * kpad);
+                       (size_t)cout_pad * kpad, 0);
     return check_launch("tcx_pack_conv_weight_h2");
+}
+
+extern "C" int tcx_pack_conv_weight_bf16(const float* wpk, void* wh, float* wscale, int cout_pad, int kpad,
+                                         void* stream) {
+    TCX_REQUIRE(wpk && wh && wscale && cout_pad > 0 && kpad > 0 && kpad % BK == 0 && aligned16(wpk) && aligned16(wh),
+                "tcx_pack_conv_weight_bf16: bad args");
+    hipLaunchKernelGGL(k_pack_h2, dim3(1), dim3(1024), 0, (hipStream_t)stream, wpk, (char*)wh, wscale,
+                       (size_t)cout_pad * kpad, 1);
+    return check_launch("tcx_pack_conv_weight_bf16");
 }
 
 extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
@@ -580,7 +602,7 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
                                  const float* resid, void* y, int out_h2, int Cout, int cout_pad, int kpad, int ks,
                                  int stride, int pad, int circular, int act, double* gn_stats, const float* pro_scale1,
                                  const float* pro_shift1, const float* pro_scale2, const float* pro_shift2,
-                                 unsigned* ovf, void* stream) {
+                                 int bf16, unsigned* ovf, void* stream) {
     TCX_REQUIRE(x1 && wh && wscale && y, "tcx_conv2d_h2: null pointer");
     TCX_REQUIRE(Bt >= 0 && H > 0 && W > 0 && C1 > 0 && C2 >= 0 && Cout > 0, "tcx_conv2d_h2: bad shape");
     TCX_REQUIRE((C2 == 0) == (x2 == nullptr), "tcx_conv2d_h2: x2/C2 mismatch");
@@ -617,12 +639,13 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
                 "tcx_conv2d_h2: prologue tables come in scale/shift pairs per source");
     p.sc1 = pro_scale1; p.sh1 = pro_shift1; p.sc2 = pro_scale2; p.sh2 = pro_shift2;
     p.wf = wfrag;
+    p.bf = bf16 != 0;  // k_conv3p / k_conv3h have no bf16 form: those shapes take the im2col kernel
     if (conv3g_applies(p, cout_pad)) return launch_conv3g(p, cout_pad, (hipStream_t)stream);
     TCX_REQUIRE(!pro_scale1 && !pro_scale2,
                 "tcx_conv2d_h2: the GroupNorm+SiLU prologue needs k_conv3g: the fragment-ordered weights "
                 "(tcx_pack_conv_weight_h2_frag) and a 3x3 stride-1 conv with W in {32, 64, 128}, Cin %% 32 == 0, "
                 "Cin <= 384, Cout padded to 96k");
-    if (conv3h_applies(p, cout_pad)) return launch_conv3h(p, cout_pad, (hipStream_t)stream);
+    if (!p.bf && conv3h_applies(p, cout_pad)) return launch_conv3h(p, cout_pad, (hipStream_t)stream);
     if (conv4s2h_applies(p, cout_pad)) return launch_conv4s2h(p, cout_pad, (hipStream_t)stream);
     return launch_conv(p, cout_pad, 0, (hipStream_t)stream);
 }
@@ -634,7 +657,7 @@ extern "C" int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, i
                              void* stream) {
     return tcx_conv2d_h2_pro(x1, x2, Bt, bmod, H, W, C1, C2, wh, nullptr, wscale, bias, bias_b, resid, y, out_h2, Cout,
                              cout_pad, kpad, ks, stride, pad, circular, act, gn_stats, nullptr, nullptr, nullptr,
-                             nullptr, ovf, stream);
+                             nullptr, 0, ovf, stream);
 }
 
 extern "C" int tcx_conv2d(const float* x1, const float* x2, int Bt, int bmod, int H, int W, int C1, int C2,

@@ -65,23 +65,26 @@ __device__ __forceinline__ float silu_split_src(float v, float sc, float sh) {
     return y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * y));
 }
 
-// 8 fp32 values -> h2 unit: hi halves (16 B) and lo halves (16 B)
+// 8 fp32 values -> h2 unit: hi halves (16 B) and lo halves (16 B); BF: bf16 halves (no range limit)
+template <bool BF>
 __device__ __forceinline__ void split8(const float (&v)[8], float4& hi, float4& lo, bool& bad) {
     unsigned h[4], l[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const unsigned a = split1(v[2 * k]), b = split1(v[2 * k + 1]);
+        const unsigned a = BF ? split1_bf(v[2 * k]) : split1(v[2 * k]);
+        const unsigned b = BF ? split1_bf(v[2 * k + 1]) : split1(v[2 * k + 1]);
         h[k] = (a & 0xffffu) | (b << 16);
         l[k] = (a >> 16) | (b & 0xffff0000u);
-        bad = bad || h2_bad(v[2 * k]) || h2_bad(v[2 * k + 1]);
+        if (!BF) bad = bad || h2_bad(v[2 * k]) || h2_bad(v[2 * k + 1]);
     }
     hi = make_float4(__uint_as_float(h[0]), __uint_as_float(h[1]), __uint_as_float(h[2]), __uint_as_float(h[3]));
     lo = make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), __uint_as_float(l[2]), __uint_as_float(l[3]));
 }
 
 // PRO: 0 = every source h2; 1 = every source fp32 + GroupNorm table (the transform is branch-free
-// and interleaved with the MFMAs of its tap); 2 = per-source at run time (mixed concat sources)
-template <int W, int NW, bool CIRC, int PRO>
+// and interleaved with the MFMAs of its tap); 2 = per-source at run time (mixed concat sources).
+// BF: bf16 records and weights, one v_mfma_f32_32x32x16_bf16 (hi x hi) per product.
+template <int W, int NW, bool CIRC, int PRO, bool BF>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
     constexpr int RT = 2, NT = G_NT, BN = 32 * NT, NTHR = 64 * NW;
     constexpr int TP = g_tp(NW);
@@ -190,8 +193,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
             for (int k = 0; k < 8; ++k) v[k] = 0.f;
         }
         bool bad = false;
-        split8(v, hv[i][0], hv[i][1], bad);
-        h2_flag(p.ovf, bad);
+        split8<BF>(v, hv[i][0], hv[i][1], bad);
+        if (!BF) h2_flag(p.ovf, bad);
     };
     auto unit_write = [&](int i, int buf) {
         const int u = tid + NTHR * i;
@@ -231,6 +234,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
         }
     };
     auto mf = [&](int rt, int s) {
+        if constexpr (BF) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, a_h[rt]),
+                                                                     __builtin_bit_cast(bf8, b_h[s][n]), acc[rt][n], 0,
+                                                                     0, 0);
+            return;
+        }
 #pragma unroll
         for (int n = 0; n < NT; ++n)
             acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[rt], b_l[s][n], acc[rt][n], 0, 0, 0);
@@ -244,6 +255,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
 
     // row-block-1 MFMAs of B set s with the GN+SiLU(+split) of halo unit i placed one value per gap
     auto mf1_transform = [&](int j, int i, int s) {
+        if constexpr (BF) {  // one MFMA per n: the transform is not interleaved
+            mf(1, s);
+            unit_transform(j, i);
+            return;
+        }
         const int u = tid + NTHR * i;
         const int c = j * G_KC + (u < NPX ? 0 : 8);
         const float4 s0 = *reinterpret_cast<const float4*>(&Ts[c]);
@@ -388,13 +404,17 @@ template <int W>
 int launch3g(const ConvParams& p, hipStream_t st) {
     constexpr int NW = g_nw(W);
     const size_t shm = conv3g_lds_bytes(W, NW, p.Cin);
-    static bool attr[6] = {false, false, false, false, false, false};
+    static bool attr[12] = {};
     const bool has1 = p.sc1 != nullptr, has2 = p.C2 > 0 && p.sc2 != nullptr;
     const int pro = !has1 && !has2 ? 0 : ((has1 && (p.C2 == 0 || has2)) ? 1 : 2);
     using K = void (*)(ConvParams);
-    const K ks[6] = {&k_conv3g<W, NW, false, 0>, &k_conv3g<W, NW, false, 1>, &k_conv3g<W, NW, false, 2>,
-                     &k_conv3g<W, NW, true, 0>, &k_conv3g<W, NW, true, 1>, &k_conv3g<W, NW, true, 2>};
-    const int ki = (p.circular ? 3 : 0) + pro;
+    const K ks[12] = {&k_conv3g<W, NW, false, 0, false>, &k_conv3g<W, NW, false, 1, false>,
+                      &k_conv3g<W, NW, false, 2, false>, &k_conv3g<W, NW, true, 0, false>,
+                      &k_conv3g<W, NW, true, 1, false>,  &k_conv3g<W, NW, true, 2, false>,
+                      &k_conv3g<W, NW, false, 0, true>,  &k_conv3g<W, NW, false, 1, true>,
+                      &k_conv3g<W, NW, false, 2, true>,  &k_conv3g<W, NW, true, 0, true>,
+                      &k_conv3g<W, NW, true, 1, true>,   &k_conv3g<W, NW, true, 2, true>};
+    const int ki = (p.bf ? 6 : 0) + (p.circular ? 3 : 0) + pro;
     const K kc = ks[ki];
     if (!attr[ki]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -33,7 +33,7 @@ constexpr size_t ds_lds_bytes(int Wo) {
     return ((size_t)ds_halo_px(Wo) * DS_HROW + 2 * 96 * DS_WROW) * sizeof(float);
 }
 
-template <int Wo, bool CIRC>
+template <int Wo, bool CIRC, bool BF>  // BF: bf16 records, one product (h2.hpp)
 __global__ __launch_bounds__(256, 2) void k_conv4s2h(ConvParams p) {
     constexpr int NT = 3;
     constexpr int NTHR = 64 * DS_NW;
@@ -154,6 +154,13 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2h(ConvParams p) {
             }
     };
     auto mf = [&](int k) {
+        if constexpr (BF) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, a_h[k]),
+                                                                 __builtin_bit_cast(bf8, b_h[k][n]), acc[n], 0, 0, 0);
+            return;
+        }
 #pragma unroll
         for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[k], b_l[k][n], acc[n], 0, 0, 0);
 #pragma unroll
@@ -205,15 +212,17 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2h(ConvParams p) {
 template <int Wo>
 int launch_ds(const ConvParams& p, hipStream_t st) {
     constexpr size_t shm = ds_lds_bytes(Wo);
-    static bool attr[2] = {false, false};
-    auto kc = p.circular ? &k_conv4s2h<Wo, true> : &k_conv4s2h<Wo, false>;
-    if (!attr[p.circular ? 1 : 0]) {
+    static bool attr[4] = {false, false, false, false};
+    const int ki = (p.circular ? 1 : 0) + (p.bf ? 2 : 0);
+    auto kc = p.bf ? (p.circular ? &k_conv4s2h<Wo, true, true> : &k_conv4s2h<Wo, false, true>)
+                   : (p.circular ? &k_conv4s2h<Wo, true, false> : &k_conv4s2h<Wo, false, false>);
+    if (!attr[ki]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)shm) != hipSuccess) {
             set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", shm);
             return TCX_EHIP;
         }
-        attr[p.circular ? 1 : 0] = true;
+        attr[ki] = true;
     }
     const int grid = (p.M / 128) * p.n_nblk;
     hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * DS_NW), shm, st, p);

@@ -37,6 +37,9 @@ struct ConvParams {
     unsigned* ovf;
     // fragment-ordered copy of the h2 weights (tcx_pack_conv_weight_h2_frag) or null: k_conv3g only
     const void* wf;
+    // bf16 single-product mode (h2.hpp): the records hold bf16 halves, weights unscaled, one
+    // v_mfma_f32_32x32x16_bf16 (hi x hi) per product instead of three f16 ones
+    int bf;
 };
 
 // Halo-staged 3x3 kernel (conv3h.hip): applicability test and launcher for tcx_conv2d_h2.
@@ -140,13 +143,13 @@ __device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc
                 if (p.out_h2) {
                     // lane pairs (2j, 2j+1) of an 8-channel group swap halves: the even lane
                     // stores the hi pair, the odd lane the lo pair (one dword each)
-                    const unsigned sp = split1(v);
+                    const unsigned sp = split1x(v, p.bf);
                     const bool odd = (li & 1) != 0;
                     const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
                     const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
                     const int pe = e - co + (co & ~7);  // the 8-channel group's first element
                     *reinterpret_cast<unsigned*>(yb + (size_t)pe * 4 + (odd ? 16 : 0) + 2 * ((co & 7) & ~1)) = word;
-                    bad = bad || h2_bad(v);
+                    bad = bad || (!p.bf && h2_bad(v));
                 } else {
                     p.y[e] = v;
                 }
@@ -212,7 +215,7 @@ __device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc
             if (p.out_h2) {
                 // h2 record of the pixel: lane pairs (2j, 2j+1) of an 8-channel group swap halves so
                 // the even lane stores the hi pair and the odd lane the lo pair (one dword each)
-                const unsigned sp = split1(v);
+                const unsigned sp = split1x(v, p.bf);
                 const bool odd = (li & 1) != 0;
                 const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
                 const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
@@ -220,7 +223,7 @@ __device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc
                 const int c8 = coc & ~7, j = (coc & 7) & ~1;
                 if (ok[r]) {
                     *reinterpret_cast<unsigned*>(reinterpret_cast<char*>(p.y) + pe * 4 + (size_t)c8 * 4 + (odd ? 16 : 0) + 2 * j) = word;
-                    bad = bad || h2_bad(v);
+                    bad = bad || (!p.bf && h2_bad(v));
                 }
             } else if (ok[r]) {
                 p.y[oidx[r]] = v;

@@ -41,6 +41,39 @@ __device__ __forceinline__ void split4(const float4 v, uint2& hi, uint2& lo) {
     lo.y = (c >> 16) | (d & 0xffff0000u);
 }
 
+// bf16 single-product mode (the "bf16" precision of the score U-Net evaluator, config 5): the same
+// record layout with hi = bf16(v) (round to nearest even) and lo = bf16(v - hi); consumers multiply
+// the hi halves only (one v_mfma_f32_32x32x16_bf16 per product), weights unscaled.  bf16 has the
+// fp32 exponent range, so nothing overflows.
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ unsigned short bf16_bits(__bf16 h) { return __builtin_bit_cast(unsigned short, h); }
+
+__device__ __forceinline__ unsigned split1_bf(float v) {
+    const __bf16 h = (__bf16)v;
+    const __bf16 l = (__bf16)(v - (float)h);
+    return (unsigned)bf16_bits(h) | ((unsigned)bf16_bits(l) << 16);
+}
+
+// either split, by a uniform flag (writers; HBM-bound, so the branch is free)
+__device__ __forceinline__ unsigned split1x(float v, bool bf) { return bf ? split1_bf(v) : split1(v); }
+
+__device__ __forceinline__ void split4x(const float4 v, uint2& hi, uint2& lo, bool bf) {
+    const unsigned a = split1x(v.x, bf), b = split1x(v.y, bf), c = split1x(v.z, bf), d = split1x(v.w, bf);
+    hi.x = (a & 0xffffu) | (b << 16);
+    hi.y = (c & 0xffffu) | (d << 16);
+    lo.x = (a >> 16) | (b & 0xffff0000u);
+    lo.y = (c >> 16) | (d & 0xffff0000u);
+}
+
+__device__ __forceinline__ void store4_h2x(char* base, size_t pix, int q, const float4 v, bool bf) {
+    uint2 hi, lo;
+    split4x(v, hi, lo, bf);
+    char* g = base + pix + 32 * (size_t)(q >> 1) + 8 * (q & 1);
+    *reinterpret_cast<uint2*>(g) = hi;
+    *reinterpret_cast<uint2*>(g + 16) = lo;
+}
+
 __device__ __forceinline__ bool h2_bad(float v) { return !(fabsf(v) < kH2Max); }
 
 // Store channels [4q, 4q+4) of one pixel whose h2 record starts at byte `pix` (= pixel * C * 4).

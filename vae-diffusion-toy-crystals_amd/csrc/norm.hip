@@ -163,7 +163,7 @@ constexpr int UPK = 4;  // output quads per thread of the upsample (4 x 4 float4
 template <bool OUTH2>
 __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ x, float* __restrict__ y, int Bt, int H,
                                                     int W, int C, const float* __restrict__ tsc,
-                                                    const float* __restrict__ tsh, unsigned* ovf) {
+                                                    const float* __restrict__ tsh, unsigned* ovf, int bf) {
     // one output row (b, oy) per blockIdx.x, a chunk of UPK * 256 of its 2W * C/4 channel quads
     // per blockIdx.y.  The row's two source rows and weights are block-uniform (32-bit index
     // math only: the former flat 64-bit div/mod per element was the cost); the 4 x UPK source
@@ -226,14 +226,14 @@ __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ x,
             const size_t q = orow + i;
             if constexpr (OUTH2) {
                 const size_t pix = ((size_t)b * 2 * H + oy) * 2 * W + ox;
-                store4_h2(reinterpret_cast<char*>(y), pix * C * 4, c4, o);
+                store4_h2x(reinterpret_cast<char*>(y), pix * C * 4, c4, o, bf != 0);
                 bad = bad || h2_bad(o.x) || h2_bad(o.y) || h2_bad(o.z) || h2_bad(o.w);
             } else {
                 *reinterpret_cast<float4*>(y + q * 4) = o;
             }
         }
     }
-    h2_flag(ovf, bad);
+    h2_flag(ovf, bad && !bf);
 }
 
 // h2-output upsample with one 8-channel group per item: a thread reads 2 x 16 B per source tap and
@@ -242,7 +242,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int UPG = 2;  // 8-channel groups per thread
 __global__ __launch_bounds__(256) void k_upsample2x_g8(const float* __restrict__ x, char* __restrict__ y, int H, int W,
                                                        int C, const float* __restrict__ tsc,
-                                                       const float* __restrict__ tsh, unsigned* ovf) {
+                                                       const float* __restrict__ tsh, unsigned* ovf, int bf) {
     bool bad = false;
     const int C8 = C / 8;
     const int oy = blockIdx.x % (2 * H), b = blockIdx.x / (2 * H);
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void k_upsample2x_g8(const float* __restrict__
                     o[e] = fmaf(ly1, fmaf(lx1, vd[e], lx0 * vc[e]), ly0 * fmaf(lx1, vb[e], lx0 * va[e]));
                     bad = bad || h2_bad(o[e]);
                 }
-                split4(make_float4(o[0], o[1], o[2], o[3]), hi[h], lo[h]);
+                split4x(make_float4(o[0], o[1], o[2], o[3]), hi[h], lo[h], bf != 0);
             }
             const size_t pix = ((size_t)b * 2 * H + oy) * 2 * W + ox;
             char* gp = y + pix * C * 4 + 32 * (size_t)g;
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void k_upsample2x_g8(const float* __restrict__
             *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo[0].x, lo[0].y, lo[1].x, lo[1].y);
         }
     }
-    h2_flag(ovf, bad);
+    h2_flag(ovf, bad && !bf);
 }
 
 // LayerNorm over rows of width Wd (+ optional FiLM h*(1+gamma)+beta), one wave per row.
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(256) void k_layernorm_film(const float* __restrict_
 // (pixel, 8-channel group) reads 32 B and writes the same 32 B (hi[8], lo[8]), so x == y is safe.
 __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y, int HW, int C,
                                                          const float* __restrict__ tsc, const float* __restrict__ tsh,
-                                                         int silu, int ppb, unsigned* ovf) {
+                                                         int silu, int ppb, unsigned* ovf, int bf) {
     extern __shared__ __attribute__((aligned(16))) float lsm[];
     float* sc = lsm;
     float* sh = lsm + ((C + 3) & ~3);
@@ -448,8 +448,8 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
                 v1.x = silu_f(v1.x); v1.y = silu_f(v1.y); v1.z = silu_f(v1.z); v1.w = silu_f(v1.w);
             }
             uint2 h0, l0, h1, l1;
-            split4(v0, h0, l0);
-            split4(v1, h1, l1);
+            split4x(v0, h0, l0, bf != 0);
+            split4x(v1, h1, l1, bf != 0);
             char* g = y + (base + (size_t)(i + 256 * k) * 8) * 4;
             *reinterpret_cast<uint4*>(g) = make_uint4(h0.x, h0.y, h1.x, h1.y);
             *reinterpret_cast<uint4*>(g + 16) = make_uint4(l0.x, l0.y, l1.x, l1.y);
@@ -471,15 +471,15 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
             v1.x = silu_f(v1.x); v1.y = silu_f(v1.y); v1.z = silu_f(v1.z); v1.w = silu_f(v1.w);
         }
         uint2 h0, l0, h1, l1;
-        split4(v0, h0, l0);
-        split4(v1, h1, l1);
+        split4x(v0, h0, l0, bf != 0);
+        split4x(v1, h1, l1, bf != 0);
         char* g = y + (base + (size_t)i * 8) * 4;
         *reinterpret_cast<uint4*>(g) = make_uint4(h0.x, h0.y, h1.x, h1.y);
         *reinterpret_cast<uint4*>(g + 16) = make_uint4(l0.x, l0.y, l1.x, l1.y);
         bad = bad || h2_bad(v0.x) || h2_bad(v0.y) || h2_bad(v0.z) || h2_bad(v0.w) || h2_bad(v1.x) || h2_bad(v1.y) ||
               h2_bad(v1.z) || h2_bad(v1.w);
     }
-    h2_flag(ovf, bad);
+    h2_flag(ovf, bad && !bf);
 }
 
 // |x| max as the bit pattern of a non-negative float (ordered like the value: an atomicMax on the
@@ -604,12 +604,14 @@ extern "C" int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, in
     if ((size_t)Bt * H * W * C == 0) return TCX_OK;
     const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 4), UPK * 256));
     hipLaunchKernelGGL(k_upsample2x<false>, grid, dim3(256), 0, (hipStream_t)stream, x, y, Bt, H, W, C, scale, shift,
-                       nullptr);
+                       nullptr, 0);
     return check_launch("tcx_upsample2x");
 }
 
-extern "C" int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
-                                 const float* shift, unsigned* ovf, void* stream) {
+namespace tcx {
+// h2 (f16x3) or bf16 (bf != 0) records out of the upsample / GroupNorm apply (unet.hip, and the C ABI below)
+int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
+                  unsigned* ovf, int bf, hipStream_t st) {
     TCX_REQUIRE(x && y && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_upsample2x_h2: bad args");
     TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x_h2: scale/shift pair");
     if ((size_t)Bt * H * W * C == 0) return TCX_OK;
@@ -619,18 +621,16 @@ extern "C" int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, 
     }();
     if (g8) {
         const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 8), UPG * 256));
-        hipLaunchKernelGGL(k_upsample2x_g8, grid, dim3(256), 0, (hipStream_t)stream, x, (char*)y, H, W, C, scale,
-                           shift, ovf);
+        hipLaunchKernelGGL(k_upsample2x_g8, grid, dim3(256), 0, st, x, (char*)y, H, W, C, scale, shift, ovf, bf);
         return check_launch("tcx_upsample2x_h2");
     }
     const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 4), UPK * 256));
-    hipLaunchKernelGGL(k_upsample2x<true>, grid, dim3(256), 0, (hipStream_t)stream, x, (float*)y, Bt, H, W, C, scale,
-                       shift, ovf);
+    hipLaunchKernelGGL(k_upsample2x<true>, grid, dim3(256), 0, st, x, (float*)y, Bt, H, W, C, scale, shift, ovf, bf);
     return check_launch("tcx_upsample2x_h2");
 }
 
-extern "C" int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale,
-                                   const float* shift, int silu, unsigned* ovf, void* stream) {
+int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
+                    unsigned* ovf, int bf, hipStream_t st) {
     TCX_REQUIRE(x && y && scale && shift && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_gn_apply_tab_h2: bad args");
     TCX_REQUIRE((const void*)x == y || (const char*)y + (size_t)Bt * HW * C * 4 <= (const char*)x ||
                 (const char*)x + (size_t)Bt * HW * C * 4 <= (const char*)y, "tcx_gn_apply_tab_h2: partial overlap");
@@ -638,9 +638,30 @@ extern "C" int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int 
     const int ppb = std::max(1, 32768 / C);
     const dim3 grid(cdiv(HW, ppb), Bt);
     const size_t shm = (size_t)2 * ((C + 3) & ~3) * sizeof(float);
-    hipLaunchKernelGGL(k_gn_apply_tab_h2, grid, dim3(256), shm, (hipStream_t)stream, x, (char*)y, HW, C, scale, shift,
-                       silu, ppb, ovf);
+    hipLaunchKernelGGL(k_gn_apply_tab_h2, grid, dim3(256), shm, st, x, (char*)y, HW, C, scale, shift, silu, ppb, ovf,
+                       bf);
     return check_launch("tcx_gn_apply_tab_h2");
+}
+}  // namespace tcx
+
+extern "C" int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
+                                 const float* shift, unsigned* ovf, void* stream) {
+    return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, ovf, 0, (hipStream_t)stream);
+}
+
+extern "C" int tcx_upsample2x_bf16(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
+                                   const float* shift, void* stream) {
+    return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, nullptr, 1, (hipStream_t)stream);
+}
+
+extern "C" int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale,
+                                   const float* shift, int silu, unsigned* ovf, void* stream) {
+    return gn_apply_tab_h2(x, y, Bt, HW, C, scale, shift, silu, ovf, 0, (hipStream_t)stream);
+}
+
+extern "C" int tcx_gn_apply_tab_bf16(const float* x, void* y, int Bt, int HW, int C, const float* scale,
+                                     const float* shift, int silu, void* stream) {
+    return gn_apply_tab_h2(x, y, Bt, HW, C, scale, shift, silu, nullptr, 1, (hipStream_t)stream);
 }
 
 extern "C" int tcx_f32_to_h2(const float* x, void* y, size_t n, unsigned* ovf, void* stream) {

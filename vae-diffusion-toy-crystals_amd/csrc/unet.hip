@@ -16,6 +16,12 @@
 
 namespace tcx {
 bool conv3g_covers(int H, int W, int Cin, int cout_pad);  // conv3g.hip
+// h2 / bf16 record writers (norm.hip, attention_split.hip): bf != 0 writes bf16 halves
+int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
+                  unsigned* ovf, int bf, hipStream_t st);
+int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
+                    unsigned* ovf, int bf, hipStream_t st);
+int attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads, int bf, hipStream_t st);
 }
 
 #include <cmath>
@@ -529,12 +535,13 @@ struct GnRef {
 struct H2Ctx {
     bool on;
     unsigned* ovf;
+    bool bf;  // precision 2: bf16 records, one bf16 MFMA per product (no range limit, no flag)
 };
 
 int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2, int Bt, int bmod, int H, int W,
             int stride, int pad, const float* bias_b, const float* resid, float* y, double* gn, int* nsplit,
             hipStream_t st, const float* sc1 = nullptr, const float* sh1 = nullptr, const float* sc2 = nullptr,
-            const float* sh2 = nullptr, H2Ctx h2 = {false, nullptr}, int out_h2 = 0) {
+            const float* sh2 = nullptr, H2Ctx h2 = {false, nullptr, false}, int out_h2 = 0) {
     const int Ho = (H + 2 * pad - cv.ks) / stride + 1, Wo = (W + 2 * pad - cv.ks) / stride + 1;
     const int HoWo = Ho * Wo;
     const bool fused = gn && HoWo % 128 == 0;
@@ -543,7 +550,7 @@ int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2
         TCX_REQUIRE(cv.wh && cv.wscale, "tcx_unet: split path needs packed h2 weights");
         TCX_TRY(tcx_conv2d_h2_pro(x1, x2, Bt, bmod, H, W, C1, C2, cv.wh, cv.whf, cv.wscale, cv.b, bias_b, resid, y, out_h2,
                                   cv.cout, cv.cout_pad, cv.kpad, cv.ks, stride, pad, 1, 0, fused ? gn : nullptr, sc1,
-                                  sh1, sc2, sh2, h2.ovf, st));
+                                  sh1, sc2, sh2, h2.bf ? 1 : 0, h2.ovf, st));
     } else {
         TCX_TRY(tcx_conv2d(x1, x2, Bt, bmod, H, W, C1, C2, cv.w, cv.b, bias_b, resid, y, cv.cout, cv.cout_pad,
                            cv.kpad, cv.ks, stride, pad, 1, 0, 0, fused ? gn : nullptr, sc1, sh1, sc2, sh2, st));
@@ -636,7 +643,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // normalised tensor is never written: norms 0, 2, 7, 9 (down1.net.1, down2.net.1, up2.net.1,
     // up1.net.1 feeding down1/down2/up2/up1 .net.3).  The skip tensors h1/h2 (norms 1, 3: read by a
     // 4x4/s2 conv AND an up-path concat) and the 16x16 mid block keep the in-place h2 apply pass.
-    if (net->precision == 1) {
+    if (net->precision >= 1) {
         pro[0] = net->down1_1.whf && conv3g_covers(H, W, C, net->down1_1.cout_pad);
         pro[2] = net->down2_1.whf && conv3g_covers(H1, W1, C2, net->down2_1.cout_pad);
         pro[7] = net->up2_1.whf && conv3g_covers(H1, W1, C, net->up2_1.cout_pad);
@@ -647,11 +654,11 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // finalize the table of norm i, or normalise `y` in place when no prologue can consume it
     // split path: every conv source is h2 (h2.hpp) — GroupNorm applies feeding a conv write h2
     // in place, convs feeding only convs (ds1, ds2, us2, us1) write h2, the rest stay fp32
-    const H2Ctx h2{net->precision == 1, net->h2_ovf};
+    const H2Ctx h2{net->precision >= 1, net->h2_ovf, net->precision == 2};
     auto norm = [&](int i, float* y, int HW, int Cn, bool to_h2 = true) -> int {
         TCX_TRY(gn_tab(net, P, i, HW, Cn, gn, ns, st));
         if (pro[i]) return TCX_OK;
-        if (h2.on && to_h2) return tcx_gn_apply_tab_h2(y, y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, h2.ovf, st);
+        if (h2.on && to_h2) return gn_apply_tab_h2(y, y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, h2.ovf, h2.bf, st);
         return tcx_gn_apply_tab(y, y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, st);
     };
     // down1 (first conv: x_t channel only, maps folded into bias0; the conv bias is inside bias0)
@@ -701,7 +708,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         const int ns_a = std::max(1, P.P2 / 256);
         TCX_TRY(tcx_gn_partials(P.a16, Bt, P.P2, C2, ns_a, gn, st));
         TCX_TRY(gn_tab(net, P, 6, P.P2, C2, gn, ns_a, st));
-        if (h2.on) TCX_TRY(tcx_gn_apply_tab_h2(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, h2.ovf, st));
+        if (h2.on) TCX_TRY(gn_apply_tab_h2(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, h2.ovf, h2.bf, st));
         else TCX_TRY(tcx_gn_apply_tab(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, st));
         const tcx_conv& q = net->qkv;
         int dummy = 0;
@@ -712,7 +719,8 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                                 (D == 16 || D == 32 || D == 48 || D == 64);
         TCX_TRY(conv_gn(q, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 0, nullptr, nullptr, P.qkv, nullptr, &dummy, st,
                         nullptr, nullptr, nullptr, nullptr, h2, split_attn ? 1 : 0));
-        if (split_attn) TCX_TRY(tcx_attention_split(P.qkv, P.b16, Bt, P.P2, C2, net->heads, st));
+        TCX_REQUIRE(split_attn || !h2.bf, "tcx_unet: bf16 precision needs the split attention (N %% 256 == 0)");
+        if (split_attn) TCX_TRY(attention_split(P.qkv, P.b16, Bt, P.P2, C2, net->heads, h2.bf, st));
         else if (h2.on) TCX_TRY(tcx_attention_h2(P.qkv, P.b16, Bt, P.P2, C2, net->heads, h2.ovf, st));
         else TCX_TRY(tcx_attention(P.qkv, P.b16, Bt, P.P2, C2, net->heads, st));
         const tcx_conv& pr = net->proj;
@@ -722,7 +730,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // us2: bilinear x2 (edge-clamped) into the free b32 buffer, then the circular 3x3 conv -> a32.
     // (The upsample-on-load conv variant re-reads 4 source taps per im2col element and measured
     // slower than this separate 250 MB pass.)
-    if (h2.on) TCX_TRY(tcx_upsample2x_h2(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, h2.ovf, st));
+    if (h2.on) TCX_TRY(upsample2x_h2(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, h2.ovf, h2.bf, st));
     else TCX_TRY(tcx_upsample2x(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, st));
     TCX_TRY(conv_gn(net->us2, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, nullptr, &ns, st,
                     nullptr, nullptr, nullptr, nullptr, h2, 1));
@@ -735,7 +743,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // us1: GN+SiLU of up2's output in place (1x per element; the upsample-side transform
     // recomputed it for 4 taps per output and measured 3x slower), upsample into the free b64, conv
     TCX_TRY(norm(8, P.a32, P.P1, C, false));
-    if (h2.on) TCX_TRY(tcx_upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, h2.ovf, st));
+    if (h2.on) TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, h2.ovf, h2.bf, st));
     else TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, st));
     TCX_TRY(conv_gn(net->us1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, nullptr, &ns, st,
                     nullptr, nullptr, nullptr, nullptr, h2, 1));
@@ -774,9 +782,12 @@ int validate(const tcx_unet* net, int B, int H, int W) {
     TCX_REQUIRE(net->time_ch + net->cond_ch <= 64 && net->y_cont_dim >= 3 && net->y_cont_dim <= 16, "tcx_unet: bad cond dims");
     TCX_REQUIRE((H / 4) * (W / 4) <= 256 || ((H / 4) * (W / 4)) % 256 == 0,
                 "tcx_unet: bottleneck attention needs N <= 256 or N %% 256 == 0 tokens");
-    TCX_REQUIRE(net->precision == 0 || net->precision == 1, "tcx_unet: precision must be 0 (fp32) or 1 (f16x3)");
+    TCX_REQUIRE(net->precision >= 0 && net->precision <= 2,
+                "tcx_unet: precision must be 0 (fp32), 1 (f16x3) or 2 (bf16)");
     TCX_REQUIRE(net->precision == 0 || (net->base_ch % 32 == 0 && ((H / 4) * (W / 4)) % 32 == 0),
-                "tcx_unet: the f16x3 split path needs base_ch %% 32 == 0 and (H/4)*(W/4) %% 32 == 0");
+                "tcx_unet: the split paths need base_ch %% 32 == 0 and (H/4)*(W/4) %% 32 == 0");
+    TCX_REQUIRE(net->precision != 2 || ((H / 4) * (W / 4)) % 256 == 0,
+                "tcx_unet: bf16 precision needs (H/4)*(W/4) %% 256 == 0 (the split attention)");
     return TCX_OK;
 }
 

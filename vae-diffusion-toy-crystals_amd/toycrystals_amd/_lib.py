@@ -91,7 +91,11 @@ _SIGS = {
                               c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
     "tcx_conv2d_h2_pro": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp,
                                   c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                  c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp]),
+                                  c_fp, c_fp, c_fp, c_fp, c_fp, c_int, c_fp, c_fp]),
+    "tcx_pack_conv_weight_bf16": (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_fp]),
+    "tcx_gn_apply_tab_bf16": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp]),
+    "tcx_upsample2x_bf16": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
+    "tcx_attention_split_bf16": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_conv_weight_h2_frag_bytes": (c_size, [c_int, c_int]),
     "tcx_pack_conv_weight_h2_frag": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp]),
     "tcx_gn_apply_tab_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp, c_fp]),
@@ -188,7 +192,7 @@ _lib = None
 # fp32-grade: DESIGN.md §3c) or "fp32" (v_mfma_f32_32x32x2_f32).  Env TCX_CONV_PRECISION or
 # set_conv_precision(); the U-Net falls back to fp32 per call where the split path does not apply
 # (base_ch % 32 != 0) or when an activation leaves the f16 range.
-_PRECISIONS = ("f16x3", "fp32")
+_PRECISIONS = ("f16x3", "fp32", "bf16")  # bf16: the score U-Net evaluator only (config 5)
 _conv_precision = os.environ.get("TCX_CONV_PRECISION", "f16x3")
 if _conv_precision not in _PRECISIONS:
     raise ValueError(f"TCX_CONV_PRECISION must be one of {_PRECISIONS}, got {_conv_precision!r}")

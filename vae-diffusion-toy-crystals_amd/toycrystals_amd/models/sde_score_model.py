@@ -26,7 +26,8 @@ import torch.nn as nn
 
 from .. import _lib
 from .. import functional as TF
-from .._lib import TCX_SAMPLE_X0_HAT, TCX_SCAL, TcxConv, TcxUnet, check, lib, ptr, require_gpu_tensor, stream_ptr
+from .._lib import (_CONV_NAMES, TCX_SAMPLE_X0_HAT, TCX_SCAL, TcxConv, TcxUnet, check, lib, ptr,
+                    require_gpu_tensor, stream_ptr)
 
 
 # =========================
@@ -198,11 +199,54 @@ class _UNetPack:
             net.gn_b[i] = dev(gnm.bias)
         self.net = net
         self.ws = None
+        self._st = st
+        self._bf = None  # bf16 packs, built on first use
+
+    def _bf16_packs(self):
+        """{conv name: (wh, wscale, whf)} in the bf16 single-product layout (tcx_pack_conv_weight_bf16)."""
+        if self._bf is None:
+            L = lib()
+            packs = {}
+            for name in _CONV_NAMES:
+                c = getattr(self.net, name)
+                if not c.wh:
+                    continue
+                wh = torch.empty((c.cout_pad, c.kpad), device=self.device, dtype=torch.float32)
+                ws = torch.empty(4, device=self.device, dtype=torch.float32)
+                check(L.tcx_pack_conv_weight_bf16(c.w, wh.data_ptr(), ws.data_ptr(), c.cout_pad, c.kpad, self._st),
+                      "pack conv weight bf16")
+                whf = None
+                if c.whf:
+                    nfb = int(L.tcx_conv_weight_h2_frag_bytes(c.cout_pad, c.cin))
+                    whf = torch.empty(nfb // 4, device=self.device, dtype=torch.float32)
+                    check(L.tcx_pack_conv_weight_h2_frag(wh.data_ptr(), whf.data_ptr(), c.cout_pad, c.kpad, c.cin,
+                                                         self._st), "pack conv weight bf16 frag")
+                packs[name] = (wh, ws, whf)
+            self._bf = packs
+        return self._bf
 
     def run(self, H: int, W: int, launch) -> None:
         """Run `launch()` (which must (re)initialise its outputs) with the configured conv
-        precision; if an f16x3 run raised the range flag, re-run it in fp32 (one host sync)."""
-        split = (_lib.conv_precision() == "f16x3" and self.split_ok and ((H // 4) * (W // 4)) % 32 == 0)
+        precision; if an f16x3 run raised the range flag, re-run it in fp32 (one host sync).
+        "bf16" (config 5's precision) runs where the split attention applies, else f16x3."""
+        prec = _lib.conv_precision()
+        split = prec in ("f16x3", "bf16") and self.split_ok and ((H // 4) * (W // 4)) % 32 == 0
+        bf = split and prec == "bf16" and ((H // 4) * (W // 4)) % 256 == 0
+        if bf:
+            saved = {}
+            for name, (wh, ws, whf) in self._bf16_packs().items():
+                c = getattr(self.net, name)
+                saved[name] = (c.wh, c.wscale, c.whf)
+                c.wh, c.wscale, c.whf = wh.data_ptr(), ws.data_ptr(), ptr(whf)
+            try:
+                self.net.precision = 2
+                launch()
+            finally:
+                for name, (a, b, f) in saved.items():
+                    c = getattr(self.net, name)
+                    c.wh, c.wscale, c.whf = a, b, f
+                self.net.precision = 0
+            return
         self.net.precision = 1 if split else 0
         if split:
             self.ovf.zero_()
