@@ -423,6 +423,13 @@ int tcx_gemm_ws(int M, int N, int K, float alpha, const float* A, long long sa_m
  * padding).  Also the ConvTranspose2d weight gradient (input/output roles swapped).  Backward of
  * nn.Conv2d (sde_score_model.py:102-105,133-134,208-225; vae.py:19-26) / ConvTranspose2d (vae.py:35-42). */
 size_t tcx_conv_wgrad_workspace(int Bt, int Ho, int Wo, int Cin, int Cout, int ks);
+/* tcx_conv_wgrad on the f16x3 split path: x1/x2 (the conv's input) and dy in h2 records, each scaled
+ * by an exact power of two (tcx_absmax + tcx_f32_to_h2_scaled); comb -> 1 / (s_x s_dy).  Products on
+ * v_mfma_f32_32x32x16_f16 (three per fp32 product), same split plan, workspace and fixed-order
+ * reduce as tcx_conv_wgrad.  C1, C2, Cout % 8 == 0. */
+int tcx_conv_wgrad_h2(const void* x1, const void* x2, int Bt, int H, int W, int C1, int C2, const void* dy, int Cout,
+                      int ks, int stride, int pad, int circular, float beta, const float* comb, float* dw, void* ws,
+                      size_t ws_bytes, void* stream);
 int tcx_conv_wgrad(const float* x1, const float* x2, int Bt, int H, int W, int C1, int C2, const float* dy,
                    int Cout, int ks, int stride, int pad, int circular, float beta, float* dw, void* ws,
                    size_t ws_bytes, void* stream);

@@ -8,6 +8,6 @@ c = sqlite3.connect(db)
 rows = c.execute("select name, grid_x, grid_y, workgroup_x, count(*), avg(duration), sum(duration) from kernels "
                  "group by name, grid_x, grid_y order by sum(duration) desc limit ?", (n,)).fetchall()
 for r in rows:
-    name = r[0].split("(")[0].replace("tcx::(anonymous namespace)::", "").replace("void ", "")
+    name = r[0].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].replace("tcx::", "")
     print(f"{name[-44:]:>44} grid=({r[1]},{r[2]}) wg={r[3]} n={r[4]:5d} avg={r[5] / 1000:7.2f} us "
           f"sum={r[6] / 1e6:7.2f} ms")

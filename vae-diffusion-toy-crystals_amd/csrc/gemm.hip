@@ -15,6 +15,7 @@
 // along the contiguous dimension and transposed on the LDS store.
 #include "common.hpp"
 #include "skinny.hpp"
+#include "h2.hpp"
 
 namespace tcx {
 namespace {
@@ -277,6 +278,7 @@ struct WgParams {
     float* part;  // [nsplit][K][Cout]
     int nsplit, cps;  // splits, 32-pixel chunks per split
     int nkblk, ncblk;
+    const float* comb;  // k_wgrad_h2: 1 / (s_x s_dy), the operands' power-of-two scales
 };
 
 // ASC: scalar im2col gather (Cin % 4 != 0); BSC: scalar dY loads (Cout % 4 != 0)
@@ -414,6 +416,143 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgParams p) {
         for (int r = 0; r < 16; ++r) {
             const int k = k0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
             if (k < p.K) dst[(size_t)k * p.Cout + co] = acc[n][r];
+        }
+    }
+}
+
+// f16x3 weight gradient: the im2col source x and dY arrive as h2 records (h2.hpp) scaled by exact
+// powers of two (functional.py: tcx_absmax + tcx_f32_to_h2_scaled); both are transposed through LDS
+// as f16 hi / lo planes [row][32 pixels] and each 16-pixel step is three v_mfma_f32_32x32x16_f16
+// (hi*lo, lo*hi, hi*hi) instead of eight fp32 ones.  Same tiling, split plan and fixed-order reduce as
+// k_wgrad; the partials are acc * comb.  Needs C1, C2, Cout % 8 == 0 (whole 4-channel quads of a record).
+template <int NT>
+__global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
+    constexpr int BN = 32 * NT;
+    constexpr int RS = 40;  // halves per LDS row: 32 pixels + 8 pad (80 B)
+    __shared__ __attribute__((aligned(16))) _Float16 Ah[2][GBM * RS];
+    __shared__ __attribute__((aligned(16))) _Float16 Al[2][GBM * RS];
+    __shared__ __attribute__((aligned(16))) _Float16 Bh[2][BN * RS];
+    __shared__ __attribute__((aligned(16))) _Float16 Bl[2][BN * RS];
+    const int split = blockIdx.y;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kblk = tile / p.ncblk, cblk = tile - (tile / p.ncblk) * p.ncblk;
+    const int k0 = kblk * GBM, c0 = cblk * BN;
+    const int tid = threadIdx.x;
+    const int px = tid & 31, q = tid >> 5;
+    const int chunk0 = split * p.cps;
+    const int nch_all = (p.M + 31) / 32;
+    const int chunk1 = min(chunk0 + p.cps, nch_all);
+    const char* x1 = reinterpret_cast<const char*>(p.x1);
+    const char* x2 = reinterpret_cast<const char*>(p.x2);
+    const char* dyb = reinterpret_cast<const char*>(p.dy);
+    // per-thread im2col quads: k = k0 + 4 (q + 8 i) .. +3 share one tap and source (C1, C2 % 8 == 0)
+    int tdy[4], tdx[4], toff[4];
+    bool tsrc1[4], tkv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = k0 + 4 * (q + 8 * i);
+        const int kk = k < p.K ? k : 0;
+        const int tap = kk / p.Cin, ci = kk - (kk / p.Cin) * p.Cin;
+        tdy[i] = tap / p.ks;
+        tdx[i] = tap - (tap / p.ks) * p.ks;
+        tsrc1[i] = ci < p.C1;
+        const int c = ci < p.C1 ? ci : ci - p.C1;
+        toff[i] = (c >> 3) * 32 + (c & 4) * 2;  // byte offset of the quad's hi half in the pixel record
+        tkv[i] = k < p.K;
+    }
+    uint2 ah[4], al[4], bh[NT], bl[NT];
+    auto load = [&](int c) {
+        const int m = c * 32 + px;
+        const bool mv = m < p.M;
+        const int mm = mv ? m : 0;
+        const int b = mm / p.HoWo, r = mm - (mm / p.HoWo) * p.HoWo;
+        const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+        const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int yy = iy0 + tdy[i], xx = ix0 + tdx[i];
+            bool ok = mv && tkv[i];
+            if (p.circular) {
+                yy = wrap_idx(yy, p.H);
+                xx = wrap_idx(xx, p.W);
+            } else {
+                ok = ok && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
+            }
+            const size_t pix = ((size_t)b * p.H + (ok ? yy : 0)) * p.W + (ok ? xx : 0);
+            const char* a = tsrc1[i] ? x1 + pix * p.C1 * 4 + toff[i] : x2 + pix * p.C2 * 4 + toff[i];
+            ah[i] = ok ? *reinterpret_cast<const uint2*>(a) : make_uint2(0u, 0u);
+            al[i] = ok ? *reinterpret_cast<const uint2*>(a + 16) : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int co = c0 + 4 * (q + 8 * j);
+            const bool ok = mv && co < p.Cout;
+            const char* d = dyb + ((size_t)mm * p.Cout + (co >> 3) * 8) * 4 + (co & 4) * 2;
+            bh[j] = ok ? *reinterpret_cast<const uint2*>(d) : make_uint2(0u, 0u);
+            bl[j] = ok ? *reinterpret_cast<const uint2*>(d + 16) : make_uint2(0u, 0u);
+        }
+    };
+    auto put4 = [&](_Float16* plane, int row0, const uint2 v) {  // 4 consecutive rows, this pixel
+        plane[(row0 + 0) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.x & 0xffffu));
+        plane[(row0 + 1) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.x >> 16));
+        plane[(row0 + 2) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.y & 0xffffu));
+        plane[(row0 + 3) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.y >> 16));
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            put4(Ah[buf], 4 * (q + 8 * i), ah[i]);
+            put4(Al[buf], 4 * (q + 8 * i), al[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            put4(Bh[buf], 4 * (q + 8 * j), bh[j]);
+            put4(Bl[buf], 4 * (q + 8 * j), bl[j]);
+        }
+    };
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
+    const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
+    if (chunk0 < chunk1) {
+        load(chunk0);
+        store(0);
+    }
+    __syncthreads();
+    for (int c = chunk0; c < chunk1; ++c) {
+        const int cur = (c - chunk0) & 1;
+        if (c + 1 < chunk1) load(c + 1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int off = 16 * s + 8 * lh;
+            const h8 fah = *reinterpret_cast<const h8*>(&Ah[cur][(wv * 32 + li) * RS + off]);
+            const h8 fal = *reinterpret_cast<const h8*>(&Al[cur][(wv * 32 + li) * RS + off]);
+            h8 fbh[NT], fbl[NT];
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                fbh[n] = *reinterpret_cast<const h8*>(&Bh[cur][(n * 32 + li) * RS + off]);
+                fbl[n] = *reinterpret_cast<const h8*>(&Bl[cur][(n * 32 + li) * RS + off]);
+            }
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbl[n], acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[n], acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbh[n], acc[n], 0, 0, 0);
+        }
+        if (c + 1 < chunk1) store(cur ^ 1);
+        __syncthreads();
+    }
+    const float sc = *p.comb;
+    float* dst = p.part + (size_t)split * p.K * p.Cout;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int co = c0 + n * 32 + li;
+        if (co >= p.Cout) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = k0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (k < p.K) dst[(size_t)k * p.Cout + co] = acc[n][r] * sc;
         }
     }
 }
@@ -677,4 +816,40 @@ extern "C" int tcx_conv_wgrad(const float* x1, const float* x2, int Bt, int H, i
     hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, st, p.part, p.nsplit, p.K, Cout, p.Cin, ks, beta,
                        dw);
     return check_launch("tcx_conv_wgrad reduce");
+}
+
+extern "C" int tcx_conv_wgrad_h2(const void* x1, const void* x2, int Bt, int H, int W, int C1, int C2, const void* dy,
+                                 int Cout, int ks, int stride, int pad, int circular, float beta, const float* comb,
+                                 float* dw, void* ws, size_t ws_bytes, void* stream) {
+    TCX_REQUIRE(x1 && dy && dw && ws && comb, "tcx_conv_wgrad_h2: null pointer");
+    TCX_REQUIRE((C2 == 0) == (x2 == nullptr) && C1 > 0 && C1 % 8 == 0 && C2 % 8 == 0 && Cout % 8 == 0 && Bt >= 0,
+                "tcx_conv_wgrad_h2: needs C1, C2, Cout %% 8 == 0 (h2 records)");
+    TCX_REQUIRE(ks >= 1 && stride >= 1 && pad >= 0, "tcx_conv_wgrad_h2: bad geometry");
+    TCX_REQUIRE(aligned16(x1) && (!x2 || aligned16(x2)) && aligned16(dy), "tcx_conv_wgrad_h2: 16-B alignment");
+    WgParams p{};
+    p.x1 = (const float*)x1; p.x2 = (const float*)x2; p.C1 = C1; p.C2 = C2; p.Cin = C1 + C2; p.H = H; p.W = W;
+    p.Ho = (H + 2 * pad - ks) / stride + 1;
+    p.Wo = (W + 2 * pad - ks) / stride + 1;
+    TCX_REQUIRE(p.Ho > 0 && p.Wo > 0, "tcx_conv_wgrad_h2: empty output");
+    p.HoWo = p.Ho * p.Wo; p.M = Bt * p.HoWo;
+    p.ks = ks; p.stride = stride; p.pad = pad; p.circular = circular;
+    p.dy = (const float*)dy; p.Cout = Cout; p.K = ks * ks * p.Cin; p.comb = comb;
+    int nt;
+    wgrad_plan(p.M, p.K, Cout, &nt, &p.nsplit, &p.cps, &p.nkblk, &p.ncblk);
+    const size_t need = (size_t)p.nsplit * p.K * Cout * sizeof(float);
+    char* base = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
+    TCX_REQUIRE(need + (base - (char*)ws) <= ws_bytes, "tcx_conv_wgrad_h2: workspace too small (%zu < %zu)",
+                ws_bytes, need + 256);
+    p.part = reinterpret_cast<float*>(base);
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(p.nkblk * p.ncblk, p.nsplit);
+    if (nt == 3) hipLaunchKernelGGL((k_wgrad_h2<3>), grid, dim3(256), 0, st, p);
+    else if (nt == 2) hipLaunchKernelGGL((k_wgrad_h2<2>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_wgrad_h2<1>), grid, dim3(256), 0, st, p);
+    TCX_TRY(check_launch("tcx_conv_wgrad_h2"));
+    const size_t n = (size_t)p.K * Cout;
+    const int blocks = (int)std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3(blocks), dim3(256), 0, st, p.part, p.nsplit, p.K, Cout, p.Cin, ks, beta,
+                       dw);
+    return check_launch("tcx_conv_wgrad_h2 reduce");
 }

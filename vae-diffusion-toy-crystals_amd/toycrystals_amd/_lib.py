@@ -92,6 +92,8 @@ _SIGS = {
     "tcx_conv2d_h2_pro": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp,
                                   c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                   c_fp, c_fp, c_fp, c_fp, c_fp, c_int, c_fp, c_fp]),
+    "tcx_conv_wgrad_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_int, c_int, c_int, c_int,
+                                  c_int, c_float, c_fp, c_fp, c_fp, c_size, c_fp]),
     "tcx_pack_conv_weight_bf16": (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_fp]),
     "tcx_gn_apply_tab_bf16": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp]),
     "tcx_upsample2x_bf16": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),

@@ -101,12 +101,14 @@ def _pack_conv(w: torch.Tensor):
 # activation in the forward, dY in the stride-1 data gradient) is converted to h2 after an exact
 # power-of-two scaling from its max |value| (gradients sit far below the f16 normal range,
 # activations can exceed its maximum), the weight is packed to h2 with its own power-of-two scale,
-# and the conv epilogue applies the product of both inverse scales.  TCX_TRAIN_SPLIT=0 keeps them
-# on fp32 MFMA.  The weight gradient stays fp32.
+# and the conv epilogue applies the product of both inverse scales.  The weight gradient of the same
+# convs runs split too (tcx_conv_wgrad_h2: x and dY scaled and converted).  TCX_TRAIN_SPLIT=0 keeps
+# all of them on fp32 MFMA.
 _TRAIN_SPLIT = os.environ.get("TCX_TRAIN_SPLIT", "1") != "0"
 
 
 _SPLIT_MIN_MACS = 4e9  # below this the scaling / conversion launches cost more than the MFMA saves
+_WGRAD_SPLIT = os.environ.get("TCX_WGRAD_FP32", "0") == "0"  # TCX_WGRAD_FP32=1: weight gradients on fp32 MFMA
 
 
 def _split_ok(x1, x2, C1, C2, ks, kpad, macs) -> bool:
@@ -116,48 +118,67 @@ def _split_ok(x1, x2, C1, C2, ks, kpad, macs) -> bool:
             and max(x1.numel(), 0 if x2 is None else x2.numel()) * 4 < (1 << 31))
 
 
-def _conv_fwd_split(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride, pad, circular, y):
+def _h2_scaled(ts):
+    """fp32 tensors sharing ONE power-of-two scale s (max |s v| in [2^13, 2^14)) -> their h2 records
+    and a 1-element float tensor holding 1/s (tcx_absmax + tcx_f32_to_h2_scaled)."""
+    L = lib()
+    st = _st(ts[0])
+    sl = torch.zeros(12, dtype=torch.int32, device=ts[0].device)  # [bits][1.0][1/s], 16 B apart
+    sl[4:5].view(torch.float32).fill_(1.0)
+    bits, one, inv = ptr(sl), ptr(sl) + 16, ptr(sl) + 32
+    for t in ts:
+        check(L.tcx_absmax(ptr(t), t.numel(), bits, st), "tcx_absmax")
+    hs = []
+    for i, t in enumerate(ts):
+        h = torch.empty_like(t)
+        check(L.tcx_f32_to_h2_scaled(ptr(t), ptr(h), t.numel(), bits, one if i == 0 else None,
+                                     inv if i == 0 else None, st), "to h2")
+        hs.append(h)
+    return hs, sl[8:9].view(torch.float32)
+
+
+def _conv_fwd_split(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride, pad, circular, y, xh=None):
+    """xh: (x1h, x2h, 1/s_x) already converted (the backward reuses the forward's / dgrad's records);
+    returns y and the operand records for reuse."""
     L = lib()
     st = _st(x1)
     B, H, W, C1 = x1.shape
     C2 = 0 if x2 is None else x2.shape[3]
-    # one scratch: [absmax bits of x][absmax bits of w][1.0][1/s_w][1/(s_w s_x)], 16 B apart
-    sc = torch.zeros(20, dtype=torch.int32, device=x1.device)
-    sc[8:12].view(torch.float32).fill_(1.0)
-    bx, bw, one, winv, comb = (ptr(sc) + 16 * i for i in range(5))
-    check(L.tcx_absmax(ptr(x1), x1.numel(), bx, st), "tcx_absmax")
-    if x2 is not None:
-        check(L.tcx_absmax(ptr(x2), x2.numel(), bx, st), "tcx_absmax")
-    check(L.tcx_absmax(ptr(wpk), wpk.numel(), bw, st), "tcx_absmax")
-    wh = torch.empty_like(wpk)  # h2 of the packed weight (the layout of tcx_pack_conv_weight_h2)
-    check(L.tcx_f32_to_h2_scaled(ptr(wpk), ptr(wh), wpk.numel(), bw, one, winv, st), "w to h2")
-    x1h = torch.empty_like(x1)
-    check(L.tcx_f32_to_h2_scaled(ptr(x1), ptr(x1h), x1.numel(), bx, winv, comb, st), "to h2")
-    x2h = None
-    if x2 is not None:
-        x2h = torch.empty_like(x2)
-        check(L.tcx_f32_to_h2_scaled(ptr(x2), ptr(x2h), x2.numel(), bx, None, None, st), "to h2")
-    check(L.tcx_conv2d_h2(ptr(x1h), ptr(x2h), B, 0, H, W, C1, C2, ptr(wh), comb, ptr(b), ptr(bias_b), ptr(resid),
-                          ptr(y), 0, Cout, cpad, kpad, ks, stride, pad, circular, 0, None, None, st), "tcx_conv2d_h2")
-    return y
+    if xh is None:
+        hs, xinv = _h2_scaled([x1] if x2 is None else [x1, x2])
+        xh = (hs[0], hs[1] if x2 is not None else None, xinv)
+    x1h, x2h, xinv = xh
+    (wh,), winv = _h2_scaled([wpk])  # h2 of the packed weight (the layout of tcx_pack_conv_weight_h2)
+    comb = winv * xinv  # 1 / (s_w s_x), applied by the conv epilogue
+    check(L.tcx_conv2d_h2(ptr(x1h), ptr(x2h), B, 0, H, W, C1, C2, ptr(wh), ptr(comb), ptr(b), ptr(bias_b),
+                          ptr(resid), ptr(y), 0, Cout, cpad, kpad, ks, stride, pad, circular, 0, None, None, st),
+          "tcx_conv2d_h2")
+    return y, xh
 
 
-def _conv_fwd(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride, pad, circular, out_hw=None):
+def _conv_fwd(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride, pad, circular, out_hw=None, keep=None,
+              xh=None):
+    """keep: a list that receives the split path's operand records (x1h, x2h, 1/s_x) when it runs;
+    xh: records converted by the caller."""
     B, H, W, C1 = x1.shape
     C2 = 0 if x2 is None else x2.shape[3]
     Ho = (H + 2 * pad - ks) // stride + 1
     Wo = (W + 2 * pad - ks) // stride + 1
     y = _empty((B, Ho, Wo, Cout), x1)
     if _split_ok(x1, x2, C1, C2, ks, kpad, float(B) * Ho * Wo * Cout * ks * ks * (C1 + C2)):
-        return _conv_fwd_split(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride, pad, circular, y)
+        y, rec = _conv_fwd_split(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride, pad, circular, y, xh)
+        if keep is not None:
+            keep.append(rec)
+        return y
     check(lib().tcx_conv2d(ptr(x1), ptr(x2), B, 0, H, W, C1, C2, ptr(wpk), ptr(b), ptr(bias_b), ptr(resid), ptr(y),
                            Cout, cpad, kpad, ks, stride, pad, circular, 0, 0, None, None, None, None, None, _st(x1)),
           "tcx_conv2d")
     return y
 
 
-def _conv_dgrad(dy, w, C_lo, n_ci, stride, pad, circular, H, W):
-    """Gradient w.r.t. input channels [C_lo, C_lo + n_ci) of a Conv2d with weight w [Cout][Cin][k][k]."""
+def _conv_dgrad(dy, w, C_lo, n_ci, stride, pad, circular, H, W, keep=None):
+    """Gradient w.r.t. input channels [C_lo, C_lo + n_ci) of a Conv2d with weight w [Cout][Cin][k][k].
+    keep: [] to receive / [rec] to reuse dY's split-path records (dyh, None, 1/s_dy)."""
     L = lib()
     Cout, Cin, ks, _ = w.shape
     B = dy.shape[0]
@@ -166,7 +187,9 @@ def _conv_dgrad(dy, w, C_lo, n_ci, stride, pad, circular, H, W):
         kpad, cpad = _rup(ks * ks * Cout), _rup(n_ci)
         wpk = _empty((cpad, kpad), dy)
         check(L.tcx_pack_conv_dgrad_weight(ptr(w), ptr(wpk), Cout, Cin, ks, C_lo, n_ci, cpad, kpad, st), "pack dgrad")
-        dx = _conv_fwd(dy, None, wpk, kpad, cpad, None, None, None, n_ci, ks, 1, ks - 1 - pad, circular)
+        xh = keep[0] if keep else None
+        dx = _conv_fwd(dy, None, wpk, kpad, cpad, None, None, None, n_ci, ks, 1, ks - 1 - pad, circular,
+                       keep=keep if (keep is not None and not keep) else None, xh=xh)
         assert dx.shape[1] == H and dx.shape[2] == W
         return dx
     if stride == 2 and ks == 4 and pad == 1 and C_lo == 0 and n_ci == Cin:
@@ -183,7 +206,9 @@ def _conv_dgrad(dy, w, C_lo, n_ci, stride, pad, circular, H, W):
     raise NotImplementedError(f"conv data gradient for stride={stride}, k={ks}, pad={pad}")
 
 
-def _conv_wgrad(x1, x2, dy, Cout, ks, stride, pad, circular):
+def _conv_wgrad(x1, x2, dy, Cout, ks, stride, pad, circular, xrec=None, dyrec=None):
+    """xrec / dyrec: the split-path records (h2, h2 or None, 1/s) of x and dY when the forward / the
+    data gradient made them: the weight gradient then runs f16x3 (tcx_conv_wgrad_h2) on them."""
     L = lib()
     B, H, W, C1 = x1.shape
     C2 = 0 if x2 is None else x2.shape[3]
@@ -191,6 +216,16 @@ def _conv_wgrad(x1, x2, dy, Cout, ks, stride, pad, circular):
     dw = _empty((Cout, C1 + C2, ks, ks), dy)
     nb = int(L.tcx_conv_wgrad_workspace(B, Ho, Wo, C1 + C2, Cout, ks))
     ws = _ws(dy.device, nb)
+    if _WGRAD_SPLIT and xrec is not None and Cout % 8 == 0 and dy.numel() * 4 < (1 << 31):
+        if dyrec is None:
+            (dyh,), dyinv = _h2_scaled([dy])
+        else:
+            dyh, _, dyinv = dyrec
+        comb = xrec[2] * dyinv
+        check(L.tcx_conv_wgrad_h2(ptr(xrec[0]), ptr(xrec[1]), B, H, W, C1, C2, ptr(dyh), Cout, ks, stride, pad,
+                                  circular, 0.0, ptr(comb), ptr(dw), ptr(ws), ws.numel(), _st(dy)),
+              "tcx_conv_wgrad_h2")
+        return dw
     check(L.tcx_conv_wgrad(ptr(x1), ptr(x2), B, H, W, C1, C2, ptr(dy), Cout, ks, stride, pad, circular, 0.0, ptr(dw),
                            ptr(ws), ws.numel(), _st(dy)), "tcx_conv_wgrad")
     return dw
@@ -204,8 +239,10 @@ class Conv2dFn(torch.autograd.Function):
         x1, x2, w, b, resid = _c(x1), _c(x2), _c(w), _c(b), _c(resid)
         Cout, Cin, ks, _ = w.shape
         wpk, kpad, cpad = _pack_conv(w)
-        y = _conv_fwd(x1, x2, wpk, kpad, cpad, b, None, resid, Cout, ks, stride, pad, circular)
+        keep = []
+        y = _conv_fwd(x1, x2, wpk, kpad, cpad, b, None, resid, Cout, ks, stride, pad, circular, keep=keep)
         ctx.save_for_backward(x1, x2, w)
+        ctx.xrec = keep[0] if keep else None  # the split path's h2 records of x for the weight gradient
         ctx.cfg = (stride, pad, circular, b is not None, resid is not None)
         return y
 
@@ -217,12 +254,15 @@ class Conv2dFn(torch.autograd.Function):
         Cout, Cin, ks, _ = w.shape
         B, H, W, C1 = x1.shape
         dx1 = dx2 = dw = db = dr = None
+        dyrec = []  # dY's h2 records, made once by the first split data-gradient conv and reused
         if ctx.needs_input_grad[0]:
-            dx1 = _conv_dgrad(dy, w, 0, C1, stride, pad, circular, H, W)
+            dx1 = _conv_dgrad(dy, w, 0, C1, stride, pad, circular, H, W, keep=dyrec)
         if x2 is not None and ctx.needs_input_grad[1]:
-            dx2 = _conv_dgrad(dy, w, C1, Cin - C1, stride, pad, circular, H, W)
+            dx2 = _conv_dgrad(dy, w, C1, Cin - C1, stride, pad, circular, H, W, keep=dyrec)
         if ctx.needs_input_grad[2]:
-            dw = _conv_wgrad(x1, x2, dy, Cout, ks, stride, pad, circular)
+            dw = _conv_wgrad(x1, x2, dy, Cout, ks, stride, pad, circular, xrec=ctx.xrec,
+                             dyrec=dyrec[0] if dyrec else None)
+        ctx.xrec = None
         if has_b and ctx.needs_input_grad[3]:
             db = _colsum_total(dy, dy.numel() // Cout, Cout)
         if has_r and ctx.needs_input_grad[4]:
