@@ -4,7 +4,7 @@ Records hold bf16 halves (hi = bf16(v), lo = bf16(v - hi)); every product is ONE
 v_mfma_f32_32x32x16_bf16 of the hi halves with fp32 accumulation.  Checks:
   * the writers produce exactly torch's round-to-nearest-even bf16 of the value (hi) and of the
     residual (lo);
-  * each bf16 kernel (k_conv3g at 32/64/128-pixel rows with and without the GroupNorm+SiLU prologue,
+  * each bf16 kernel (k_conv3g at 16/32/64/128-pixel rows with and without the GroupNorm+SiLU prologue,
     the im2col kernel, k_conv4s2h, the split attention) against a float64 reference computed on the
     SAME bf16-rounded operands: then only the fp32 accumulation differs (5e-6 of the output scale);
     the attention additionally rounds P and its output to bf16 (1e-2);
@@ -103,7 +103,8 @@ def conv_ref(x, w, b, stride, pad):
     (2, 96, 0, 64, 96, 3, 1, True),      # k_conv3g, 64-px rows
     (2, 96, 96, 32, 96, 3, 1, True),     # k_conv3g, two sources, 32-px rows
     (1, 96, 0, 128, 96, 3, 1, True),     # k_conv3g, 128-px rows
-    (2, 64, 0, 16, 64, 3, 1, True),      # 16-px rows: the im2col kernel (no bf16 k_conv3p)
+    (2, 64, 0, 16, 96, 3, 1, True),      # k_conv3g, 16-px rows (mid block)
+    (2, 64, 0, 16, 64, 3, 1, False),     # no fragment copy: the im2col kernel (no bf16 k_conv3p)
     (2, 96, 0, 64, 96, 4, 2, False),     # k_conv4s2h (ds1 at 64 -> 32)
     (2, 192, 0, 16, 576, 1, 1, False),   # 1x1 (qkv): the im2col kernel
 ])

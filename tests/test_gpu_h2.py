@@ -178,6 +178,7 @@ def rand_tabs(B, C, seed):
     (2, 96, 96, 64, True, False),    # up1_1 / down1_1 (64^2)
     (2, 192, 192, 32, True, False),  # down2_1 (32^2)
     (2, 96, 96, 32, True, False),    # up2_1
+    (2, 192, 192, 16, True, False),  # mid_1 (16^2 rows)
     (1, 96, 96, 128, True, False),   # config 5's 128^2 rows
     (2, 64, 96, 32, False, False),   # zero padding: the padded ring is 0 AFTER the transform
     (2, 96, 96, 64, True, True),     # concat: source 1 h2, source 2 fp32 + tables
@@ -223,9 +224,9 @@ def test_conv_h2_gn_prologue_gn_stats_and_range_flag():
 
 
 def test_conv_h2_pro_rejects_uncovered_shape():
-    """A prologue on a shape k_conv3g does not cover (16x16 rows) is an error, not a silent drop."""
+    """A prologue on a shape k_conv3g does not cover (8x8 rows) is an error, not a silent drop."""
     from toycrystals_amd._lib import TcxError
-    x = rng.standard_normal((2, 96, 16, 16))
+    x = rng.standard_normal((2, 96, 8, 8))
     w = rng.standard_normal((96, 96, 3, 3)) / 30
     with pytest.raises(TcxError, match="prologue"):
         run_conv_h2_pro(x, w, np.zeros(96), True, rand_tabs(2, 96, 1))

@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvParams p) {
     }
     }  // !SPL
 
-    conv_epilogue<NT, (SPL != 0), 4>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(&As[0][0]));
+    conv_epilogue<NT, SPL, 4>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(&As[0][0]));
 }
 
 template <int NT>
@@ -643,7 +643,7 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
     if (conv3g_applies(p, cout_pad)) return launch_conv3g(p, cout_pad, (hipStream_t)stream);
     TCX_REQUIRE(!pro_scale1 && !pro_scale2,
                 "tcx_conv2d_h2: the GroupNorm+SiLU prologue needs k_conv3g: the fragment-ordered weights "
-                "(tcx_pack_conv_weight_h2_frag) and a 3x3 stride-1 conv with W in {32, 64, 128}, Cin %% 32 == 0, "
+                "(tcx_pack_conv_weight_h2_frag) and a 3x3 stride-1 conv with W in {16, 32, 64, 128}, Cin %% 32 == 0, "
                 "Cin <= 384, Cout padded to 96k");
     if (!p.bf && conv3h_applies(p, cout_pad)) return launch_conv3h(p, cout_pad, (hipStream_t)stream);
     if (conv4s2h_applies(p, cout_pad)) return launch_conv4s2h(p, cout_pad, (hipStream_t)stream);

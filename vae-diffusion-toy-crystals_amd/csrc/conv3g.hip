@@ -369,8 +369,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
 
     __syncthreads();  // LDS -> epilogue reduction scratch
     double* red = reinterpret_cast<double*>(sm);
-    conv_epi_store<NT, true, RT * NW>(p, acc[0], m0, n0, RT * wv, lane, red);
-    conv_epi_store<NT, true, RT * NW>(p, acc[1], m0, n0, RT * wv + 1, lane, red);
+    conv_epi_store<NT, BF ? 2 : 1, RT * NW>(p, acc[0], m0, n0, RT * wv, lane, red);
+    conv_epi_store<NT, BF ? 2 : 1, RT * NW>(p, acc[1], m0, n0, RT * wv + 1, lane, red);
     if (p.gn) {
         __syncthreads();
         conv_epi_gn<NT, RT * NW>(p, m0, n0, tid, NTHR, red);
@@ -441,7 +441,7 @@ bool conv3g_enabled() {
 }
 
 bool conv3g_covers(int H, int W, int Cin, int cout_pad) {
-    if (!conv3g_enabled() || !(W == 32 || W == 64 || W == 128)) return false;
+    if (!conv3g_enabled() || !(W == 16 || W == 32 || W == 64 || W == 128)) return false;
     const int tp = g_tp(g_nw(W));
     return H % (tp / W) == 0 && (H * W) % tp == 0 && Cin % 32 == 0 && Cin <= 384 && cout_pad % 96 == 0;
 }
@@ -459,6 +459,7 @@ int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st) {
     int rc;
     if (p.W == 64) rc = launch3g<64>(p, st);
     else if (p.W == 32) rc = launch3g<32>(p, st);
+    else if (p.W == 16) rc = launch3g<16>(p, st);
     else rc = launch3g<128>(p, st);
     prof_end(st, 2.0 * (double)p.M * p.Cout * 9 * p.Cin);
     return rc;

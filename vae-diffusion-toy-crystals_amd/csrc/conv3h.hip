@@ -255,14 +255,14 @@ __global__ __launch_bounds__(64 * NW, RT == 1 ? 2 : 1) void k_conv3h(ConvParams 
     }
     __syncthreads();  // the halo buffers become the epilogue's reduction scratch
     if constexpr (RT == 1) {
-        conv_epilogue<NT, true, NW>(p, acc[0], m0, n0, wv, tid, reinterpret_cast<double*>(sm));
+        conv_epilogue<NT, 1, NW>(p, acc[0], m0, n0, wv, tid, reinterpret_cast<double*>(sm));
     } else {
         // two explicit calls, not a loop: a rolled loop over the (large) inlined epilogue would index
         // acc dynamically and keep the whole accumulator array in scratch, stored after every tap
         double* red = reinterpret_cast<double*>(sm);
         static_assert(RT == 2, "RT is 1 or 2");
-        conv_epi_store<NT, true, RT * NW>(p, acc[0], m0, n0, RT * wv, lane, red);
-        conv_epi_store<NT, true, RT * NW>(p, acc[1], m0, n0, RT * wv + 1, lane, red);
+        conv_epi_store<NT, 1, RT * NW>(p, acc[0], m0, n0, RT * wv, lane, red);
+        conv_epi_store<NT, 1, RT * NW>(p, acc[1], m0, n0, RT * wv + 1, lane, red);
         if (p.gn) {
             __syncthreads();
             conv_epi_gn<NT, RT * NW>(p, m0, n0, tid, NTHR, red);
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3p(ConvParams p) {
         }
     }
     __syncthreads();
-    conv_epilogue<NT, true, NW>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
+    conv_epilogue<NT, 1, NW>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -651,8 +651,8 @@ __global__ __launch_bounds__(256, 1) void k_conv3w(ConvParams p) {
 
     __syncthreads();  // halo buffers -> epilogue scratch
     double* red = reinterpret_cast<double*>(sm);
-    conv_epi_store<NT, true, 2 * NW>(p, acc[0], m0, n0, 2 * wv, lane, red);
-    conv_epi_store<NT, true, 2 * NW>(p, acc[1], m0, n0, 2 * wv + 1, lane, red);
+    conv_epi_store<NT, 1, 2 * NW>(p, acc[0], m0, n0, 2 * wv, lane, red);
+    conv_epi_store<NT, 1, 2 * NW>(p, acc[1], m0, n0, 2 * wv + 1, lane, red);
     if (p.gn) {
         __syncthreads();
         conv_epi_gn<NT, 2 * NW>(p, m0, n0, tid, NTHR, red);

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2h(ConvParams p) {
         }
     }
     __syncthreads();  // the halo buffer becomes the epilogue's reduction scratch
-    conv_epilogue<NT, true, DS_NW>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
+    conv_epilogue<NT, BF ? 2 : 1, DS_NW>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
 }
 
 template <int Wo>

@@ -109,13 +109,15 @@ __device__ __forceinline__ void bilin_axis(int d, int n, int& i0, int& i1, float
 // conv_epi_store: one wave's 32 x 32*NT block (NW = waves of 32 rows in the tile, virtual waves
 // when a wave owns several row blocks); conv_epi_gn: the per-128-pixel-group reduction of the
 // partials in `red`, after a barrier.
-template <int NT, bool SPL, int NW>
+// SPL: 0 = fp32 MFMA accumulators (an h2 output follows p.bf), 1 = f16x3, 2 = bf16 single product
+template <int NT, int SPL, int NW>
 __device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc)[NT], int m0, int n0, int wv,
                                                int lane, double* red) {
     constexpr int BN = 32 * NT;
     const int li = lane & 31;
     const int lh = lane >> 5;
     const bool gn = p.gn != nullptr;
+    const bool bf = SPL == 2 || (SPL == 0 && p.bf != 0);  // compile-time for the split kernels
     // Fast path (every U-Net conv): dense NHWC output, whole tiles inside one image, no per-batch
     // bias, output columns all valid, 32-bit element offsets; no per-row index arithmetic beyond
     // one scalar multiple of Cout per accumulator row, GroupNorm partials summed per lane in fp32
@@ -143,13 +145,13 @@ __device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc
                 if (p.out_h2) {
                     // lane pairs (2j, 2j+1) of an 8-channel group swap halves: the even lane
                     // stores the hi pair, the odd lane the lo pair (one dword each)
-                    const unsigned sp = split1x(v, p.bf);
+                    const unsigned sp = split1x(v, bf);
                     const bool odd = (li & 1) != 0;
                     const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
                     const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
                     const int pe = e - co + (co & ~7);  // the 8-channel group's first element
                     *reinterpret_cast<unsigned*>(yb + (size_t)pe * 4 + (odd ? 16 : 0) + 2 * ((co & 7) & ~1)) = word;
-                    bad = bad || (!p.bf && h2_bad(v));
+                    bad = bad || (!bf && h2_bad(v));
                 } else {
                     p.y[e] = v;
                 }
@@ -215,7 +217,7 @@ __device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc
             if (p.out_h2) {
                 // h2 record of the pixel: lane pairs (2j, 2j+1) of an 8-channel group swap halves so
                 // the even lane stores the hi pair and the odd lane the lo pair (one dword each)
-                const unsigned sp = split1x(v, p.bf);
+                const unsigned sp = split1x(v, bf);
                 const bool odd = (li & 1) != 0;
                 const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
                 const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
@@ -223,7 +225,7 @@ __device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc
                 const int c8 = coc & ~7, j = (coc & 7) & ~1;
                 if (ok[r]) {
                     *reinterpret_cast<unsigned*>(reinterpret_cast<char*>(p.y) + pe * 4 + (size_t)c8 * 4 + (odd ? 16 : 0) + 2 * j) = word;
-                    bad = bad || (!p.bf && h2_bad(v));
+                    bad = bad || (!bf && h2_bad(v));
                 }
             } else if (ok[r]) {
                 p.y[oidx[r]] = v;
@@ -272,7 +274,7 @@ __device__ __forceinline__ void conv_epi_gn(const ConvParams& p, int m0, int n0,
     }
 }
 
-template <int NT, bool SPL, int NW>
+template <int NT, int SPL, int NW>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x16 (&acc)[NT], int m0, int n0, int wv,
                                               int tid, double* red) {
     conv_epi_store<NT, SPL, NW>(p, acc, m0, n0, wv, tid & 63, red);

@@ -638,16 +638,17 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         pro[7] = can(C, 0, P.P1);
         pro[9] = can(C, 0, P.P0);
     }
-    // Split path: a GroupNorm+SiLU whose only consumer is a 3x3 conv on k_conv3g (rows of 32/64/128
+    // Split path: a GroupNorm+SiLU whose only consumer is a 3x3 conv on k_conv3g (rows of 16/32/64/128
     // pixels) is applied by that conv's halo staging from the fp32 tensor (tcx_conv2d_h2_pro), so the
-    // normalised tensor is never written: norms 0, 2, 7, 9 (down1.net.1, down2.net.1, up2.net.1,
-    // up1.net.1 feeding down1/down2/up2/up1 .net.3).  The skip tensors h1/h2 (norms 1, 3: read by a
-    // 4x4/s2 conv AND an up-path concat) and the 16x16 mid block keep the in-place h2 apply pass.
+    // normalised tensor is never written: norms 0, 2, 4, 7, 9 (down1.net.1, down2.net.1, mid.net.1,
+    // up2.net.1, up1.net.1 feeding the .net.3 conv of their block).  The skip tensors h1/h2 (norms 1,
+    // 3: read by a 4x4/s2 conv AND an up-path concat) keep the in-place h2 apply pass.
     if (net->precision >= 1) {
         pro[0] = net->down1_1.whf && conv3g_covers(H, W, C, net->down1_1.cout_pad);
         pro[2] = net->down2_1.whf && conv3g_covers(H1, W1, C2, net->down2_1.cout_pad);
         pro[7] = net->up2_1.whf && conv3g_covers(H1, W1, C, net->up2_1.cout_pad);
         pro[9] = net->up1_1.whf && conv3g_covers(H, W, C, net->up1_1.cout_pad);
+        pro[4] = net->mid_1.whf && conv3g_covers(H2, W2, C2, net->mid_1.cout_pad);  // mid.net.1 -> mid.net.3
     }
     auto SC = [&](int i) -> const float* { return pro[i] ? P.sc(i) : nullptr; };
     auto SH = [&](int i) -> const float* { return pro[i] ? P.sh(i) : nullptr; };
