@@ -28,7 +28,7 @@ def rup(v, a=32):
     return (v + a - 1) // a * a
 
 
-def bench(name, H, C1, C2, Co, ks, s, pad, ups, reps=20, gn=True):
+def bench(name, H, C1, C2, Co, ks, s, pad, ups, reps=20, gn=os.environ.get("GN", "1") == "1"):
     Cin = C1 + C2
     kpad, cpad = rup(ks * ks * Cin), rup(Co)
     x1 = torch.randn(Bt, H, H, C1, device="cuda")

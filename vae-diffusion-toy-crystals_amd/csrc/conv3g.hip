@@ -369,8 +369,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
 
     __syncthreads();  // LDS -> epilogue reduction scratch
     double* red = reinterpret_cast<double*>(sm);
-    conv_epi_store<NT, BF ? 2 : 1, RT * NW>(p, acc[0], m0, n0, RT * wv, lane, red);
-    conv_epi_store<NT, BF ? 2 : 1, RT * NW>(p, acc[1], m0, n0, RT * wv + 1, lane, red);
+    conv_epi_store_rt<NT, BF ? 2 : 1, RT * NW, RT>(p, acc, m0, n0, RT * wv, lane, red);
     if (p.gn) {
         __syncthreads();
         conv_epi_gn<NT, RT * NW>(p, m0, n0, tid, NTHR, red);
@@ -452,12 +451,17 @@ bool conv3g_applies(const ConvParams& p, int cout_pad) {
            p.osy == 1 && p.osx == 1;
 }
 
+// conv3l.hip: the same conv with the B fragments staged once per workgroup in an LDS ring
+bool conv3l_takes(const ConvParams& p);
+int launch_conv3l(const ConvParams& p, hipStream_t st);
+
 int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st) {
     p.n_nblk = cout_pad / 96;
     if (p.M == 0) return TCX_OK;
     prof_begin(st);
     int rc;
-    if (p.W == 64) rc = launch3g<64>(p, st);
+    if (conv3l_takes(p)) rc = launch_conv3l(p, st);
+    else if (p.W == 64) rc = launch3g<64>(p, st);
     else if (p.W == 32) rc = launch3g<32>(p, st);
     else if (p.W == 16) rc = launch3g<16>(p, st);
     else rc = launch3g<128>(p, st);

@@ -261,8 +261,7 @@ __global__ __launch_bounds__(64 * NW, RT == 1 ? 2 : 1) void k_conv3h(ConvParams 
         // acc dynamically and keep the whole accumulator array in scratch, stored after every tap
         double* red = reinterpret_cast<double*>(sm);
         static_assert(RT == 2, "RT is 1 or 2");
-        conv_epi_store<NT, 1, RT * NW>(p, acc[0], m0, n0, RT * wv, lane, red);
-        conv_epi_store<NT, 1, RT * NW>(p, acc[1], m0, n0, RT * wv + 1, lane, red);
+        conv_epi_store_rt<NT, 1, RT * NW, 2>(p, reinterpret_cast<f32x16(&)[2][NT]>(acc), m0, n0, RT * wv, lane, red);
         if (p.gn) {
             __syncthreads();
             conv_epi_gn<NT, RT * NW>(p, m0, n0, tid, NTHR, red);
@@ -651,8 +650,7 @@ __global__ __launch_bounds__(256, 1) void k_conv3w(ConvParams p) {
 
     __syncthreads();  // halo buffers -> epilogue scratch
     double* red = reinterpret_cast<double*>(sm);
-    conv_epi_store<NT, 1, 2 * NW>(p, acc[0], m0, n0, 2 * wv, lane, red);
-    conv_epi_store<NT, 1, 2 * NW>(p, acc[1], m0, n0, 2 * wv + 1, lane, red);
+    conv_epi_store_rt<NT, 1, 2 * NW, 2>(p, reinterpret_cast<f32x16(&)[2][NT]>(acc), m0, n0, 2 * wv, lane, red);
     if (p.gn) {
         __syncthreads();
         conv_epi_gn<NT, 2 * NW>(p, m0, n0, tid, NTHR, red);

@@ -1,0 +1,450 @@
+// k_conv3l: the 3x3 stride-1 circular conv of the U-Net at rows of 32 / 64 pixels (every _ConvBlock
+// conv and us*_conv at 64^2 / 32^2: /root/reference/src/toycrystals/models/sde_score_model.py:102,
+// 105,218,222) on the f16x3 split path, with the optional GroupNorm + SiLU prologue (:103-107) of
+// k_conv3g.  Same tiles, accumulators, halo pipeline and epilogue as k_conv3g (conv3g.hip); what
+// changes is where the B (weight) fragments come from.
+//
+// Why: k_conv3g loads every B fragment straight from global memory into each wave's registers, so
+// the 4 waves of a workgroup fetch the same 6 KB per tap through the vector-memory return path.
+// PMC on up1_1 (profiles/r02_ze_*): TD busy 89 %, TA busy 67 % of the kernel's cycles, MFMA pipe
+// busy 48 % — the load path, not the MFMA, sets the pace.  Here each workgroup stages a tap pair's
+// 12 KB of fragments ONCE (3 dwordx4 loads per wave, written with ds_write_b128 into a two-pair LDS
+// ring) and every wave reads its B fragments with ds_read_b128: the load-path bytes per tap drop
+// from 24 KB to 6 KB per workgroup, the LDS gets 6 extra conflict-free b128 reads per 18 MFMAs.
+//
+// Tap c (0 .. 9 cpt - 1, chunk j = c / 9, tap t = c % 9) of one wave:
+//   ds_read B(c+1) -> register set (c+1)&1 | read A1(t) | 9 MFMAs row block 0 | read A0(t+1) |
+//   9 MFMAs row block 1 (+ GN+SiLU of one halo unit) | halo unit load / store (as k_conv3g) |
+//   c even: write the staged pair c/2+1 into ring slot (c/2+1)&1, load pair c/2+2, barrier.
+// Pair k = taps {2k, 2k+1} is written during tap 2k-2, made visible by the barrier after it, read
+// during taps 2k-1 and 2k (prefetch one tap ahead), and its slot is rewritten during tap 2k+2, after
+// the barrier that ends tap 2k.  One barrier per two taps, which also orders the halo double buffer
+// (halo j+1 is stored during taps 2-5 of chunk j; an even tap lies between tap 5 and tap 8).
+//
+// LDS (one array): halo [2][NPX][64 B] with the 16-B pieces of a pixel XOR-swizzled by (col >> 2) & 3
+// (conflict-free ds_read_b128 of 32 consecutive pixels at any tap offset, and conflict-free
+// ds_write_b128 of 8 consecutive pixels), the B ring [2 pairs][2 taps][3 n][hi, lo][64 lanes][16 B]
+// = 24 KB, the GroupNorm tables [2][Cin]: 78 KB at W = 64, Cin = 384 — two workgroups per CU.
+#include "conv_common.hpp"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace tcx {
+namespace {
+
+constexpr int L_KC = 16;     // input channels per chunk
+constexpr int L_NT = 3;      // 32-channel accumulator tiles per wave (96 output channels)
+constexpr int L_NW = 4;      // waves per workgroup (256-pixel tiles)
+constexpr int L_TP = 64 * L_NW;
+constexpr int L_PAIR = 2 * L_NT * 2 * 1024;  // bytes of B fragments per tap pair (12 KB)
+
+__host__ __device__ constexpr int l_npx(int W) { return (L_TP / W + 2) * (W + 2); }
+__host__ __device__ constexpr int l_units(int W) { return (2 * l_npx(W) + 64 * L_NW - 1) / (64 * L_NW); }
+constexpr size_t conv3l_lds_bytes(int W, int Cin) {
+    return (size_t)2 * l_npx(W) * 64 + 2 * (size_t)L_PAIR + 2 * (size_t)Cin * sizeof(float);
+}
+
+__device__ __forceinline__ float l_silu(float v, float sc, float sh) {
+    const float y = fmaf(v, sc, sh);
+    return y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * y));
+}
+
+// diagnostic timestamps (TCX_CONV3L_DBG=1, W = 64 without prologue only): per workgroup, wave 0,
+// s_memrealtime (100 MHz) at entry, after the prologue barrier, after the last tap, at exit, and the
+// hardware id (XCC / SE / CU / slot) of the workgroup
+constexpr int L_NSTAMP = 8192;
+__device__ unsigned long long l_stamps[L_NSTAMP][5];
+
+// PRO: 0 = every source h2; 1 = every source fp32 + GroupNorm table; 2 = per source at run time.
+// DBG: 0 product; 1 timestamps; 2 timestamps and no output stores (diagnostics only)
+template <int W, int PRO, int DBG = 0>
+__global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
+    constexpr int RT = 2, NT = L_NT, BN = 32 * NT, NTHR = 64 * L_NW;
+    constexpr int W2 = W + 2;
+    constexpr int NPX = l_npx(W);
+    constexpr int NU = 2 * NPX;   // 8-channel halo units per chunk
+    constexpr int UPT = l_units(W);
+    constexpr int HB = NPX * 64;  // bytes per halo buffer
+    constexpr int RING = 2 * HB;  // byte offset of the B ring
+    constexpr int TAB = RING + 2 * L_PAIR;
+    // row block 1 of a wave: 32 pixels further in the row (W = 64) or the next row (W = 32); the
+    // swizzle term depends only on the column, so both are an immediate offset from row block 0
+    constexpr int RT1 = W == 64 ? 32 * 64 : W2 * 64;
+    static_assert(W == 32 || W == 64, "k_conv3l: rows of 32 or 64 pixels");
+    static_assert(UPT <= 4, "halo units per thread: stores must finish by tap 5");
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    char* const smc = reinterpret_cast<char*>(sm);
+    float* const Ts = reinterpret_cast<float*>(smc + TAB);  // [2][Cin]: scale, shift of this tile's image
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar offsets)
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mblk = tile / p.n_nblk;
+    const int nblk = tile - mblk * p.n_nblk;
+    const int m0 = mblk * L_TP, n0 = nblk * BN;
+    const int b = m0 / p.HoWo;
+    const int r0 = (m0 - b * p.HoWo) / W;
+    const int bs = p.bmod > 0 ? b % p.bmod : b;
+    const int H = p.H;
+    const int Cin = p.Cin;
+    const int cpt = Cin / L_KC;  // chunks (even: Cin % 32 == 0)
+    const int nch = 9 * cpt;
+    const bool gn1 = PRO == 1 || (PRO == 2 && p.sc1 != nullptr);
+    const bool gn2 = PRO == 1 || (PRO == 2 && p.sc2 != nullptr);
+
+    const __amdgpu_buffer_rsrc_t r1 = mk_rsrc(p.x1, p.bytes1);
+    const __amdgpu_buffer_rsrc_t r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
+    const __amdgpu_buffer_rsrc_t rw = mk_rsrc(reinterpret_cast<const float*>(p.wf), p.bytesw);
+    auto stamp = [&](int slot) {
+        if constexpr (DBG != 0) {
+            if (tid == 0 && blockIdx.x < L_NSTAMP) l_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
+    stamp(0);
+
+    if (PRO != 0 && (gn1 || gn2)) {
+        for (int c = tid; c < Cin; c += NTHR) {
+            const bool s1 = c < p.C1;
+            const float* sc = s1 ? p.sc1 : p.sc2;
+            const float* sh = s1 ? p.sh1 : p.sh2;
+            const int cc = s1 ? c : c - p.C1;
+            const int Cs = s1 ? p.C1 : p.C2;
+            Ts[c] = sc ? sc[(size_t)b * Cs + cc] : 1.f;
+            Ts[Cin + c] = sh ? sh[(size_t)b * Cs + cc] : 0.f;
+        }
+    }
+
+    // ---- halo plan: unit u = tid + NTHR i -> halo pixel u % NPX, 8-channel group u / NPX; the
+    // unit's hi piece (logical piece 2g) lands at byte 64 s + 16 ((2g) ^ sw(col)), its lo piece
+    // (2g + 1) at that address ^ 16
+    const int rowb = p.C1 * 4;
+    int hoff[UPT];  // source byte offset of the unit
+    int hdst[UPT];  // LDS byte offset of the unit's hi piece in buffer 0
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+        const int u = tid + NTHR * i;
+        const int hp = u < NPX ? u : u - NPX;
+        const int g = u < NPX ? 0 : 1;
+        const int hr = hp / W2, hc = hp - hr * W2;
+        const int y = wrap_idx(r0 + hr - 1, H), x = wrap_idx(hc - 1, W);
+        hoff[i] = u < NU ? ((bs * H + y) * W + x) * rowb + g * 32 : kOOB;
+        hdst[i] = hp * 64 + 16 * ((2 * g) ^ ((hc >> 2) & 3));
+    }
+    float4 hv[UPT][2];
+    auto src_of = [&](int j, __amdgpu_buffer_rsrc_t& rs, int& cc) {
+        const int ci0 = j * L_KC;
+        const bool s1 = ci0 < p.C1;
+        cc = (s1 ? ci0 : ci0 - p.C1) * 4;
+        rs = s1 ? r1 : r2;
+        return s1 ? gn1 : gn2;
+    };
+    auto unit_load = [&](int j, int i) {
+        __amdgpu_buffer_rsrc_t rs;
+        int cc;
+        src_of(j, rs, cc);
+        hv[i][0] = bld4(rs, hoff[i], cc);
+        hv[i][1] = bld4(rs, hoff[i], cc + 16);
+    };
+    auto unit_transform = [&](int j, int i) {
+        if constexpr (PRO == 0) return;
+        __amdgpu_buffer_rsrc_t rs;
+        int cc;
+        const bool gn = src_of(j, rs, cc);
+        if (PRO == 2 && !gn) return;
+        const int u = tid + NTHR * i;
+        const int c = j * L_KC + (u < NPX ? 0 : 8);
+        const float4 s0 = *reinterpret_cast<const float4*>(&Ts[c]);
+        const float4 s1v = *reinterpret_cast<const float4*>(&Ts[c + 4]);
+        const float4 h0 = *reinterpret_cast<const float4*>(&Ts[Cin + c]);
+        const float4 h1 = *reinterpret_cast<const float4*>(&Ts[Cin + c + 4]);
+        const float v[8] = {l_silu(hv[i][0].x, s0.x, h0.x), l_silu(hv[i][0].y, s0.y, h0.y),
+                            l_silu(hv[i][0].z, s0.z, h0.z), l_silu(hv[i][0].w, s0.w, h0.w),
+                            l_silu(hv[i][1].x, s1v.x, h1.x), l_silu(hv[i][1].y, s1v.y, h1.y),
+                            l_silu(hv[i][1].z, s1v.z, h1.z), l_silu(hv[i][1].w, s1v.w, h1.w)};
+        unsigned h[4], l[4];
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const unsigned a = split1(v[2 * k]), bb = split1(v[2 * k + 1]);
+            h[k] = (a & 0xffffu) | (bb << 16);
+            l[k] = (a >> 16) | (bb & 0xffff0000u);
+            bad = bad || h2_bad(v[2 * k]) || h2_bad(v[2 * k + 1]);
+        }
+        hv[i][0] = make_float4(__uint_as_float(h[0]), __uint_as_float(h[1]), __uint_as_float(h[2]), __uint_as_float(h[3]));
+        hv[i][1] = make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), __uint_as_float(l[2]), __uint_as_float(l[3]));
+        h2_flag(p.ovf, bad);
+    };
+    auto unit_write = [&](int i, int buf) {
+        const int u = tid + NTHR * i;
+        if (!((i + 1) * NTHR <= NU || u < NU)) return;
+        *reinterpret_cast<float4*>(smc + buf * HB + hdst[i]) = hv[i][0];
+        *reinterpret_cast<float4*>(smc + buf * HB + (hdst[i] ^ 16)) = hv[i][1];
+    };
+
+    // ---- A fragment addresses: lane (li, lh) of row block 0 at tap (dy, dx) reads pixel slot
+    // s = (rr + dy) W2 + cc + dx, logical pieces 2 lh (hi) and 2 lh + 1 (lo)
+    int xa[3];
+    {
+        const int mloc = (wv * RT) * 32 + li;
+        const int rr = mloc / W, cc = mloc % W;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+            xa[dx] = (rr * W2 + cc + dx) * 64 + 16 * ((2 * lh) ^ (((cc + dx) >> 2) & 3));
+    }
+    f32x16 acc[RT][NT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[rt][n] = (f32x16){};
+    h8 a_h[RT], a_l[RT], b_h[2][NT], b_l[2][NT];
+    auto rd_a = [&](int rt, int t, int hb) {
+        const int dy = t / 3, dx = t - 3 * (t / 3);
+        const int off = hb * HB + rt * RT1 + dy * W2 * 64;
+        a_h[rt] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + xa[dx] + off));
+        a_l[rt] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + (xa[dx] ^ 16) + off));
+    };
+    // B(c) from the ring: pair slot (c >> 1) & 1, tap c & 1 of the pair; fragment n hi at +2 KB n
+    const int bl = lane * 16;
+    auto rd_b = [&](int s, int c) {
+        const char* B = smc + RING + ((c >> 1) & 1) * L_PAIR + (c & 1) * (L_PAIR / 2) + bl;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            b_h[s][n] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(B + n * 2048));
+            b_l[s][n] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(B + n * 2048 + 1024));
+        }
+    };
+    // staging of pair k: wave wv moves KB [3 wv, 3 wv + 3) of the pair's 12 KB
+    float4 bst[3];
+    const int npair = nch / 2;
+    const int bsl = bl + wv * 3072;  // this wave's bytes of a pair (VGPR offset)
+    auto ld_pair = [&](int k) {
+        k = k < npair ? k : npair - 1;
+        const int base = (nblk * nch + 2 * k) * NT * 2048;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) bst[i] = bld4(rw, bsl, base + i * 1024);
+    };
+    auto wr_pair = [&](int k) {
+        char* d = smc + RING + (k & 1) * L_PAIR + wv * 3072 + bl;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) *reinterpret_cast<float4*>(d + i * 1024) = bst[i];
+    };
+    auto mf = [&](int rt, int s) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[rt], b_l[s][n], acc[rt][n], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_l[rt], b_h[s][n], acc[rt][n], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[rt], b_h[s][n], acc[rt][n], 0, 0, 0);
+    };
+    // row-block-1 MFMAs with the GN+SiLU(+split) of halo unit i placed one value per gap (k_conv3g)
+    auto mf1_transform = [&](int j, int i, int s) {
+        const int u = tid + NTHR * i;
+        const int c = j * L_KC + (u < NPX ? 0 : 8);
+        const float4 s0 = *reinterpret_cast<const float4*>(&Ts[c]);
+        const float4 s1v = *reinterpret_cast<const float4*>(&Ts[c + 4]);
+        const float4 h0 = *reinterpret_cast<const float4*>(&Ts[Cin + c]);
+        const float4 h1 = *reinterpret_cast<const float4*>(&Ts[Cin + c + 4]);
+        const float xs[8] = {hv[i][0].x, hv[i][0].y, hv[i][0].z, hv[i][0].w, hv[i][1].x, hv[i][1].y, hv[i][1].z,
+                             hv[i][1].w};
+        const float scs[8] = {s0.x, s0.y, s0.z, s0.w, s1v.x, s1v.y, s1v.z, s1v.w};
+        const float shs[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        unsigned sp[8];
+        bool bad = false;
+        const h8* As[3] = {&a_h[1], &a_l[1], &a_h[1]};
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int g = k / 3, n = k - 3 * (k / 3);
+            const h8& bb = g == 0 ? b_l[s][n] : b_h[s][n];
+            acc[1][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*As[g], bb, acc[1][n], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (k < 8) {
+                const float v = l_silu(xs[k], scs[k], shs[k]);
+                bad = bad || h2_bad(v);
+                sp[k] = split1(v);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        unsigned h[4], l[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            h[k] = (sp[2 * k] & 0xffffu) | (sp[2 * k + 1] << 16);
+            l[k] = (sp[2 * k] >> 16) | (sp[2 * k + 1] & 0xffff0000u);
+        }
+        hv[i][0] = make_float4(__uint_as_float(h[0]), __uint_as_float(h[1]), __uint_as_float(h[2]), __uint_as_float(h[3]));
+        hv[i][1] = make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), __uint_as_float(l[2]), __uint_as_float(l[3]));
+        h2_flag(p.ovf, bad);
+    };
+
+    // ---- prologue: tables, pair 0 in the ring, pair 1 staged, halo 0 in LDS; B(0), A0(0) in registers
+    ld_pair(0);
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) unit_load(0, i);
+    if (gn1 || gn2) __syncthreads();  // Ts before the first transform
+    wr_pair(0);
+    ld_pair(1);
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+        unit_transform(0, i);
+        unit_write(i, 0);
+    }
+    __syncthreads();
+    stamp(1);
+    rd_b(0, 0);
+    rd_a(0, 0, 0);
+
+    // one tap: T compile-time tap index, S = c & 1 (register set of B(c)), HBc halo buffer of chunk j
+    auto iter = [&](int j, auto T, auto S, auto HBc) {
+        constexpr int t = decltype(T)::value;
+        constexpr int s = decltype(S)::value;
+        constexpr int hb = decltype(HBc)::value;
+        const int c = 9 * j + t;
+        const bool more = j + 1 < cpt;
+        rd_b(s ^ 1, c + 1);
+        if (t != 8) rd_a(1, t, hb);  // A1(8) was read during tap 7
+        __builtin_amdgcn_sched_barrier(0);
+        mf(0, s);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t == 8) rd_a(0, 0, hb ^ 1);
+        else rd_a(0, t + 1, hb);
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr bool st = t >= 2 && t < UPT + 2;  // this tap stores halo unit t - 2 of chunk j+1
+        if constexpr (st && PRO == 1) {
+            mf1_transform(more ? j + 1 : j, t - 2, s);
+        } else {
+            mf(1, s);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (t == 7) rd_a(1, 8, hb);
+        if constexpr (t < UPT) unit_load(more ? j + 1 : j, t);
+        if constexpr (st) {
+            if constexpr (PRO == 2) unit_transform(more ? j + 1 : j, t - 2);
+            unit_write(t - 2, hb ^ 1);
+        }
+        if constexpr (s == 0) {  // c even: pair c/2 + 1 into the ring, load pair c/2 + 2, barrier
+            wr_pair((c >> 1) + 1);
+            ld_pair((c >> 1) + 2);
+            __syncthreads();
+        }
+    };
+    auto nine = [&](int j, auto E) {  // E = (9 j) & 1 = j & 1: register set of tap 0 = halo buffer
+        using O = std::integral_constant<int, decltype(E)::value ^ 1>;
+        iter(j, std::integral_constant<int, 0>{}, E, E);
+        iter(j, std::integral_constant<int, 1>{}, O{}, E);
+        iter(j, std::integral_constant<int, 2>{}, E, E);
+        iter(j, std::integral_constant<int, 3>{}, O{}, E);
+        iter(j, std::integral_constant<int, 4>{}, E, E);
+        iter(j, std::integral_constant<int, 5>{}, O{}, E);
+        iter(j, std::integral_constant<int, 6>{}, E, E);
+        iter(j, std::integral_constant<int, 7>{}, O{}, E);
+        iter(j, std::integral_constant<int, 8>{}, E, E);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    for (int j = 0; j < cpt; j += 2) {
+        nine(j, S0{});
+        nine(j + 1, S1{});
+    }
+
+    __syncthreads();  // LDS -> epilogue reduction scratch
+    stamp(2);
+    if constexpr (DBG == 2) {  // timing only: one value per lane keeps the accumulators live
+        float v = 0.f;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v += acc[rt][n][r];
+        if (v == 12345.f) p.y[tid] = v;
+    } else {
+        double* red = reinterpret_cast<double*>(sm);
+        conv_epi_store_rt<NT, 1, RT * L_NW, RT>(p, acc, m0, n0, RT * wv, lane, red);
+        if (p.gn) {
+            __syncthreads();
+            conv_epi_gn<NT, RT * L_NW>(p, m0, n0, tid, NTHR, red);
+        }
+    }
+    if constexpr (DBG != 0) {
+        __syncthreads();
+        stamp(3);
+        if (tid == 0 && blockIdx.x < L_NSTAMP) {
+            unsigned hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            l_stamps[blockIdx.x][4] = ((unsigned long long)xcc << 32) | hw;
+        }
+    }
+}
+
+template <int W>
+int launch3l(const ConvParams& p, hipStream_t st) {
+    const size_t shm = conv3l_lds_bytes(W, p.Cin);
+    static bool attr[3] = {};
+    const bool has1 = p.sc1 != nullptr, has2 = p.C2 > 0 && p.sc2 != nullptr;
+    const int pro = !has1 && !has2 ? 0 : ((has1 && (p.C2 == 0 || has2)) ? 1 : 2);
+    using K = void (*)(ConvParams);
+    const K ks[3] = {&k_conv3l<W, 0>, &k_conv3l<W, 1>, &k_conv3l<W, 2>};
+    K kc = ks[pro];
+    static const int dbg = [] {
+        const char* e = getenv("TCX_CONV3L_DBG");
+        return e ? atoi(e) : 0;
+    }();
+    if (W == 64 && pro == 0 && dbg == 1) kc = &k_conv3l<64, 0, 1>;
+    if (W == 64 && pro == 0 && dbg == 2) kc = &k_conv3l<64, 0, 2>;
+    if (dbg) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)conv3l_lds_bytes(W, 384));
+    }
+    if (!attr[pro]) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)conv3l_lds_bytes(W, 384)) != hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3l_lds_bytes(W, 384));
+            return TCX_EHIP;
+        }
+        attr[pro] = true;
+    }
+    const int grid = (p.M / L_TP) * p.n_nblk;
+    hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * L_NW), shm, st, p);
+    return check_launch("tcx_conv2d_h2(halo 3l)");
+}
+
+}  // namespace
+
+// TCX_CONV3L=0 keeps k_conv3g at rows of 32 / 64 pixels (A/B measurements)
+bool conv3l_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("TCX_CONV3L");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// called by launch_conv3g once conv3g_applies() holds (fragment-ordered weights, Cin % 32 == 0,
+// Cin <= 384, cout_pad % 96 == 0, whole-row tiles)
+bool conv3l_takes(const ConvParams& p) {
+    return conv3l_enabled() && !p.bf && p.circular && (p.W == 32 || p.W == 64) && p.M % L_TP == 0 &&
+           p.HoWo % L_TP == 0;
+}
+
+int launch_conv3l(const ConvParams& p, hipStream_t st) {
+    return p.W == 64 ? launch3l<64>(p, st) : launch3l<32>(p, st);
+}
+
+}  // namespace tcx
+
+// diagnostics: the timestamps of the last TCX_CONV3L_DBG launch, [n][5] (entry, prologue done, last
+// tap done, exit, (XCC << 32) | HW_ID)
+extern "C" int tcx_conv3l_stamps(unsigned long long* out, int n_workgroups) {
+    TCX_REQUIRE(out && n_workgroups >= 0, "tcx_conv3l_stamps: bad args");
+    const int n = n_workgroups < tcx::L_NSTAMP ? n_workgroups : tcx::L_NSTAMP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tcx::l_stamps), (size_t)n * 5 * sizeof(unsigned long long), 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return tcx::check_launch("tcx_conv3l_stamps");
+    return TCX_OK;
+}

@@ -110,35 +110,54 @@ __device__ __forceinline__ void bilin_axis(int d, int n, int& i0, int& i1, float
 // when a wave owns several row blocks); conv_epi_gn: the per-128-pixel-group reduction of the
 // partials in `red`, after a barrier.
 // SPL: 0 = fp32 MFMA accumulators (an h2 output follows p.bf), 1 = f16x3, 2 = bf16 single product
-template <int NT, int SPL, int NW>
-__device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc)[NT], int m0, int n0, int wv,
-                                               int lane, double* red) {
+// Fast path (every U-Net conv): dense NHWC output, whole tiles inside one image, no per-batch bias,
+// output columns all valid, 32-bit element offsets.  Every load (weight scale, bias, residual) is
+// issued before the first store: on gfx950 one counter (vmcnt) tracks loads AND stores, so a load
+// after a store makes the wave wait for that store to be acknowledged by memory — with the bias
+// loaded per 32-channel tile after the previous tile's 16 stores, the epilogue of a 256-pixel tile
+// took ~26 us (memory write latency x the drains, profiles/r02_zg_*) against ~0.5 us without stores.
+// RT row blocks of 32 pixels per wave (wave wv owns virtual waves wv0 .. wv0 + RT - 1).
+template <int NT, int SPL, int NW, int RT>
+__device__ __forceinline__ bool conv_epi_fast(const ConvParams& p, int m0) {
+    constexpr int BN = 32 * NT;
+    return p.osy == 1 && p.osx == 1 && p.bias_b == nullptr && p.M % (32 * NW) == 0 && p.HoWo % (32 * NW) == 0 &&
+           p.Cout % BN == 0 && (long long)p.M * p.Cout < (1ll << 29);
+}
+
+template <int NT, int SPL, int NW, int RT>
+__device__ __forceinline__ void conv_epi_store_fast(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
+                                                    int wv0, int lane, double* red) {
     constexpr int BN = 32 * NT;
     const int li = lane & 31;
     const int lh = lane >> 5;
     const bool gn = p.gn != nullptr;
-    const bool bf = SPL == 2 || (SPL == 0 && p.bf != 0);  // compile-time for the split kernels
-    // Fast path (every U-Net conv): dense NHWC output, whole tiles inside one image, no per-batch
-    // bias, output columns all valid, 32-bit element offsets; no per-row index arithmetic beyond
-    // one scalar multiple of Cout per accumulator row, GroupNorm partials summed per lane in fp32
-    // over its 16 rows (then fp64 across lanes and waves).
-    const bool fast = p.osy == 1 && p.osx == 1 && p.bias_b == nullptr && p.M % (32 * NW) == 0 &&
-                      p.HoWo % (32 * NW) == 0 && p.Cout % BN == 0 && (long long)p.M * p.Cout < (1ll << 29);
-    if (fast) {
-        const float wsc = SPL ? *p.wscale : 1.f;
+    const bool bf = SPL == 2 || (SPL == 0 && p.bf != 0);
+    const float wsc = SPL ? *p.wscale : 1.f;
+    float bco[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) bco[n] = p.bias ? p.bias[n0 + n * 32 + li] : 0.f;
+    char* const yb = reinterpret_cast<char*>(p.y);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int wv = wv0 + rt;
         const int obase = (m0 + wv * 32 + 4 * lh) * p.Cout;
-        char* const yb = reinterpret_cast<char*>(p.y);
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int co = n0 + n * 32 + li;
-            const float bco = p.bias ? p.bias[co] : 0.f;
+            float add[16];
+            if (p.resid) {  // attention proj only: the 16 residuals of this block before its stores
+#pragma unroll
+                for (int r = 0; r < 16; ++r) add[r] = bco[n] + p.resid[obase + ((r & 3) + 8 * (r >> 2)) * p.Cout + co];
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) add[r] = bco[n];
+            }
             float s = 0.f, ss = 0.f;
             bool bad = false;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int e = obase + ((r & 3) + 8 * (r >> 2)) * p.Cout + co;
-                float v = (SPL ? acc[n][r] * wsc : acc[n][r]) + bco;
-                if (p.resid) v += p.resid[e];
+                float v = (SPL ? acc[rt][n][r] * wsc : acc[rt][n][r]) + add[r];
                 if (p.act == 1) v = fmaxf(v, 0.f);
                 else if (p.act == 2) v = 1.f / (1.f + expf(-v));
                 else if (p.act == 3) v = silu_f(v);
@@ -169,7 +188,25 @@ __device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc
                 }
             }
         }
-    } else {
+    }
+}
+
+// Fused epilogue of a conv tile: wave wv owns output rows m0 + 32*wv + [0, 32) and columns
+// n0 + [0, 32*NT).  C/D map of the 32x32 MFMAs: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+// bias / per-batch bias / residual / activation, fp32 or h2 store, and the fp64 GroupNorm partials
+// of every 128-pixel group of waves (4 waves each; red: LDS scratch [NW][32*NT][2] doubles).
+// conv_epi_store: one wave's 32 x 32*NT block (NW = waves of 32 rows in the tile, virtual waves
+// when a wave owns several row blocks); conv_epi_gn: the per-128-pixel-group reduction of the
+// partials in `red`, after a barrier.
+// SPL: 0 = fp32 MFMA accumulators (an h2 output follows p.bf), 1 = f16x3, 2 = bf16 single product
+template <int NT, int SPL, int NW>
+__device__ __forceinline__ void conv_epi_store_general(const ConvParams& p, f32x16 (&acc)[NT], int m0, int n0, int wv,
+                                                       int lane, double* red) {
+    constexpr int BN = 32 * NT;
+    const int li = lane & 31;
+    const int lh = lane >> 5;
+    const bool gn = p.gn != nullptr;
+    const bool bf = SPL == 2 || (SPL == 0 && p.bf != 0);  // compile-time for the split kernels
     const bool dense_out = p.osy == 1 && p.osx == 1;
     const bool one_img = p.HoWo % (32 * NW) == 0;  // the whole tile belongs to image m0 / HoWo
     const int btile = m0 / p.HoWo;
@@ -245,7 +282,27 @@ __device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc
             }
         }
     }
+}
+
+// RT row blocks per wave (acc[rt] is virtual wave wv0 + rt)
+template <int NT, int SPL, int NW, int RT>
+__device__ __forceinline__ void conv_epi_store_rt(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0, int wv0,
+                                                  int lane, double* red) {
+    if (conv_epi_fast<NT, SPL, NW, RT>(p, m0)) {
+        conv_epi_store_fast<NT, SPL, NW, RT>(p, acc, m0, n0, wv0, lane, red);
+    } else {
+        // explicit calls, not a loop: a rolled loop over the (large) inlined general epilogue would
+        // index acc dynamically and keep the whole accumulator array in scratch
+        static_assert(RT == 1 || RT == 2, "RT is 1 or 2");
+        conv_epi_store_general<NT, SPL, NW>(p, acc[0], m0, n0, wv0, lane, red);
+        if constexpr (RT == 2) conv_epi_store_general<NT, SPL, NW>(p, acc[1], m0, n0, wv0 + 1, lane, red);
     }
+}
+
+template <int NT, int SPL, int NW>
+__device__ __forceinline__ void conv_epi_store(const ConvParams& p, f32x16 (&acc)[NT], int m0, int n0, int wv,
+                                               int lane, double* red) {
+    conv_epi_store_rt<NT, SPL, NW, 1>(p, reinterpret_cast<f32x16(&)[1][NT]>(acc), m0, n0, wv, lane, red);
 }
 
 template <int NT, int NW>

@@ -127,6 +127,7 @@ _SIGS = {
                               c_size, c_fp]),
     "tcx_layernorm_film": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_float, c_fp]),
     "tcx_skinny_stamps": (c_int, [c_fp, c_int]),
+    "tcx_conv3l_stamps": (c_int, [c_fp, c_int]),
     "tcx_prior_workspace": (c_size, [ctypes.POINTER(TcxPrior), c_int, c_int]),
     "tcx_prior_forward": (c_int, [ctypes.POINTER(TcxPrior), c_fp, c_fp, c_fp, c_fp, c_int, c_fp, c_fp, c_fp, c_size,
                                   c_fp]),
