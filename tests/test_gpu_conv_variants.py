@@ -1,6 +1,6 @@
 """GPU: the non-default split-path conv variants stay parity-green.
 
-The kernel variant is chosen once per process from the environment (csrc/conv3l.hip TCX_CONV3L, csrc/conv3g.hip TCX_CONV3G,
+The kernel variant is chosen once per process from the environment (csrc/conv3l.hip TCX_CONV3L / TCX_CONV3L_GLDS, csrc/conv3g.hip TCX_CONV3G,
 csrc/conv3h.hip halo_nw / halo_rt / halo_pipe, csrc/conv4s2h.hip TCX_NO_DSHALO), so each variant runs in ONE child process
 (sequential, one GPU process at a time besides this one) that checks the 3x3 and 4x4/s2 U-Net
 conv shapes against the fp64 numpy oracle at the fp32 gate (2e-5 of the output scale, as
@@ -39,6 +39,7 @@ assert worst <= 2e-5, worst
 
 @pytest.mark.parametrize("env", [
     {"TCX_CONV3L": "0"},                          # k_conv3g (B fragments from global) at 32/64-px rows
+    {"TCX_CONV3L_GLDS": "0"},                     # k_conv3l register-staged (not LDS-DMA) for h2 sources
     {"TCX_CONV3G": "0"},                          # k_conv3p (the round-1 default) on every 3x3 row width
     {"TCX_CONV3G": "0", "TCX_HALO_PIPE": "0"},    # unpipelined k_conv3h (4 waves, two workgroups per CU)
     {"TCX_CONV3G": "0", "TCX_HALO_PNW": "8"},     # k_conv3p with 8 waves, 256-pixel tiles

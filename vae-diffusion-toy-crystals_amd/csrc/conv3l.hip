@@ -57,7 +57,7 @@ constexpr int L_NSTAMP = 8192;
 __device__ unsigned long long l_stamps[L_NSTAMP][5];
 
 // PRO: 0 = every source h2; 1 = every source fp32 + GroupNorm table; 2 = per source at run time.
-// DBG: 0 product; 1 timestamps; 2 timestamps and no output stores (diagnostics only)
+// DBG: 0 product; 1 timestamps; 2 timestamps and no output stores; 3-6 ablations (launch3l)
 template <int W, int PRO, int DBG = 0>
 __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
     constexpr int RT = 2, NT = L_NT, BN = 32 * NT, NTHR = 64 * L_NW;
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
         constexpr int hb = decltype(HBc)::value;
         const int c = 9 * j + t;
         const bool more = j + 1 < cpt;
-        rd_b(s ^ 1, c + 1);
+        if (DBG != 6) rd_b(s ^ 1, c + 1);
         if (t != 8) rd_a(1, t, hb);  // A1(8) was read during tap 7
         __builtin_amdgcn_sched_barrier(0);
         mf(0, s);
@@ -320,15 +320,17 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
         }
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
-        if constexpr (t < UPT) unit_load(more ? j + 1 : j, t);
-        if constexpr (st) {
+        if constexpr (t < UPT && DBG != 4) unit_load(more ? j + 1 : j, t);
+        if constexpr (st && DBG != 4) {
             if constexpr (PRO == 2) unit_transform(more ? j + 1 : j, t - 2);
             unit_write(t - 2, hb ^ 1);
         }
         if constexpr (s == 0) {  // c even: pair c/2 + 1 into the ring, load pair c/2 + 2, barrier
-            wr_pair((c >> 1) + 1);
-            ld_pair((c >> 1) + 2);
-            __syncthreads();
+            if constexpr (DBG != 5) {
+                wr_pair((c >> 1) + 1);
+                ld_pair((c >> 1) + 2);
+            }
+            if constexpr (DBG != 3) __syncthreads();
         }
     };
     auto nine = [&](int j, auto E) {  // E = (9 j) & 1 = j & 1: register set of tap 0 = halo buffer
@@ -382,6 +384,214 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
     }
 }
 
+
+// ---- k_conv3lg: the PRO = 0 form (every source h2) with ALL staging by LDS-DMA and split roles.
+// vmcnt is one in-order counter per wave: in k_conv3l a wait for a tap pair's weights (L2, issued
+// two taps earlier) also waits for every halo load issued before it (HBM), so the halo gets at most
+// ~2 taps of latency cover; ablations at up1_1 (profiles/r02_zi_*): no halo staging -9 %, no weight
+// staging -6 % of the launch.  Here waves 0-1 move the weight pairs (6 x 1 KB buffer_load ... lds
+// each per pair) and waves 2-3 the halo (13 / 12 x 1 KB per chunk): a wave only ever waits for its
+// own kind of load.  The halo of chunk j+1 is issued at taps 0-3 of chunk j and waited for at tap 6/7
+// (4-7 taps of cover), a pair at tap 2k-3 and waited for at tap 2k-2.  No VGPR staging, no
+// ds_write; waits are explicit s_waitcnt before raw s_barrier (hipcc's __syncthreads would drain
+// every LDS-DMA in flight).  The halo slot image is the swizzled one of k_conv3l, written lane-
+// linearly: lane l of halo instruction i fills slot 16 i + l / 4, physical piece l % 4, so it reads
+// logical piece (l % 4) ^ sw(col) of that pixel (the per-lane source address carries the swizzle).
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+constexpr int WAIT_VM0 = 0x0F70;    // s_waitcnt vmcnt(0)
+constexpr int WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
+
+template <int W>
+__global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
+    constexpr int RT = 2, NT = L_NT, NTHR = 64 * L_NW;
+    constexpr int W2 = W + 2;
+    constexpr int NPX = l_npx(W);
+    constexpr int NI = (NPX + 15) / 16;  // halo instructions per chunk (16 slots each)
+    constexpr int NIH = (NI + 1) / 2;    // per halo wave (wave 2: even i, wave 3: odd i)
+    constexpr int HB = NI * 16 * 64;
+    constexpr int RING = 2 * HB;
+    constexpr int RT1 = W == 64 ? 32 * 64 : W2 * 64;
+    static_assert(W == 32 || W == 64, "k_conv3lg: rows of 32 or 64 pixels");
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    char* const smc = reinterpret_cast<char*>(sm);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mblk = tile / p.n_nblk;
+    const int nblk = tile - mblk * p.n_nblk;
+    const int m0 = mblk * L_TP, n0 = nblk * 32 * NT;
+    const int b = m0 / p.HoWo;
+    const int r0 = (m0 - b * p.HoWo) / W;
+    const int bs = p.bmod > 0 ? b % p.bmod : b;
+    const int H = p.H;
+    const int cpt = p.Cin / L_KC;
+    const int nch = 9 * cpt;
+    const int npair = nch / 2;
+
+    const __amdgpu_buffer_rsrc_t r1 = mk_rsrc(p.x1, p.bytes1);
+    const __amdgpu_buffer_rsrc_t r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
+    const __amdgpu_buffer_rsrc_t rw = mk_rsrc(reinterpret_cast<const float*>(p.wf), p.bytesw);
+
+    // halo waves: per-lane source offsets of their instructions (chunk-invariant; the chunk's channel
+    // offset rides in soffset)
+    const int hw = wv & 1;
+    const int rowb = p.C1 * 4;
+    int hvo[NIH];
+#pragma unroll
+    for (int q = 0; q < NIH; ++q) {
+        const int sl = 16 * (2 * q + hw) + (lane >> 2);
+        const int ss = sl < NPX ? sl : NPX - 1;  // padding slots read a valid pixel
+        const int hr = ss / W2, hc = ss - hr * W2;
+        const int hcs = sl - (sl / W2) * W2;      // the slot's own column (its swizzle)
+        const int y = wrap_idx(r0 + hr - 1, H), x = wrap_idx(hc - 1, W);
+        hvo[q] = ((bs * H + y) * W + x) * rowb + 16 * ((lane & 3) ^ ((hcs >> 2) & 3));
+    }
+    auto halo_issue = [&](int j, int buf, int q0, int q1) {
+        const int ci0 = j * L_KC;
+        const bool s1 = ci0 < p.C1;
+        const int cc = (s1 ? ci0 : ci0 - p.C1) * 4;
+        const __amdgpu_buffer_rsrc_t rs = s1 ? r1 : r2;
+#pragma unroll
+        for (int q = 0; q < NIH; ++q) {
+            if (q < q0 || q >= q1) continue;
+            const int i = 2 * q + hw;
+            if (i < NI) lds_dma16(rs, smc + buf * HB + i * 1024, hvo[q], cc);
+        }
+    };
+    // weight waves: pair k (12 KB) -> ring slot k & 1; wave w moves KB [6 w, 6 w + 6)
+    auto pair_issue = [&](int k) {
+        k = k < npair ? k : npair - 1;
+        const int base = (nblk * nch + 2 * k) * NT * 2048 + wv * 6144;
+        char* const d = smc + RING + (k & 1) * L_PAIR + wv * 6144;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) lds_dma16(rw, d + i * 1024, lane * 16, base + i * 1024);
+    };
+
+    int xa[3];
+    {
+        const int mloc = (wv * RT) * 32 + li;
+        const int rr = mloc / W, cc = mloc % W;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+            xa[dx] = (rr * W2 + cc + dx) * 64 + 16 * ((2 * lh) ^ (((cc + dx) >> 2) & 3));
+    }
+    f32x16 acc[RT][NT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[rt][n] = (f32x16){};
+    h8 a_h[RT], a_l[RT], b_h[2][NT], b_l[2][NT];
+    auto rd_a = [&](int rt, int t, int hb) {
+        const int dy = t / 3, dx = t - 3 * (t / 3);
+        const int off = hb * HB + rt * RT1 + dy * W2 * 64;
+        a_h[rt] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + xa[dx] + off));
+        a_l[rt] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + (xa[dx] ^ 16) + off));
+    };
+    const int bl = lane * 16;
+    auto rd_b = [&](int s, int c) {
+        const char* B = smc + RING + ((c >> 1) & 1) * L_PAIR + (c & 1) * (L_PAIR / 2) + bl;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            b_h[s][n] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(B + n * 2048));
+            b_l[s][n] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(B + n * 2048 + 1024));
+        }
+    };
+    auto mf = [&](int rt, int s) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[rt], b_l[s][n], acc[rt][n], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_l[rt], b_h[s][n], acc[rt][n], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[rt], b_h[s][n], acc[rt][n], 0, 0, 0);
+    };
+    auto barrier = [&]() {
+        __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+        __builtin_amdgcn_s_barrier();
+    };
+
+    // ---- prologue: pairs 0, 1 and halo 0 in LDS
+    if (wv < 2) {
+        pair_issue(0);
+        pair_issue(1);
+    } else {
+        halo_issue(0, 0, 0, NIH);
+    }
+    __builtin_amdgcn_s_waitcnt(WAIT_VM0);
+    barrier();
+    rd_b(0, 0);
+    rd_a(0, 0, 0);
+
+    auto iter = [&](int j, auto T, auto S, auto HBc) {
+        constexpr int t = decltype(T)::value;
+        constexpr int s = decltype(S)::value;
+        constexpr int hb = decltype(HBc)::value;
+        const int c = 9 * j + t;
+        rd_b(s ^ 1, c + 1);
+        if (t != 8) rd_a(1, t, hb);
+        __builtin_amdgcn_sched_barrier(0);
+        mf(0, s);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t == 8) rd_a(0, 0, hb ^ 1);
+        else rd_a(0, t + 1, hb);
+        __builtin_amdgcn_sched_barrier(0);
+        mf(1, s);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t == 7) rd_a(1, 8, hb);
+        if (wv < 2) {
+            if constexpr (s == 1) pair_issue((c + 3) >> 1);  // odd tap 2k-3: pair k
+        } else if constexpr (t < 4) {
+            // halo of chunk j+1 into the other buffer, a quarter per tap (not after the last chunk)
+            constexpr int q0 = (NIH * t) / 4, q1 = (NIH * (t + 1)) / 4;
+            if (j + 1 < cpt) halo_issue(j + 1, hb ^ 1, q0, q1);
+        }
+        if constexpr (s == 0) {  // even tap: the barrier that publishes pair c/2 + 1 (and halo j+1 at
+                                 // tap 6 of an even chunk / tap 7 of an odd one)
+            constexpr bool halo_wait = t == (hb ? 7 : 6);
+            if (wv < 2 || halo_wait) __builtin_amdgcn_s_waitcnt(WAIT_VM0);
+            barrier();
+        }
+    };
+    auto nine = [&](int j, auto E) {
+        using O = std::integral_constant<int, decltype(E)::value ^ 1>;
+        iter(j, std::integral_constant<int, 0>{}, E, E);
+        iter(j, std::integral_constant<int, 1>{}, O{}, E);
+        iter(j, std::integral_constant<int, 2>{}, E, E);
+        iter(j, std::integral_constant<int, 3>{}, O{}, E);
+        iter(j, std::integral_constant<int, 4>{}, E, E);
+        iter(j, std::integral_constant<int, 5>{}, O{}, E);
+        iter(j, std::integral_constant<int, 6>{}, E, E);
+        iter(j, std::integral_constant<int, 7>{}, O{}, E);
+        iter(j, std::integral_constant<int, 8>{}, E, E);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    for (int j = 0; j < cpt; j += 2) {
+        nine(j, S0{});
+        nine(j + 1, S1{});
+    }
+
+    __builtin_amdgcn_s_waitcnt(WAIT_VM0);  // the clamped tail pairs land before LDS is reused
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(sm);
+    conv_epi_store_rt<NT, 1, RT * L_NW, RT>(p, acc, m0, n0, RT * wv, lane, red);
+    if (p.gn) {
+        __syncthreads();
+        conv_epi_gn<NT, RT * L_NW>(p, m0, n0, tid, NTHR, red);
+    }
+}
+
+template <int W>
+constexpr size_t conv3lg_lds_bytes() {
+    return (size_t)2 * ((l_npx(W) + 15) / 16) * 16 * 64 + 2 * (size_t)L_PAIR;
+}
+
 template <int W>
 int launch3l(const ConvParams& p, hipStream_t st) {
     const size_t shm = conv3l_lds_bytes(W, p.Cin);
@@ -391,12 +601,22 @@ int launch3l(const ConvParams& p, hipStream_t st) {
     using K = void (*)(ConvParams);
     const K ks[3] = {&k_conv3l<W, 0>, &k_conv3l<W, 1>, &k_conv3l<W, 2>};
     K kc = ks[pro];
+    static const bool glds = [] {
+        const char* e = getenv("TCX_CONV3L_GLDS");
+        return !(e && e[0] == '0');
+    }();
     static const int dbg = [] {
         const char* e = getenv("TCX_CONV3L_DBG");
         return e ? atoi(e) : 0;
     }();
+    // diagnostics (wrong results except 1 and 2): 1 stamps, 2 no output stores, 3 no barriers in the
+    // tap loop, 4 no halo staging in the loop, 5 no B pair staging, 6 no B fragment reads
     if (W == 64 && pro == 0 && dbg == 1) kc = &k_conv3l<64, 0, 1>;
     if (W == 64 && pro == 0 && dbg == 2) kc = &k_conv3l<64, 0, 2>;
+    if (W == 64 && pro == 0 && dbg == 3) kc = &k_conv3l<64, 0, 3>;
+    if (W == 64 && pro == 0 && dbg == 4) kc = &k_conv3l<64, 0, 4>;
+    if (W == 64 && pro == 0 && dbg == 5) kc = &k_conv3l<64, 0, 5>;
+    if (W == 64 && pro == 0 && dbg == 6) kc = &k_conv3l<64, 0, 6>;
     if (dbg) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)conv3l_lds_bytes(W, 384));
@@ -410,6 +630,19 @@ int launch3l(const ConvParams& p, hipStream_t st) {
         attr[pro] = true;
     }
     const int grid = (p.M / L_TP) * p.n_nblk;
+    if (pro == 0 && glds && dbg == 0) {  // every source h2: the LDS-DMA form
+        static bool attr_g = false;
+        if (!attr_g) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3lg<W>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)conv3lg_lds_bytes<W>()) != hipSuccess) {
+                set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3lg_lds_bytes<W>());
+                return TCX_EHIP;
+            }
+            attr_g = true;
+        }
+        hipLaunchKernelGGL(k_conv3lg<W>, dim3(grid), dim3(64 * L_NW), conv3lg_lds_bytes<W>(), st, p);
+        return check_launch("tcx_conv2d_h2(halo 3lg)");
+    }
     hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * L_NW), shm, st, p);
     return check_launch("tcx_conv2d_h2(halo 3l)");
 }
