@@ -1,6 +1,6 @@
 """GPU: the non-default split-path conv variants stay parity-green.
 
-The kernel variant is chosen once per process from the environment (csrc/conv3l.hip TCX_CONV3L / TCX_CONV3L_GLDS, csrc/conv3g.hip TCX_CONV3G,
+The kernel variant is chosen once per process from the environment (csrc/conv3l.hip TCX_CONV3L / TCX_CONV3L_GLDS / TCX_CONV3L_GLDS_PRO, csrc/conv3g.hip TCX_CONV3G,
 csrc/conv3h.hip halo_nw / halo_rt / halo_pipe, csrc/conv4s2h.hip TCX_NO_DSHALO), so each variant runs in ONE child process
 (sequential, one GPU process at a time besides this one) that checks the 3x3 and 4x4/s2 U-Net
 conv shapes against the fp64 numpy oracle at the fp32 gate (2e-5 of the output scale, as
@@ -32,6 +32,17 @@ for (B, Ci, Co, H, ks, s) in [(2, 96, 96, 64, 3, 1), (2, 192, 192, 32, 3, 1), (2
     got = run_conv_h2(x, w, b, s, 1, True)
     err = float(np.abs(got - ref).max()) / max(1.0, float(np.abs(ref).max()))
     worst = max(worst, err)
+# GroupNorm+SiLU prologue (tcx_conv2d_h2_pro) at the 64^2 and 32^2 shapes of the evaluator
+from test_gpu_h2 import run_conv_h2_pro, gn_silu_ref, rand_tabs
+for (B, Ci, H) in [(2, 96, 64), (2, 192, 32)]:
+    x = rng.standard_normal((B, Ci, H, H)) * 2.0
+    w = rng.standard_normal((Ci, Ci, 3, 3)) / np.sqrt(Ci * 9)
+    b = rng.standard_normal(Ci)
+    tabs = rand_tabs(B, Ci, 3)
+    ref = nn_np.conv2d(gn_silu_ref(x.astype(np.float32).astype(np.float64), tabs), w, b, padding=1, mode="circular")
+    got = run_conv_h2_pro(x, w, b, True, tabs)
+    err = float(np.abs(got - ref).max()) / max(1.0, float(np.abs(ref).max()))
+    worst = max(worst, err)
 print("worst", worst)
 assert worst <= 2e-5, worst
 """.replace("ROOT", repr(ROOT))
@@ -40,6 +51,7 @@ assert worst <= 2e-5, worst
 @pytest.mark.parametrize("env", [
     {"TCX_CONV3L": "0"},                          # k_conv3g (B fragments from global) at 32/64-px rows
     {"TCX_CONV3L_GLDS": "0"},                     # k_conv3l register-staged (not LDS-DMA) for h2 sources
+    {"TCX_CONV3L_GLDS_PRO": "1"},                 # k_conv3lg's GroupNorm+SiLU prologue form
     {"TCX_CONV3G": "0"},                          # k_conv3p (the round-1 default) on every 3x3 row width
     {"TCX_CONV3G": "0", "TCX_HALO_PIPE": "0"},    # unpipelined k_conv3h (4 waves, two workgroups per CU)
     {"TCX_CONV3G": "0", "TCX_HALO_PNW": "8"},     # k_conv3p with 8 waves, 256-pixel tiles

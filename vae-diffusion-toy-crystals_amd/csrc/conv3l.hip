@@ -385,7 +385,8 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
 }
 
 
-// ---- k_conv3lg: the PRO = 0 form (every source h2) with ALL staging by LDS-DMA and split roles.
+// ---- k_conv3lg: the single-source forms (PRO 0: h2 source; PRO 1: fp32 source + GroupNorm+SiLU
+// tables) with ALL staging by LDS-DMA and split roles.
 // vmcnt is one in-order counter per wave: in k_conv3l a wait for a tap pair's weights (L2, issued
 // two taps earlier) also waits for every halo load issued before it (HBM), so the halo gets at most
 // ~2 taps of latency cover; ablations at up1_1 (profiles/r02_zi_*): no halo staging -9 %, no weight
@@ -397,13 +398,30 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
 // every LDS-DMA in flight).  The halo slot image is the swizzled one of k_conv3l, written lane-
 // linearly: lane l of halo instruction i fills slot 16 i + l / 4, physical piece l % 4, so it reads
 // logical piece (l % 4) ^ sw(col) of that pixel (the per-lane source address carries the swizzle).
+// PRO 1: the halo waves DMA the raw fp32 chunk (16 channels = 64 B per pixel, the size of its h2
+// record) into the same slots; it is published by the barrier of tap 4 (even chunk) / 5 (odd), and
+// during the next two taps every wave rewrites its quarter of the units IN PLACE as h2 of
+// silu(x sc + sh) (per unit: two ds_read_b128, eight values one per MFMA gap, two ds_write_b128).
+// Waves 0-1 own the 8-channel group 0 of every slot, waves 2-3 group 1, so a wave's GroupNorm
+// scale/shift for the chunk are 16 wave-uniform values (scalar loads, no LDS table).
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+// 8 wave-uniform floats by a scalar load (lgkmcnt, not the in-order vmcnt of the LDS-DMA stream;
+// hipcc emits a vector load for a uniform address in a kernel that also stores to global memory)
+__device__ __forceinline__ f32x8 sload8(const float* ptr) {
+    const unsigned long long a = (unsigned long long)ptr;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const unsigned long long u = ((unsigned long long)hi << 32) | lo;
+    f32x8 r;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(u) : "memory");
+    return r;
 }
 constexpr int WAIT_VM0 = 0x0F70;    // s_waitcnt vmcnt(0)
 constexpr int WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
 
-template <int W>
+template <int W, int PRO>
 __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     constexpr int RT = 2, NT = L_NT, NTHR = 64 * L_NW;
     constexpr int W2 = W + 2;
@@ -436,20 +454,20 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     const __amdgpu_buffer_rsrc_t r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
     const __amdgpu_buffer_rsrc_t rw = mk_rsrc(reinterpret_cast<const float*>(p.wf), p.bytesw);
 
-    // halo waves: per-lane source offsets of their instructions (chunk-invariant; the chunk's channel
+    // halo waves: the per-lane source offset of instruction i (computed at issue: keeping all 13 live
+    // across the tap loop cost more registers than the ~12 VALU per instruction; the chunk's channel
     // offset rides in soffset)
     const int hw = wv & 1;
     const int rowb = p.C1 * 4;
-    int hvo[NIH];
-#pragma unroll
-    for (int q = 0; q < NIH; ++q) {
-        const int sl = 16 * (2 * q + hw) + (lane >> 2);
+    const int img0 = bs * H;
+    auto halo_voff = [&](int i) {
+        const int sl = 16 * i + (lane >> 2);
         const int ss = sl < NPX ? sl : NPX - 1;  // padding slots read a valid pixel
         const int hr = ss / W2, hc = ss - hr * W2;
-        const int hcs = sl - (sl / W2) * W2;      // the slot's own column (its swizzle)
+        const int hcs = sl < NPX ? hc : sl - (sl / W2) * W2;  // the slot's own column (its swizzle)
         const int y = wrap_idx(r0 + hr - 1, H), x = wrap_idx(hc - 1, W);
-        hvo[q] = ((bs * H + y) * W + x) * rowb + 16 * ((lane & 3) ^ ((hcs >> 2) & 3));
-    }
+        return ((img0 + y) * W + x) * rowb + 16 * ((lane & 3) ^ ((hcs >> 2) & 3));
+    };
     auto halo_issue = [&](int j, int buf, int q0, int q1) {
         const int ci0 = j * L_KC;
         const bool s1 = ci0 < p.C1;
@@ -459,7 +477,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         for (int q = 0; q < NIH; ++q) {
             if (q < q0 || q >= q1) continue;
             const int i = 2 * q + hw;
-            if (i < NI) lds_dma16(rs, smc + buf * HB + i * 1024, hvo[q], cc);
+            if (i < NI) lds_dma16(rs, smc + buf * HB + i * 1024, halo_voff(i), cc);
         }
     };
     // weight waves: pair k (12 KB) -> ring slot k & 1; wave w moves KB [6 w, 6 w + 6)
@@ -516,6 +534,95 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         __builtin_amdgcn_s_barrier();
     };
 
+    // PRO 1: units of this wave: group g = wv >> 1, slots (wv & 1) 64 + lane + 128 i (i < 4)
+    constexpr int NPXS = NPX;
+    const int tg = wv >> 1;
+    // lanes past the last slot rewrite a padding slot (no divergence around MFMAs); several lanes
+    // share one, so what they read may already be another lane's h2: their range flag is masked
+    int tdst[4];
+    unsigned tval = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int hp0 = (wv & 1) * 64 + lane + 128 * i;
+        const int hp = hp0 < NPXS ? hp0 : NPXS + (lane & 3);
+        const int hc = hp % W2;
+        tdst[i] = hp * 64 + 16 * ((2 * tg) ^ ((hc >> 2) & 3));
+        tval |= hp0 < NPXS ? 1u << i : 0u;
+    }
+    float tsc[8], tsh[8];  // this wave's group of the chunk being transformed (wave-uniform)
+    auto load_tabs = [&](int j) {
+        const size_t o = (size_t)b * p.C1 + j * L_KC + 8 * tg;
+        const f32x8 a = sload8(p.sc1 + o), c = sload8(p.sh1 + o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            tsc[k] = a[k];
+            tsh[k] = c[k];
+        }
+    };
+    // MFMAs of row block rt with the transform of unit i (buffer buf) one value per gap
+    auto mf_transform = [&](int rt, int s, int i, int buf, bool live) {
+        char* const d = smc + buf * HB + tdst[i];
+        const float4 x0 = *reinterpret_cast<const float4*>(d);
+        const float4 x1 = *reinterpret_cast<const float4*>(smc + buf * HB + (tdst[i] ^ 16));
+        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        unsigned sp[8];
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int g = k / 3, n = k - 3 * (k / 3);
+            const h8& aa = g == 1 ? a_l[rt] : a_h[rt];
+            const h8& bb = g == 0 ? b_l[s][n] : b_h[s][n];
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa, bb, acc[rt][n], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (k < 8) {
+                const float v = l_silu(xs[k], tsc[k], tsh[k]);
+                bad = bad || h2_bad(v);
+                sp[k] = split1(v);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        unsigned h[4], l[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            h[k] = (sp[2 * k] & 0xffffu) | (sp[2 * k + 1] << 16);
+            l[k] = (sp[2 * k] >> 16) | (sp[2 * k + 1] & 0xffff0000u);
+        }
+        *reinterpret_cast<float4*>(d) =
+            make_float4(__uint_as_float(h[0]), __uint_as_float(h[1]), __uint_as_float(h[2]), __uint_as_float(h[3]));
+        *reinterpret_cast<float4*>(smc + buf * HB + (tdst[i] ^ 16)) =
+            make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), __uint_as_float(l[2]), __uint_as_float(l[3]));
+        h2_flag(p.ovf, bad && live && ((tval >> i) & 1));  // after the last chunk: no raw data
+    };
+    // the whole chunk's transform at once (prologue)
+    auto transform_all = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            char* const d = smc + buf * HB + tdst[i];
+            const float4 x0 = *reinterpret_cast<const float4*>(d);
+            const float4 x1 = *reinterpret_cast<const float4*>(smc + buf * HB + (tdst[i] ^ 16));
+            const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            unsigned sp[8];
+            bool bad = false;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float v = l_silu(xs[k], tsc[k], tsh[k]);
+                bad = bad || h2_bad(v);
+                sp[k] = split1(v);
+            }
+            unsigned h[4], l[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                h[k] = (sp[2 * k] & 0xffffu) | (sp[2 * k + 1] << 16);
+                l[k] = (sp[2 * k] >> 16) | (sp[2 * k + 1] & 0xffff0000u);
+            }
+            *reinterpret_cast<float4*>(d) =
+                make_float4(__uint_as_float(h[0]), __uint_as_float(h[1]), __uint_as_float(h[2]), __uint_as_float(h[3]));
+            *reinterpret_cast<float4*>(smc + buf * HB + (tdst[i] ^ 16)) =
+                make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), __uint_as_float(l[2]), __uint_as_float(l[3]));
+            h2_flag(p.ovf, bad && ((tval >> i) & 1));
+        }
+    };
+
     // ---- prologue: pairs 0, 1 and halo 0 in LDS
     if (wv < 2) {
         pair_issue(0);
@@ -525,6 +632,12 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     }
     __builtin_amdgcn_s_waitcnt(WAIT_VM0);
     barrier();
+    if constexpr (PRO == 1) {
+        load_tabs(0);
+        transform_all(0);
+        barrier();
+        if (cpt > 1) load_tabs(1);
+    }
     rd_b(0, 0);
     rd_a(0, 0, 0);
 
@@ -533,27 +646,40 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         constexpr int s = decltype(S)::value;
         constexpr int hb = decltype(HBc)::value;
         const int c = 9 * j + t;
+        // PRO 1: raw halo j+1 published at tap 4 (even chunk) / 5 (odd); transformed in the next
+        // two taps (units 0-1, then 2-3); h2 published at tap 6 / 7
+        constexpr int TR = hb ? 6 : 5;  // first transform tap
+        constexpr bool tr = PRO == 1 && (t == TR || t == TR + 1);
+        const bool more = j + 1 < cpt;
         rd_b(s ^ 1, c + 1);
         if (t != 8) rd_a(1, t, hb);
         __builtin_amdgcn_sched_barrier(0);
-        mf(0, s);
+        if constexpr (tr) mf_transform(0, s, 2 * (t - TR), hb ^ 1, more);
+        else mf(0, s);
         __builtin_amdgcn_sched_barrier(0);
         if (t == 8) rd_a(0, 0, hb ^ 1);
         else rd_a(0, t + 1, hb);
         __builtin_amdgcn_sched_barrier(0);
-        mf(1, s);
+        if constexpr (tr) mf_transform(1, s, 2 * (t - TR) + 1, hb ^ 1, more);
+        else mf(1, s);
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
         if (wv < 2) {
             if constexpr (s == 1) pair_issue((c + 3) >> 1);  // odd tap 2k-3: pair k
-        } else if constexpr (t < 4) {
-            // halo of chunk j+1 into the other buffer, a quarter per tap (not after the last chunk)
-            constexpr int q0 = (NIH * t) / 4, q1 = (NIH * (t + 1)) / 4;
-            if (j + 1 < cpt) halo_issue(j + 1, hb ^ 1, q0, q1);
+        } else if constexpr (PRO == 0 ? t < 4 : t < 2) {
+            // halo of chunk j+1 into the other buffer (not after the last chunk): PRO 0 a quarter per
+            // tap over taps 0-3, PRO 1 half per tap over taps 0-1 (the raw data is waited for at tap 4/5)
+            constexpr int NQ = PRO == 0 ? 4 : 2;
+            constexpr int q0 = (NIH * t) / NQ, q1 = (NIH * (t + 1)) / NQ;
+            if (more) halo_issue(j + 1, hb ^ 1, q0, q1);
         }
-        if constexpr (s == 0) {  // even tap: the barrier that publishes pair c/2 + 1 (and halo j+1 at
-                                 // tap 6 of an even chunk / tap 7 of an odd one)
-            constexpr bool halo_wait = t == (hb ? 7 : 6);
+        if constexpr (PRO == 1 && t == TR + 1) {
+            if (j + 2 < cpt) load_tabs(j + 2);
+        }
+        if constexpr (s == 0) {  // even tap: the barrier that publishes pair c/2 + 1 (and halo j+1:
+                                 // PRO 0 at tap 6 of an even chunk / 7 of an odd one; PRO 1 the raw
+                                 // data at tap 4 / 5)
+            constexpr bool halo_wait = PRO == 0 ? t == (hb ? 7 : 6) : t == TR - 1;
             if (wv < 2 || halo_wait) __builtin_amdgcn_s_waitcnt(WAIT_VM0);
             barrier();
         }
@@ -605,6 +731,12 @@ int launch3l(const ConvParams& p, hipStream_t st) {
         const char* e = getenv("TCX_CONV3L_GLDS");
         return !(e && e[0] == '0');
     }();
+    // the prologue form of k_conv3lg: parity-green but no faster than the register-staged k_conv3l
+    // (its GN+SiLU transform is squeezed into two taps; profiles/r02_zk_*), so off by default
+    static const bool glds_pro = [] {
+        const char* e = getenv("TCX_CONV3L_GLDS_PRO");
+        return e && e[0] == '1';
+    }();
     static const int dbg = [] {
         const char* e = getenv("TCX_CONV3L_DBG");
         return e ? atoi(e) : 0;
@@ -630,17 +762,18 @@ int launch3l(const ConvParams& p, hipStream_t st) {
         attr[pro] = true;
     }
     const int grid = (p.M / L_TP) * p.n_nblk;
-    if (pro == 0 && glds && dbg == 0) {  // every source h2: the LDS-DMA form
-        static bool attr_g = false;
-        if (!attr_g) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3lg<W>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)conv3lg_lds_bytes<W>()) != hipSuccess) {
+    if ((pro == 0 || (pro == 1 && p.C2 == 0 && glds_pro)) && glds && dbg == 0) {  // the LDS-DMA form
+        static bool attr_g[2] = {};
+        const K kg = pro ? &k_conv3lg<W, 1> : &k_conv3lg<W, 0>;
+        if (!attr_g[pro]) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(kg), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)conv3lg_lds_bytes<W>()) != hipSuccess) {
                 set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3lg_lds_bytes<W>());
                 return TCX_EHIP;
             }
-            attr_g = true;
+            attr_g[pro] = true;
         }
-        hipLaunchKernelGGL(k_conv3lg<W>, dim3(grid), dim3(64 * L_NW), conv3lg_lds_bytes<W>(), st, p);
+        hipLaunchKernelGGL(kg, dim3(grid), dim3(64 * L_NW), conv3lg_lds_bytes<W>(), st, p);
         return check_launch("tcx_conv2d_h2(halo 3lg)");
     }
     hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * L_NW), shm, st, p);

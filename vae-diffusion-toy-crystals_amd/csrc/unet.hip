@@ -643,7 +643,13 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // normalised tensor is never written: norms 0, 2, 4, 7, 9 (down1.net.1, down2.net.1, mid.net.1,
     // up2.net.1, up1.net.1 feeding the .net.3 conv of their block).  The skip tensors h1/h2 (norms 1,
     // 3: read by a 4x4/s2 conv AND an up-path concat) keep the in-place h2 apply pass.
-    if (net->precision >= 1) {
+    // TCX_GN_PRO=0: every GroupNorm as an h2 apply pass (A/B of the prologue against the LDS-DMA
+    // h2-source conv)
+    static const bool gn_pro = [] {
+        const char* e = getenv("TCX_GN_PRO");
+        return !(e && e[0] == '0');
+    }();
+    if (net->precision >= 1 && gn_pro) {
         pro[0] = net->down1_1.whf && conv3g_covers(H, W, C, net->down1_1.cout_pad);
         pro[2] = net->down2_1.whf && conv3g_covers(H1, W1, C2, net->down2_1.cout_pad);
         pro[7] = net->up2_1.whf && conv3g_covers(H1, W1, C, net->up2_1.cout_pad);
