@@ -392,8 +392,8 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
 // ~2 taps of latency cover; ablations at up1_1 (profiles/r02_zi_*): no halo staging -9 %, no weight
 // staging -6 % of the launch.  Here waves 0-1 move the weight pairs (6 x 1 KB buffer_load ... lds
 // each per pair) and waves 2-3 the halo (13 / 12 x 1 KB per chunk): a wave only ever waits for its
-// own kind of load.  The halo of chunk j+1 is issued at taps 0-3 of chunk j and waited for at tap 6/7
-// (4-7 taps of cover), a pair at tap 2k-3 and waited for at tap 2k-2.  No VGPR staging, no
+// own kind of load.  The halo of chunk j+1 is issued at the start of taps 0-3 of chunk j and waited for
+// at tap 6/7 (4-7 taps of cover), a pair at the start of tap 2k-3 and waited for at the end of 2k-2.  No VGPR staging, no
 // ds_write; waits are explicit s_waitcnt before raw s_barrier (hipcc's __syncthreads would drain
 // every LDS-DMA in flight).  The halo slot image is the swizzled one of k_conv3l, written lane-
 // linearly: lane l of halo instruction i fills slot 16 i + l / 4, physical piece l % 4, so it reads
@@ -651,6 +651,18 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         constexpr int TR = hb ? 6 : 5;  // first transform tap
         constexpr bool tr = PRO == 1 && (t == TR || t == TR + 1);
         const bool more = j + 1 < cpt;
+        // LDS-DMA issue first thing in the tap (right after the barrier that freed the target): a
+        // pair issued at the start of odd tap 2k-3 has two taps of latency cover before its wait
+        if (wv < 2) {
+            if constexpr (s == 1) pair_issue((c + 3) >> 1);
+        } else if constexpr (PRO == 0 ? t < 4 : t < 2) {
+            // halo of chunk j+1 into the other buffer (not after the last chunk): PRO 0 a quarter per
+            // tap over taps 0-3, PRO 1 half per tap over taps 0-1 (the raw data is waited for at tap 4/5)
+            constexpr int NQ = PRO == 0 ? 4 : 2;
+            constexpr int q0 = (NIH * t) / NQ, q1 = (NIH * (t + 1)) / NQ;
+            if (more) halo_issue(j + 1, hb ^ 1, q0, q1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
         rd_b(s ^ 1, c + 1);
         if (t != 8) rd_a(1, t, hb);
         __builtin_amdgcn_sched_barrier(0);
@@ -664,15 +676,6 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         else mf(1, s);
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
-        if (wv < 2) {
-            if constexpr (s == 1) pair_issue((c + 3) >> 1);  // odd tap 2k-3: pair k
-        } else if constexpr (PRO == 0 ? t < 4 : t < 2) {
-            // halo of chunk j+1 into the other buffer (not after the last chunk): PRO 0 a quarter per
-            // tap over taps 0-3, PRO 1 half per tap over taps 0-1 (the raw data is waited for at tap 4/5)
-            constexpr int NQ = PRO == 0 ? 4 : 2;
-            constexpr int q0 = (NIH * t) / NQ, q1 = (NIH * (t + 1)) / NQ;
-            if (more) halo_issue(j + 1, hb ^ 1, q0, q1);
-        }
         if constexpr (PRO == 1 && t == TR + 1) {
             if (j + 2 < cpt) load_tabs(j + 2);
         }
