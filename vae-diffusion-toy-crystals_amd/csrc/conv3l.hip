@@ -460,13 +460,23 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     const int hw = wv & 1;
     const int rowb = p.C1 * 4;
     const int img0 = bs * H;
+    // slot 16 i + ls (ls = lane / 4) of instruction i (compile-time i after unrolling) lies in halo
+    // row R(i) or R(i) + 1: the row's image offset (with the circular wrap) is wave-uniform scalar
+    // work, the lane only selects between the two and adds its column
+    const int ls = lane >> 2;
     auto halo_voff = [&](int i) {
-        const int sl = 16 * i + (lane >> 2);
-        const int ss = sl < NPX ? sl : NPX - 1;  // padding slots read a valid pixel
-        const int hr = ss / W2, hc = ss - hr * W2;
-        const int hcs = sl < NPX ? hc : sl - (sl / W2) * W2;  // the slot's own column (its swizzle)
-        const int y = wrap_idx(r0 + hr - 1, H), x = wrap_idx(hc - 1, W);
-        return ((img0 + y) * W + x) * rowb + 16 * ((lane & 3) ^ ((hcs >> 2) & 3));
+        const int hr0 = (16 * i) / W2;                // compile-time after unrolling
+        const int th = W2 * (hr0 + 1) - 16 * i;       // lanes with ls >= th are in row hr0 + 1
+        const int y0 = wrap_idx(r0 + hr0 - 1, H), y1 = wrap_idx(r0 + hr0, H);
+        const int yo0 = (img0 + y0) * W * rowb, yo1 = (img0 + y1) * W * rowb;
+        const bool nx = ls >= th;
+        int hc = 16 * i - hr0 * W2 + ls - (nx ? W2 : 0);
+        const int sl = 16 * i + ls;
+        const int hcs = hc;                            // the slot's own column (its swizzle)
+        if (sl >= NPX) hc = (NPX - 1) % W2;            // padding slots read a valid pixel
+        const int x = hc == 0 ? W - 1 : (hc == W + 1 ? 0 : hc - 1);
+        const int yo = (sl >= NPX) ? (img0 + wrap_idx(r0 + (NPX - 1) / W2 - 1, H)) * W * rowb : (nx ? yo1 : yo0);
+        return yo + x * rowb + 16 * ((lane & 3) ^ ((hcs >> 2) & 3));
     };
     auto halo_issue = [&](int j, int buf, int q0, int q1) {
         const int ci0 = j * L_KC;

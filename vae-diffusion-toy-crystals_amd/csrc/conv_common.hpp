@@ -102,20 +102,13 @@ __device__ __forceinline__ void bilin_axis(int d, int n, int& i0, int& i1, float
     l0 = 1.f - l1;
 }
 
-// Fused epilogue of a conv tile: wave wv owns output rows m0 + 32*wv + [0, 32) and columns
-// n0 + [0, 32*NT).  C/D map of the 32x32 MFMAs: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-// bias / per-batch bias / residual / activation, fp32 or h2 store, and the fp64 GroupNorm partials
-// of every 128-pixel group of waves (4 waves each; red: LDS scratch [NW][32*NT][2] doubles).
-// conv_epi_store: one wave's 32 x 32*NT block (NW = waves of 32 rows in the tile, virtual waves
-// when a wave owns several row blocks); conv_epi_gn: the per-128-pixel-group reduction of the
-// partials in `red`, after a barrier.
-// SPL: 0 = fp32 MFMA accumulators (an h2 output follows p.bf), 1 = f16x3, 2 = bf16 single product
 // Fast path (every U-Net conv): dense NHWC output, whole tiles inside one image, no per-batch bias,
 // output columns all valid, 32-bit element offsets.  Every load (weight scale, bias, residual) is
 // issued before the first store: on gfx950 one counter (vmcnt) tracks loads AND stores, so a load
-// after a store makes the wave wait for that store to be acknowledged by memory — with the bias
-// loaded per 32-channel tile after the previous tile's 16 stores, the epilogue of a 256-pixel tile
-// took ~26 us (memory write latency x the drains, profiles/r02_zg_*) against ~0.5 us without stores.
+// after a store makes the wave wait until that store is acknowledged (the round-1 form loaded the
+// bias per 32-channel tile after the previous tile's 16 stores: 2-3 % of a 64^2 launch).  Stores go
+// through a buffer resource with the wave-uniform row offset in soffset, and the scale/bias and
+// GroupNorm sums run on packed fp32 pairs (v_pk_fma_f32), to keep the epilogue's VALU small.
 // RT row blocks of 32 pixels per wave (wave wv owns virtual waves wv0 .. wv0 + RT - 1).
 template <int NT, int SPL, int NW, int RT>
 __device__ __forceinline__ bool conv_epi_fast(const ConvParams& p, int m0) {
@@ -123,6 +116,8 @@ __device__ __forceinline__ bool conv_epi_fast(const ConvParams& p, int m0) {
     return p.osy == 1 && p.osx == 1 && p.bias_b == nullptr && p.M % (32 * NW) == 0 && p.HoWo % (32 * NW) == 0 &&
            p.Cout % BN == 0 && (long long)p.M * p.Cout < (1ll << 29);
 }
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int NT, int SPL, int NW, int RT>
 __device__ __forceinline__ void conv_epi_store_fast(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
@@ -136,50 +131,64 @@ __device__ __forceinline__ void conv_epi_store_fast(const ConvParams& p, f32x16 
     float bco[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) bco[n] = p.bias ? p.bias[n0 + n * 32 + li] : 0.f;
-    char* const yb = reinterpret_cast<char*>(p.y);
+    // accumulator row r of a lane is output pixel pix0 + (r & 3) + 8 (r >> 2): a per-lane byte
+    // offset (VGPR) plus a wave-uniform row offset (SGPR soffset)
+    const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, (unsigned)((long long)p.M * p.Cout * 4));
+    const int rowb = p.Cout * 4;
+    const f32x2 wsc2 = {wsc, wsc};
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
         const int wv = wv0 + rt;
-        const int obase = (m0 + wv * 32 + 4 * lh) * p.Cout;
+        const int pix0 = m0 + wv * 32 + 4 * lh;
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
             const int co = n0 + n * 32 + li;
-            float add[16];
+            // fp32: the element; h2: the lane's dword of its 8-channel group record (even lane the
+            // hi pair, odd lane the lo pair)
+            const bool odd = (li & 1) != 0;
+            const int vo = p.out_h2 ? pix0 * rowb + (co & ~7) * 4 + (odd ? 16 : 0) + 2 * ((co & 7) & ~1)
+                                    : (pix0 * p.Cout + co) * 4;
+            f32x2 add[8];
             if (p.resid) {  // attention proj only: the 16 residuals of this block before its stores
 #pragma unroll
-                for (int r = 0; r < 16; ++r) add[r] = bco[n] + p.resid[obase + ((r & 3) + 8 * (r >> 2)) * p.Cout + co];
+                for (int r = 0; r < 16; ++r)
+                    add[r >> 1][r & 1] = bco[n] + p.resid[(pix0 + (r & 3) + 8 * (r >> 2)) * p.Cout + co];
             } else {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) add[r] = bco[n];
+                for (int k = 0; k < 8; ++k) add[k] = (f32x2){bco[n], bco[n]};
             }
-            float s = 0.f, ss = 0.f;
+            f32x2 s2 = {0.f, 0.f}, ss2 = {0.f, 0.f};
             bool bad = false;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int e = obase + ((r & 3) + 8 * (r >> 2)) * p.Cout + co;
-                float v = (SPL ? acc[rt][n][r] * wsc : acc[rt][n][r]) + add[r];
-                if (p.act == 1) v = fmaxf(v, 0.f);
-                else if (p.act == 2) v = 1.f / (1.f + expf(-v));
-                else if (p.act == 3) v = silu_f(v);
-                if (p.out_h2) {
-                    // lane pairs (2j, 2j+1) of an 8-channel group swap halves: the even lane
-                    // stores the hi pair, the odd lane the lo pair (one dword each)
-                    const unsigned sp = split1x(v, bf);
-                    const bool odd = (li & 1) != 0;
-                    const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
-                    const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
-                    const int pe = e - co + (co & ~7);  // the 8-channel group's first element
-                    *reinterpret_cast<unsigned*>(yb + (size_t)pe * 4 + (odd ? 16 : 0) + 2 * ((co & 7) & ~1)) = word;
-                    bad = bad || (!bf && h2_bad(v));
-                } else {
-                    p.y[e] = v;
+            for (int k = 0; k < 8; ++k) {
+                const f32x2 a = {acc[rt][n][2 * k], acc[rt][n][2 * k + 1]};
+                f32x2 v2 = SPL ? a * wsc2 + add[k] : a + add[k];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int r = 2 * k + e;
+                    float v = v2[e];
+                    if (p.act == 1) v = fmaxf(v, 0.f);
+                    else if (p.act == 2) v = 1.f / (1.f + expf(-v));
+                    else if (p.act == 3) v = silu_f(v);
+                    v2[e] = v;
+                    const int so = ((r & 3) + 8 * (r >> 2)) * rowb;
+                    if (p.out_h2) {
+                        // lane pairs (2j, 2j+1) of an 8-channel group swap halves
+                        const unsigned sp = split1x(v, bf);
+                        const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
+                        const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
+                        __builtin_amdgcn_raw_buffer_store_b32(word, ry, vo, so, 0);
+                        bad = bad || (!bf && h2_bad(v));
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, vo, so, 0);
+                    }
                 }
-                s += v;
-                ss = fmaf(v, v, ss);
+                s2 += v2;
+                ss2 = v2 * v2 + ss2;
             }
             h2_flag(p.ovf, bad);
             if (gn) {
-                double ds = (double)s, dss = (double)ss;
+                double ds = (double)s2.x + (double)s2.y, dss = (double)ss2.x + (double)ss2.y;
                 ds += __shfl_xor(ds, 32);
                 dss += __shfl_xor(dss, 32);
                 if (lh == 0) {
