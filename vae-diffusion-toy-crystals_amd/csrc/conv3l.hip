@@ -656,10 +656,14 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         constexpr int s = decltype(S)::value;
         constexpr int hb = decltype(HBc)::value;
         const int c = 9 * j + t;
-        // PRO 1: raw halo j+1 published at tap 4 (even chunk) / 5 (odd); transformed in the next
-        // two taps (units 0-1, then 2-3); h2 published at tap 6 / 7
+        // PRO 1: raw halo j+1 published by the barrier of tap 4 (even chunk) / 5 (odd); one unit per
+        // tap transformed in the row-block-0 MFMA gaps from the next tap on (even chunk: taps 5-8;
+        // odd: units 0 and 1 in tap 6, then 7, 8); the h2 is published by a barrier at the end of tap
+        // 8 (an extra one in an odd chunk), so A0 of the next chunk's tap 0 is read after it
         constexpr int TR = hb ? 6 : 5;  // first transform tap
-        constexpr bool tr = PRO == 1 && (t == TR || t == TR + 1);
+        constexpr bool tr = PRO == 1 && t >= TR;
+        constexpr int u0 = hb ? (t == 6 ? 0 : t - 5) : t - 5;  // unit in the row-block-0 gaps
+        constexpr bool tr1 = PRO == 1 && hb && t == 6;         // unit 1 in the row-block-1 gaps
         const bool more = j + 1 < cpt;
         // LDS-DMA issue first thing in the tap (right after the barrier that freed the target): a
         // pair issued at the start of odd tap 2k-3 has two taps of latency cover before its wait
@@ -673,21 +677,26 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
             if (more) halo_issue(j + 1, hb ^ 1, q0, q1);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (PRO == 1 && t == 0) rd_a(0, 0, hb);  // published at the end of the last tap
         rd_b(s ^ 1, c + 1);
         if (t != 8) rd_a(1, t, hb);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (tr) mf_transform(0, s, 2 * (t - TR), hb ^ 1, more);
+        if constexpr (tr) mf_transform(0, s, u0, hb ^ 1, more);
         else mf(0, s);
         __builtin_amdgcn_sched_barrier(0);
-        if (t == 8) rd_a(0, 0, hb ^ 1);
-        else rd_a(0, t + 1, hb);
+        if (t == 8) {
+            if constexpr (PRO == 0) rd_a(0, 0, hb ^ 1);
+        } else {
+            rd_a(0, t + 1, hb);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (tr) mf_transform(1, s, 2 * (t - TR) + 1, hb ^ 1, more);
+        if constexpr (tr1) mf_transform(1, s, 1, hb ^ 1, more);
         else mf(1, s);
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
-        if constexpr (PRO == 1 && t == TR + 1) {
+        if constexpr (PRO == 1 && t == 8) {
             if (j + 2 < cpt) load_tabs(j + 2);
+            if constexpr (s == 1) barrier();  // odd chunk: publish the transformed halo
         }
         if constexpr (s == 0) {  // even tap: the barrier that publishes pair c/2 + 1 (and halo j+1:
                                  // PRO 0 at tap 6 of an even chunk / 7 of an odd one; PRO 1 the raw
@@ -744,12 +753,14 @@ int launch3l(const ConvParams& p, hipStream_t st) {
         const char* e = getenv("TCX_CONV3L_GLDS");
         return !(e && e[0] == '0');
     }();
-    // the prologue form of k_conv3lg: parity-green but no faster than the register-staged k_conv3l
-    // (its GN+SiLU transform is squeezed into two taps; profiles/r02_zk_*), so off by default
-    static const bool glds_pro = [] {
+    // the prologue form of k_conv3lg (transform spread over taps 5-8): 2-4 % faster than the
+    // register-staged k_conv3l at 64^2, 2-3 % slower at 32^2 (profiles/r02_zp_*): default at W = 64;
+    // TCX_CONV3L_GLDS_PRO=1 everywhere, =0 nowhere
+    static const int glds_pro_env = [] {
         const char* e = getenv("TCX_CONV3L_GLDS_PRO");
-        return e && e[0] == '1';
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
+    const bool glds_pro = glds_pro_env < 0 ? W == 64 : glds_pro_env == 1;
     static const int dbg = [] {
         const char* e = getenv("TCX_CONV3L_DBG");
         return e ? atoi(e) : 0;
