@@ -47,13 +47,14 @@ FP32_PEAK_TFLOPS = 157.3         # MI355X fp32 MFMA (= vector) peak, MI355X_MICR
 F16_PEAK_TFLOPS = 2500.0         # MI355X dense f16/bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 multiply-add
 # HBM bytes per conv launch (the launches the roofline times), measured by rocprofv3 PMC passes on
-# this sampler (tools/gpu/pmc_bench_traffic.sh -> tools/pmc_traffic.py, profiles/r01_x_pmc_traffic.txt):
-# FETCH_SIZE x 2 (gfx950 reports half of 16-B/lane reads) + WRITE_SIZE, averaged over the k_conv<>
-# and k_conv3h<> launches of an evaluation.  A counter pass cannot run inside this process, so the
+# this sampler (tools/gpu/verify.sh -> tools/pmc_traffic.py, profiles/r02_zq_pmc_traffic.txt):
+# FETCH_SIZE x 2 (gfx950 reports half of 16-B/lane reads) + WRITE_SIZE, averaged over the conv
+# launches of an evaluation.  A counter pass cannot run inside this process, so the
 # measured value is carried here with its source; it applies to the f16x3 path it was taken on.
-TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 504.0e6}
-TRAFFIC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE over the default kernels (k_conv3g 32/64 with and "
-                  "without the GN+SiLU prologue, k_conv3p 16, k_conv4s2h, k_conv SPL), profiles/r02_x_pmc_traffic.txt")
+TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 503.3e6}
+TRAFFIC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE over the default kernels (k_conv3lg 32/64 h2 and "
+                  "64 GN+SiLU prologue, k_conv3l 32 prologue, k_conv3g 16, k_conv4s2h, k_conv SPL), "
+                  "profiles/r02_zq_pmc_traffic.txt")
 
 
 def _cpu_model() -> str:
