@@ -1,6 +1,6 @@
 """GPU: the non-default split-path conv variants stay parity-green.
 
-The kernel variant is chosen once per process from the environment (csrc/conv3l.hip TCX_CONV3L / TCX_CONV3L_GLDS / TCX_CONV3L_GLDS_PRO, csrc/conv3g.hip TCX_CONV3G,
+The kernel variant is chosen once per process from the environment (csrc/conv3l.hip TCX_CONV3L / TCX_CONV3L_GLDS / TCX_CONV3L_GLDS_PRO / TCX_CONV3L16, csrc/conv3g.hip TCX_CONV3G,
 csrc/conv3h.hip halo_nw / halo_rt / halo_pipe, csrc/conv4s2h.hip TCX_NO_DSHALO), so each variant runs in ONE child process
 (sequential, one GPU process at a time besides this one) that checks the 3x3 and 4x4/s2 U-Net
 conv shapes against the fp64 numpy oracle at the fp32 gate (2e-5 of the output scale, as
@@ -32,11 +32,11 @@ for (B, Ci, Co, H, ks, s) in [(2, 96, 96, 64, 3, 1), (2, 192, 192, 32, 3, 1), (2
     got = run_conv_h2(x, w, b, s, 1, True)
     err = float(np.abs(got - ref).max()) / max(1.0, float(np.abs(ref).max()))
     worst = max(worst, err)
-# GroupNorm+SiLU prologue (tcx_conv2d_h2_pro) at the 64^2 and 32^2 shapes of the evaluator (only on
+# GroupNorm+SiLU prologue (tcx_conv2d_h2_pro) at the 64^2, 32^2 and 16^2 shapes of the evaluator (only on
 # the kernels that have one: not with TCX_CONV3G=0, where the evaluator falls back to apply passes)
 import os
 from test_gpu_h2 import run_conv_h2_pro, gn_silu_ref, rand_tabs
-for (B, Ci, H) in ([(2, 96, 64), (2, 192, 32)] if os.environ.get("TCX_CONV3G") != "0" else []):
+for (B, Ci, H) in ([(2, 96, 64), (2, 192, 32), (2, 192, 16)] if os.environ.get("TCX_CONV3G") != "0" else []):
     x = rng.standard_normal((B, Ci, H, H)) * 2.0
     w = rng.standard_normal((Ci, Ci, 3, 3)) / np.sqrt(Ci * 9)
     b = rng.standard_normal(Ci)
@@ -55,6 +55,8 @@ assert worst <= 2e-5, worst
     {"TCX_CONV3L_GLDS": "0"},                     # k_conv3l register-staged (not LDS-DMA) for h2 sources
     {"TCX_CONV3L_GLDS_PRO": "1"},                 # k_conv3lg's GroupNorm+SiLU prologue form at 32^2 too
     {"TCX_CONV3L_GLDS_PRO": "0"},                 # k_conv3l's register-staged prologue at 64^2 too
+    {"TCX_CONV3L16": "0"},                        # k_conv3g (not k_conv3lg) at 16-px rows
+    {"TCX_CONV3L16": "2"},                        # k_conv3lg's prologue form at 16-px rows too
     {"TCX_CONV3G": "0"},                          # k_conv3p (the round-1 default) on every 3x3 row width
     {"TCX_CONV3G": "0", "TCX_HALO_PIPE": "0"},    # unpipelined k_conv3h (4 waves, two workgroups per CU)
     {"TCX_CONV3G": "0", "TCX_HALO_PNW": "8"},     # k_conv3p with 8 waves, 256-pixel tiles

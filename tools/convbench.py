@@ -53,7 +53,7 @@ def bench(name, H, C1, C2, Co, ks, s, pad, ups, reps=20, gn=os.environ.get("GN",
             check(L.tcx_f32_to_h2(t.data_ptr(), o.data_ptr(), t.numel(), None, st))
             return o
         # PRO=1 (H2 mode): source 1 stays fp32 and k_conv3g applies GroupNorm+SiLU tables while staging
-        h2pro = os.environ.get("PRO", "0") == "1" and ks == 3 and s == 1 and C2 == 0 and H >= 32
+        h2pro = os.environ.get("PRO", "0") == "1" and ks == 3 and s == 1 and C2 == 0 and H >= 16
         hp = [t.data_ptr() for t in tabs[:2]] if (h2pro and use_pro) else [None, None]
         if hp[0] is None:
             x1 = h2(x1)

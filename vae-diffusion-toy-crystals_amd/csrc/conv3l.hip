@@ -22,6 +22,7 @@
 // (halo j+1 is stored during taps 2-5 of chunk j; an even tap lies between tap 5 and tap 8).
 //
 // LDS (one array): halo [2][NPX][64 B] with the 16-B pieces of a pixel XOR-swizzled by (col >> 2) & 3
+// (k_conv3lg at 16-px rows: (col >> 1) & 3)
 // (conflict-free ds_read_b128 of 32 consecutive pixels at any tap offset, and conflict-free
 // ds_write_b128 of 8 consecutive pixels), the B ring [2 pairs][2 taps][3 n][hi, lo][64 lanes][16 B]
 // = 24 KB, the GroupNorm tables [2][Cin]: 78 KB at W = 64, Cin = 384 — two workgroups per CU.
@@ -430,8 +431,12 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     constexpr int NIH = (NI + 1) / 2;    // per halo wave (wave 2: even i, wave 3: odd i)
     constexpr int HB = NI * 16 * 64;
     constexpr int RING = 2 * HB;
-    constexpr int RT1 = W == 64 ? 32 * 64 : W2 * 64;
-    static_assert(W == 32 || W == 64, "k_conv3lg: rows of 32 or 64 pixels");
+    // row block 1 of a wave: 32 pixels on (W = 64), the next row (32), two rows on (16)
+    constexpr int RT1 = W == 64 ? 32 * 64 : (W == 32 ? W2 * 64 : 2 * W2 * 64);
+    static_assert(W == 16 || W == 32 || W == 64, "k_conv3lg: rows of 16, 32 or 64 pixels");
+    // piece swizzle by column: (col >> 2) & 3 at 32/64-px rows; at 16-px rows a row block spans two
+    // rows, for which (col >> 1) & 3 is the conflict-free choice (exhaustive check over taps/rows)
+    auto sw = [](int col) { return W == 16 ? (col >> 1) & 3 : (col >> 2) & 3; };
     extern __shared__ __attribute__((aligned(16))) float sm[];
     char* const smc = reinterpret_cast<char*>(sm);
 
@@ -476,7 +481,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         if (sl >= NPX) hc = (NPX - 1) % W2;            // padding slots read a valid pixel
         const int x = hc == 0 ? W - 1 : (hc == W + 1 ? 0 : hc - 1);
         const int yo = (sl >= NPX) ? (img0 + wrap_idx(r0 + (NPX - 1) / W2 - 1, H)) * W * rowb : (nx ? yo1 : yo0);
-        return yo + x * rowb + 16 * ((lane & 3) ^ ((hcs >> 2) & 3));
+        return yo + x * rowb + 16 * ((lane & 3) ^ sw(hcs));
     };
     auto halo_issue = [&](int j, int buf, int q0, int q1) {
         const int ci0 = j * L_KC;
@@ -505,7 +510,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         const int rr = mloc / W, cc = mloc % W;
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx)
-            xa[dx] = (rr * W2 + cc + dx) * 64 + 16 * ((2 * lh) ^ (((cc + dx) >> 2) & 3));
+            xa[dx] = (rr * W2 + cc + dx) * 64 + 16 * ((2 * lh) ^ sw(cc + dx));
     }
     f32x16 acc[RT][NT];
 #pragma unroll
@@ -556,7 +561,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         const int hp0 = (wv & 1) * 64 + lane + 128 * i;
         const int hp = hp0 < NPXS ? hp0 : NPXS + (lane & 3);
         const int hc = hp % W2;
-        tdst[i] = hp * 64 + 16 * ((2 * tg) ^ ((hc >> 2) & 3));
+        tdst[i] = hp * 64 + 16 * ((2 * tg) ^ sw(hc));
         tval |= hp0 < NPXS ? 1u << i : 0u;
     }
     float tsc[8], tsh[8];  // this wave's group of the chunk being transformed (wave-uniform)
@@ -818,11 +823,40 @@ bool conv3l_enabled() {
 // called by launch_conv3g once conv3g_applies() holds (fragment-ordered weights, Cin % 32 == 0,
 // Cin <= 384, cout_pad % 96 == 0, whole-row tiles)
 bool conv3l_takes(const ConvParams& p) {
-    return conv3l_enabled() && !p.bf && p.circular && (p.W == 32 || p.W == 64) && p.M % L_TP == 0 &&
-           p.HoWo % L_TP == 0;
+    if (!conv3l_enabled() || p.bf || !p.circular || p.M % L_TP != 0 || p.HoWo % L_TP != 0) return false;
+    if (p.W == 32 || p.W == 64) return true;
+    // 16-px rows: the LDS-DMA kernel for h2 sources (mid.net.0: 2 % faster than k_conv3g); its
+    // GroupNorm prologue form is 9 % slower than k_conv3g's there (profiles/r02_zt_*), so that stays
+    // (TCX_CONV3L16=0: k_conv3g for both, =2: k_conv3lg for both)
+    static const int on16 = [] {
+        const char* e = getenv("TCX_CONV3L16");
+        return e ? atoi(e) : 1;
+    }();
+    const bool has2 = p.C2 > 0 && p.sc2 != nullptr;
+    if (p.W != 16 || on16 == 0 || has2) return false;
+    return p.sc1 == nullptr ? true : (on16 == 2 && p.C2 == 0);
+}
+
+// 16-px rows (the mid block, one 256-pixel tile per 16x16 image): only the LDS-DMA form exists
+template <int PRO>
+int launch3lg16(const ConvParams& p, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3lg<16, PRO>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)conv3lg_lds_bytes<16>()) != hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3lg_lds_bytes<16>());
+            return TCX_EHIP;
+        }
+        attr = true;
+    }
+    const int grid = (p.M / L_TP) * p.n_nblk;
+    void (*const kg)(ConvParams) = &k_conv3lg<16, PRO>;
+    hipLaunchKernelGGL(kg, dim3(grid), dim3(64 * L_NW), conv3lg_lds_bytes<16>(), st, p);
+    return check_launch("tcx_conv2d_h2(halo 3lg16)");
 }
 
 int launch_conv3l(const ConvParams& p, hipStream_t st) {
+    if (p.W == 16) return p.sc1 ? launch3lg16<1>(p, st) : launch3lg16<0>(p, st);
     return p.W == 64 ? launch3l<64>(p, st) : launch3l<32>(p, st);
 }
 
