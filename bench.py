@@ -229,9 +229,9 @@ def main() -> int:
         args.steps = steps_saved
 
     if args.precision == "f16x3":
-        kname = ("split-path convs: k_conv3lg (3x3, 32/64-px rows, LDS-DMA halo + weight ring; GN+SiLU prologue "
-                 "at 64^2), k_conv3l (GN+SiLU prologue at 32^2), k_conv3g (16-px rows), k_conv4s2h (4x4/s2 halo), "
-                 "k_conv<SPL> (1x1) — f16x3, 3 f16 MFMAs per fp32 MAC; all conv launches of the pass")
+        kname = ("split-path convs: k_conv3lg (3x3 at 16/32/64-px rows, LDS-DMA halo + weight ring, GN+SiLU "
+                 "prologue), k_conv3g (16-px GN+SiLU prologue), k_conv4s2h (4x4/s2 halo), k_conv<SPL> (1x1) — "
+                 "f16x3, 3 f16 MFMAs per fp32 MAC; all conv launches of the pass")
         peak = F16_PEAK_TFLOPS / SPLIT_PRODUCTS
         peak_basis = "2500 TFLOP/s dense f16 MFMA / 3 products per fp32 MAC; achieved in fp32-equivalent FLOPs"
     elif args.precision == "bf16":

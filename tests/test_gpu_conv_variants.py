@@ -53,8 +53,7 @@ assert worst <= 2e-5, worst
 @pytest.mark.parametrize("env", [
     {"TCX_CONV3L": "0"},                          # k_conv3g (B fragments from global) at 32/64-px rows
     {"TCX_CONV3L_GLDS": "0"},                     # k_conv3l register-staged (not LDS-DMA) for h2 sources
-    {"TCX_CONV3L_GLDS_PRO": "1"},                 # k_conv3lg's GroupNorm+SiLU prologue form at 32^2 too
-    {"TCX_CONV3L_GLDS_PRO": "0"},                 # k_conv3l's register-staged prologue at 64^2 too
+    {"TCX_CONV3L_GLDS_PRO": "0"},                 # k_conv3l's register-staged GroupNorm+SiLU prologue
     {"TCX_CONV3L16": "0"},                        # k_conv3g (not k_conv3lg) at 16-px rows
     {"TCX_CONV3L16": "2"},                        # k_conv3lg's prologue form at 16-px rows too
     {"TCX_CONV3G": "0"},                          # k_conv3p (the round-1 default) on every 3x3 row width

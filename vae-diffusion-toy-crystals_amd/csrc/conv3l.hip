@@ -551,13 +551,14 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
 
     // PRO 1: units of this wave: group g = wv >> 1, slots (wv & 1) 64 + lane + 128 i (i < 4)
     constexpr int NPXS = NPX;
+    constexpr int TU = (NPX + 127) / 128;  // units per thread: 4 at 64-px rows, 3 at 32 and 16
     const int tg = wv >> 1;
     // lanes past the last slot rewrite a padding slot (no divergence around MFMAs); several lanes
     // share one, so what they read may already be another lane's h2: their range flag is masked
-    int tdst[4];
+    int tdst[TU];
     unsigned tval = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < TU; ++i) {
         const int hp0 = (wv & 1) * 64 + lane + 128 * i;
         const int hp = hp0 < NPXS ? hp0 : NPXS + (lane & 3);
         const int hc = hp % W2;
@@ -611,7 +612,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     // the whole chunk's transform at once (prologue)
     auto transform_all = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < TU; ++i) {
             char* const d = smc + buf * HB + tdst[i];
             const float4 x0 = *reinterpret_cast<const float4*>(d);
             const float4 x1 = *reinterpret_cast<const float4*>(smc + buf * HB + (tdst[i] ^ 16));
@@ -666,7 +667,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         // odd: units 0 and 1 in tap 6, then 7, 8); the h2 is published by a barrier at the end of tap
         // 8 (an extra one in an odd chunk), so A0 of the next chunk's tap 0 is read after it
         constexpr int TR = hb ? 6 : 5;  // first transform tap
-        constexpr bool tr = PRO == 1 && t >= TR;
+        constexpr bool tr = PRO == 1 && t >= TR && (hb ? (t == 6 ? 0 : t - 5) : t - 5) < TU;
         constexpr int u0 = hb ? (t == 6 ? 0 : t - 5) : t - 5;  // unit in the row-block-0 gaps
         constexpr bool tr1 = PRO == 1 && hb && t == 6;         // unit 1 in the row-block-1 gaps
         const bool more = j + 1 < cpt;
@@ -758,14 +759,13 @@ int launch3l(const ConvParams& p, hipStream_t st) {
         const char* e = getenv("TCX_CONV3L_GLDS");
         return !(e && e[0] == '0');
     }();
-    // the prologue form of k_conv3lg (transform spread over taps 5-8): 2-4 % faster than the
-    // register-staged k_conv3l at 64^2, 2-3 % slower at 32^2 (profiles/r02_zp_*): default at W = 64;
-    // TCX_CONV3L_GLDS_PRO=1 everywhere, =0 nowhere
-    static const int glds_pro_env = [] {
+    // the prologue form of k_conv3lg (transform spread over taps 5-8, 3 units per thread at 32-px
+    // rows): 2-4 % faster than the register-staged k_conv3l at 64^2 (profiles/r02_zp_*), even at 32^2
+    // (r02_zu_*); default; TCX_CONV3L_GLDS_PRO=0 keeps k_conv3l for single-source prologues
+    static const bool glds_pro = [] {
         const char* e = getenv("TCX_CONV3L_GLDS_PRO");
-        return e ? (e[0] == '1' ? 1 : 0) : -1;
+        return !(e && e[0] == '0');
     }();
-    const bool glds_pro = glds_pro_env < 0 ? W == 64 : glds_pro_env == 1;
     static const int dbg = [] {
         const char* e = getenv("TCX_CONV3L_DBG");
         return e ? atoi(e) : 0;
