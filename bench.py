@@ -117,7 +117,7 @@ def main() -> int:
                     help="64 (the metric's config 2); 256 with --batch 64 = config 5's per-GPU share (512 over 8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=128)
-    ap.add_argument("--lanes", "--lanes-alt", dest="lanes", type=int, default=3,
+    ap.add_argument("--lanes", "--lanes-alt", dest="lanes", type=int, default=4,
                     help="concurrent sampling lanes of the timed region (tcx_set_sample_lanes, 1-4; images are "
                          "bit-identical for every value); the roofline pass after it always runs one lane")
     ap.add_argument("--precision", choices=["f16x3", "fp32", "bf16"], default="f16x3",

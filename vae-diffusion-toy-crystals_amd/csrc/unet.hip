@@ -858,7 +858,10 @@ LaneSync* lane_sync() {
     if (!tried) {
         tried = true;
         bool ok = true;
-        for (int i = 0; i < 4; ++i) ok = ok && hipStreamCreateWithFlags(&ls.s[i], hipStreamNonBlocking) == hipSuccess;
+        // lane 0 runs on the caller's stream, so L lanes use L streams (the box has 4 hardware queues:
+        // a fifth stream would share one and serialise)
+        ls.s[0] = nullptr;
+        for (int i = 1; i < 4; ++i) ok = ok && hipStreamCreateWithFlags(&ls.s[i], hipStreamNonBlocking) == hipSuccess;
         for (int i = 0; i < 5; ++i) ok = ok && hipEventCreateWithFlags(&ls.ev[i], hipEventDisableTiming) == hipSuccess;
         ls.ok = ok;
     }
@@ -965,8 +968,9 @@ extern "C" int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y
         const size_t lws = lane_ws_bytes(net, rows, H, W, L);
         char* wbase = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
         hipStream_t st = (hipStream_t)stream;
+        auto lst = [&](int l) { return l == 0 ? st : ls->s[l]; };
         TCX_REQUIRE(hipEventRecord(ls->ev[4], st) == hipSuccess, "tcx_sde_sample: event record");
-        for (int l = 0; l < L; ++l)
+        for (int l = 1; l < L; ++l)
             TCX_REQUIRE(hipStreamWaitEvent(ls->s[l], ls->ev[4], 0) == hipSuccess, "tcx_sde_sample: stream wait");
         for (int i = 0; i <= n_steps; ++i) {
             const float* row = scal_table + (size_t)i * TCX_SCAL;
@@ -977,15 +981,15 @@ extern "C" int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y
                     TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, y_cat + b0, y_cont + (size_t)b0 * net->y_cont_dim,
                                            b1 - b0, H, W, guidance, 1, row,
                                            noise ? noise + (size_t)i * img + e : nullptr, seed, (uint64_t)i, x + e,
-                                           nullptr, wbase + l * lws, lws, ls->s[l], e));
+                                           nullptr, wbase + l * lws, lws, lst(l), e));
                 } else {  // final projection -> image written over x
                     TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, y_cat + b0, y_cont + (size_t)b0 * net->y_cont_dim,
                                            b1 - b0, H, W, guidance, fmode, row, nullptr, seed, 0, nullptr, x + e,
-                                           wbase + l * lws, lws, ls->s[l], e));
+                                           wbase + l * lws, lws, lst(l), e));
                 }
             }
         }
-        for (int l = 0; l < L; ++l) {
+        for (int l = 1; l < L; ++l) {
             TCX_REQUIRE(hipEventRecord(ls->ev[l], ls->s[l]) == hipSuccess, "tcx_sde_sample: event record");
             TCX_REQUIRE(hipStreamWaitEvent(st, ls->ev[l], 0) == hipSuccess, "tcx_sde_sample: stream wait");
         }
@@ -1032,8 +1036,9 @@ extern "C" int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y
         const size_t lws = lane_ws_bytes(net, rows, H, W, L);
         char* wbase = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
         hipStream_t st = (hipStream_t)stream;
+        auto lst = [&](int l) { return l == 0 ? st : ls->s[l]; };
         TCX_REQUIRE(hipEventRecord(ls->ev[4], st) == hipSuccess, "tcx_ode_sample: event record");
-        for (int l = 0; l < L; ++l)
+        for (int l = 1; l < L; ++l)
             TCX_REQUIRE(hipStreamWaitEvent(ls->s[l], ls->ev[4], 0) == hipSuccess, "tcx_ode_sample: stream wait");
         for (int i = 0; i <= n_steps; ++i) {
             const float* row = scal_table + (size_t)i * TCX_SCAL;
@@ -1045,16 +1050,16 @@ extern "C" int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y
                 char* w = wbase + l * lws;
                 if (i < n_steps) {
                     TCX_TRY(unet_eval_impl(net, x + e, xe + e, row, 0, yc, yv, b1 - b0, H, W, guidance, 3, row, nullptr,
-                                           0, 0, x + e, d + e, w, lws, ls->s[l], e));
+                                           0, 0, x + e, d + e, w, lws, lst(l), e));
                     TCX_TRY(unet_eval_impl(net, xe + e, nullptr, row + TCX_SCAL, 0, yc, yv, b1 - b0, H, W, guidance, 4,
-                                           row, nullptr, 0, 0, x + e, d + e, w, lws, ls->s[l], e));
+                                           row, nullptr, 0, 0, x + e, d + e, w, lws, lst(l), e));
                 } else {
                     TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, yc, yv, b1 - b0, H, W, guidance, fmode, row,
-                                           nullptr, 0, 0, nullptr, x + e, w, lws, ls->s[l], e));
+                                           nullptr, 0, 0, nullptr, x + e, w, lws, lst(l), e));
                 }
             }
         }
-        for (int l = 0; l < L; ++l) {
+        for (int l = 1; l < L; ++l) {
             TCX_REQUIRE(hipEventRecord(ls->ev[l], ls->s[l]) == hipSuccess, "tcx_ode_sample: event record");
             TCX_REQUIRE(hipStreamWaitEvent(st, ls->ev[l], 0) == hipSuccess, "tcx_ode_sample: stream wait");
         }
