@@ -423,36 +423,22 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
     const int n8 = (p1 - p0) * C8;
     bool bad = false;
     // In place (x == y): the compiler must assume each store may alias the next loads, so the
-    // loads of GU groups are issued explicitly before any of their stores (each thread's groups are
-    // distinct elements) — and software-pipelined one batch ahead: batch n+1's loads are issued
-    // BEFORE batch n's stores, so waiting for them does not also wait for those stores (one in-order
-    // vmcnt counts loads and stores; the unpipelined loop measured 4.85-4.95 TB/s).
+    // loads of GU groups are issued explicitly before any of their stores (each thread's groups
+    // are distinct elements) — one group in flight per thread measured 4.85 TB/s.
     constexpr int GU = 4;
     int i = threadIdx.x;
-    float4 u0[GU], u1[GU];
-    auto load_batch = [&](int ib) {
+    for (; i + (GU - 1) * 256 < n8; i += GU * 256) {
+        float4 u0[GU], u1[GU];
 #pragma unroll
         for (int k = 0; k < GU; ++k) {
-            const float* src = x + base + (size_t)(ib + 256 * k) * 8;
+            const float* src = x + base + (size_t)(i + 256 * k) * 8;
             u0[k] = *reinterpret_cast<const float4*>(src);
             u1[k] = *reinterpret_cast<const float4*>(src + 4);
         }
-    };
-    if (i + (GU - 1) * 256 < n8) load_batch(i);
-    for (; i + (GU - 1) * 256 < n8; i += GU * 256) {
-        float4 w0[GU], w1[GU];
-#pragma unroll
-        for (int k = 0; k < GU; ++k) {
-            w0[k] = u0[k];
-            w1[k] = u1[k];
-        }
-        // unconditional (the last batch re-reads itself): a load under a branch makes hipcc wait
-        // for it at the join, which would serialise the pipeline again
-        load_batch(i + GU * 256 + (GU - 1) * 256 < n8 ? i + GU * 256 : i);
 #pragma unroll
         for (int k = 0; k < GU; ++k) {
             const int c0 = ((i + 256 * k) % C8) * 8;
-            float4 v0 = w0[k], v1 = w1[k];
+            float4 v0 = u0[k], v1 = u1[k];
             v0.x = fmaf(v0.x, sc[c0], sh[c0]); v0.y = fmaf(v0.y, sc[c0 + 1], sh[c0 + 1]);
             v0.z = fmaf(v0.z, sc[c0 + 2], sh[c0 + 2]); v0.w = fmaf(v0.w, sc[c0 + 3], sh[c0 + 3]);
             v1.x = fmaf(v1.x, sc[c0 + 4], sh[c0 + 4]); v1.y = fmaf(v1.y, sc[c0 + 5], sh[c0 + 5]);
