@@ -132,11 +132,13 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from toycrystals_amd.dist import all_reduce_, dist_backend, local_device
+    device = local_device(local_rank)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(device)
+        backend = dist_backend()  # nccl (RCCL); TCX_DIST_BACKEND=gloo only to rehearse ranks sharing a GPU
+        dist.init_process_group(backend, **({"device_id": device} if backend == "nccl" else {}))
 
     from toycrystals_amd._lib import lib, set_conv_precision
     set_conv_precision(args.precision)
@@ -153,9 +155,11 @@ def main() -> int:
     shape = (B, 1, S, S)
 
     def run(i: int) -> torch.Tensor:
+        # rank r samples images [r*B, (r+1)*B) of ONE global batch: one seed per pass, the shard's
+        # Philox element offset (dist.sample_sharded semantics), so N GPUs = the 1-GPU images of N*B
         return sample_reverse_sde_euler_maruyama(model, sde, y_cat, y_cont, shape, n_steps=args.n_steps,
                                                  guidance_scale=args.cfg, t_end=args.t_end,
-                                                 seed=1_000_003 * (rank + 1) + i)
+                                                 seed=1_000_003 + i, elem_offset=rank * B * S * S)
 
     _last_out = [None]
 
@@ -172,7 +176,7 @@ def main() -> int:
         if world > 1:
             dist.barrier()
             t = torch.tensor([el], device=device, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            all_reduce_(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el
 

@@ -306,8 +306,20 @@ int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const
                       int B, int H, int W, int n_steps, float guidance, const float* scal_table,
                       int flags, void* ws, size_t ws_bytes, void* stream);
 
+/* tcx_sde_sample_ex on one shard of a larger sampling batch (batch-DP sampling):
+ * the Philox counter of element i of x is e_base + i, so images [s, e) of a B-image batch sampled
+ * with e_base = s*H*W are bit-identical to those rows of the whole batch sampled in one call with the
+ * same seed (the reference draws ONE stream for the whole batch, sde_score_model.py:537,557).
+ * e_base = 0 is tcx_sde_sample_ex.  Host-injected `noise` is this shard's slice. */
+int tcx_sde_sample_shard(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont,
+                         int B, int H, int W, int n_steps, float guidance, const float* scal_table,
+                         const float* noise, uint64_t seed, int flags, uint64_t e_base, void* ws,
+                         size_t ws_bytes, void* stream);
+
 /* Standard normal draws from Philox4x32-10 (+ Box-Muller), keyed (seed, stream id). */
 int tcx_randn(float* out, size_t n, uint64_t seed, uint64_t stream_id, void* stream);
+/* The same draws for elements [e_off, e_off + n) of the (seed, stream id) sequence: a shard of x_T. */
+int tcx_randn_at(float* out, size_t n, uint64_t seed, uint64_t stream_id, uint64_t e_off, void* stream);
 
 /* ------------------------------------------------------------------ latent prior / MLP */
 

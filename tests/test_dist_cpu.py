@@ -86,8 +86,16 @@ def _bucket_worker(rank, world, port, q):
         for step in range(2):
             g = torch.Generator().manual_seed(100 * step + rank)
             x = torch.randn(8, 16, generator=g)
-            for p in model.parameters():
-                p.grad = None
+            if step == 0:  # a step begun without zero_grad(): the hooks adopt the fresh gradients
+                for p in model.parameters():
+                    p.grad = None
+            else:  # gradient-as-bucket-view: autograd accumulates straight into the buckets
+                ar.zero_grad()
+                flats = [f for _, f, _ in ar.buckets]
+                in_bucket = all(any(f.data_ptr() <= p.grad.data_ptr() < f.data_ptr() + f.numel() * 4 for f in flats)
+                                for p in model.parameters())
+                if not in_bucket:
+                    raise AssertionError("zero_grad() did not point the gradients into the buckets")
             model(x).square().mean().backward()
             ar.finish()
             got = [p.grad.clone() for p in model.parameters()]
@@ -134,13 +142,17 @@ def _presence_worker(rank, world, port, q):
         some = torch.nn.Parameter(torch.ones(3))    # gets a gradient on rank 0 only
         never = torch.nn.Parameter(torch.ones(5))   # no rank produces a gradient
         ar = BucketedGradAllReduce([used, some, never], bucket_mb=1e-6)  # one bucket per parameter
-        loss = (used * (rank + 1)).sum()
-        if rank == 0:
-            loss = loss + (some * 4.0).sum()
-        loss.backward()
-        ar.finish()
-        ok = (torch.allclose(used.grad, torch.full((4,), (1 + world) / 2))
-              and torch.allclose(some.grad, torch.full((3,), 4.0 / world)) and never.grad is None)
+        ok = True
+        for step in range(2):  # step 0 from grad None, step 1 from zero_grad()'s bucket views
+            if step == 1:
+                ar.zero_grad()
+            loss = (used * (rank + 1)).sum()
+            if rank == 0:
+                loss = loss + (some * 4.0).sum()
+            loss.backward()
+            ar.finish()
+            ok = ok and (torch.allclose(used.grad, torch.full((4,), (1 + world) / 2))
+                         and torch.allclose(some.grad, torch.full((3,), 4.0 / world)) and never.grad is None)
         q.put((rank, ok, ""))
     except Exception as e:  # report instead of leaving the parent waiting on the queue
         q.put((rank, False, repr(e)))

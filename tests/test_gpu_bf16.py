@@ -183,3 +183,102 @@ def test_bf16_unet_forward_vs_reference(golden, name):
     print(f"{name}: bf16 {e1:.2e}, f16x3 {e2:.2e} of the output scale vs the reference fp32 forward")
     assert e2 < 2e-5
     assert e1 < 3e-2 and e1 > 10 * e2  # really the bf16 path (8-bit operands), within its gate
+
+
+@pytest.fixture
+def bf16():
+    from toycrystals_amd import _lib
+    old = _lib.conv_precision()
+    _lib.set_conv_precision("bf16")
+    yield
+    _lib.set_conv_precision(old)
+
+
+def test_bf16_sde_256px_vs_reference(golden, bf16):
+    """Config 5's sampler at 256x256 in bf16 (2 reverse-SDE steps + projection, CFG 1.5, base 96)
+    against the reference's fp32 run of the same draws (sde96_2step_h256).  Stated gates for 8-bit
+    operands: x0_hat within 3e-2 of max(1, |x0_hat|max) (observed 3.7e-3), image mean-abs 5e-3; the
+    image is (x0_hat + 1)/2 clamped, so its max-abs gate is half the x0_hat gate in absolute terms
+    (this untrained net's x0_hat reaches tens, so single pixels move by ~0.2, observed printed)."""
+    from test_gpu_models import run_sde, unet
+    from toycrystals_amd.models.sde_score_model import host_noise
+    g = golden("sde96_2step_h256")
+    m = unet(96)
+    B = int(g["B"])
+    shape = (B, 1, 256, 256)
+    torch.manual_seed(int(g["noise_seed"]))
+    noise = host_noise(shape, int(g["steps"]) + 1)
+    out, x0 = run_sde(m, g, noise.cuda(), shape)
+    img = float(np.abs(out - g["out"]).max())
+    x0e = float(np.abs(x0 - g["x0_unclamped"]).max()) / max(1.0, float(np.abs(g["x0_unclamped"]).max()))
+    print(f"bf16 sde96_2step_h256: image max-abs {img:.3e} mean-abs {float(np.abs(out - g['out']).mean()):.3e}, "
+          f"x0_hat rel {x0e:.3e}")
+    scale = max(1.0, float(np.abs(g["x0_unclamped"]).max()))
+    assert x0e < 3e-2 and float(np.abs(out - g["out"]).mean()) < 5e-3 and img <= 0.5 * 3e-2 * scale
+    assert np.abs(np.clip((x0 + 1.0) * 0.5, 0.0, 1.0) - out).max() < 1e-6
+
+
+def test_bf16_trained_sde300_trajectory_drift(golden):
+    """How far the bf16 path's 300-step reverse SDE (CFG 1.5, t_end 0.005) drifts from the fp32-grade
+    f16x3 trajectory and from the reference's own fp32 run, on the trained base-96 model
+    (trained96_ema, B = 8, the reference's recorded draws; /root/reference/src/toycrystals/models/
+    sde_score_model.py:507-569).  Measured (r03_a): the image differs from the f16x3 trajectory by
+    2.4e-3 mean-abs, but single pixels by up to 0.33 (x0_hat up to 0.62 of its scale): the per-step
+    bf16 rounding (~7e-3 of a forward) is absorbed on most of the image and amplified at a few
+    unstable pixels of the stochastic trajectory.  Stated bounds vs both references: image mean-abs
+    <= 5e-3, max-abs <= 0.5, and at most 2 % of the pixels off by more than 1e-2 (printed)."""
+    from test_gpu_models import run_sde, unet
+    from toycrystals_amd import _lib
+    from toycrystals_amd.models.sde_score_model import host_noise
+    g = golden("sde96_trained_300")
+    m = unet(96, golden("trained96_ema"))
+    B, steps = int(g["B"]), int(g["steps"])
+    torch.manual_seed(int(g["noise_seed"]))
+    noise = host_noise((B, 1, 64, 64), steps + 1).cuda()
+    old = _lib.conv_precision()
+    try:
+        _lib.set_conv_precision("f16x3")
+        out_h2, x0_h2 = run_sde(m, g, noise, (B, 1, 64, 64))
+        _lib.set_conv_precision("bf16")
+        out_bf, x0_bf = run_sde(m, g, noise, (B, 1, 64, 64))
+    finally:
+        _lib.set_conv_precision(old)
+    scale = max(1.0, float(np.abs(g["x0_unclamped"]).max()))
+    for what, ref_img, ref_x0 in (("f16x3", out_h2, x0_h2), ("reference fp32", g["out"], g["x0_unclamped"])):
+        d = np.abs(out_bf - ref_img)
+        x0e = float(np.abs(x0_bf - ref_x0).max()) / scale
+        off = float((d > 1e-2).mean())
+        print(f"bf16 300-step vs {what}: image max-abs {float(d.max()):.3e} mean-abs {float(d.mean()):.3e}, "
+              f"p99 {float(np.quantile(d, 0.99)):.3e}, p99.9 {float(np.quantile(d, 0.999)):.3e}, "
+              f"pixels off by > 1e-2: {100 * off:.2f} %, x0_hat rel {x0e:.3e}")
+        assert float(d.mean()) <= 5e-3 and float(d.max()) <= 0.5 and off <= 0.02
+    assert float(np.abs(out_h2 - g["out"]).max()) < 1e-4  # the fp32-grade path on the same run
+    assert float(np.abs(out_bf - out_h2).max()) > 1e-5  # really the bf16 path
+
+
+def test_bf16_256px_b64_workload(bf16):
+    """Config 5's per-GPU workload: 256x256, B = 64 (512 over 8 GPUs), 300 reverse-SDE steps, CFG 1.5,
+    bf16, in-kernel Philox.  With CFG the 128 rows exceed the 84-row pass cap (2 GiB activations),
+    so every evaluation runs two passes (42 + 22 images).  The images are finite and in [0, 1], and
+    each checked image equals itself sampled alone at its Philox element offset, bit for bit (first
+    and last of each pass).  This random-init net saturates the clamped image, so the same check runs
+    on the unclamped x0_hat too (every pixel of the trajectory)."""
+    from test_gpu_models import unet
+    from toycrystals_amd.models.sde_score_model import VPSDE, sample_reverse_sde_euler_maruyama
+    m = unet(96)
+    sde = VPSDE(0.1, 30.0)
+    B, S = 64, 256
+    y_cat = (torch.arange(B) % 4).cuda()
+    y_cont = torch.zeros(B, 4, device="cuda")
+    y_cont[:, 1] = torch.linspace(0.0, np.pi / 3, B, device="cuda")
+    kw = dict(n_steps=300, guidance_scale=1.5, t_end=0.005, seed=77)
+    x = sample_reverse_sde_euler_maruyama(m, sde, y_cat, y_cont, (B, 1, S, S), **kw)
+    assert bool(torch.isfinite(x).all()) and float(x.min()) >= 0.0 and float(x.max()) <= 1.0
+    print(f"bf16 256px B=64: mean {float(x.mean()):.4f}, unsaturated {float(((x > 0) & (x < 1)).float().mean()):.3f}")
+    x0 = sample_reverse_sde_euler_maruyama(m, sde, y_cat, y_cont, (B, 1, S, S), return_x0_hat=True, **kw)
+    assert bool(torch.isfinite(x0).all())
+    assert torch.equal(torch.clamp((x0 + 1.0) * 0.5, 0.0, 1.0), x)
+    for i in (0, 41, 42, 63):
+        xi = sample_reverse_sde_euler_maruyama(m, sde, y_cat[i:i + 1], y_cont[i:i + 1], (1, 1, S, S),
+                                               elem_offset=i * S * S, return_x0_hat=True, **kw)
+        assert torch.equal(xi[0], x0[i]), (i, float((xi[0] - x0[i]).abs().max()))

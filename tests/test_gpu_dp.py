@@ -107,3 +107,32 @@ def test_prior_step_shards_equal_full_batch():
 
     full = step(slice(0, B))
     _compare(full, [step(slice(0, B // 2)), step(slice(B // 2, B))], "DiffusionPriorFiLM MSE")
+
+
+@pytest.mark.parametrize("sampler_name", ["sde", "ode"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_sample_sharded_equals_one_gpu_run(monkeypatch, sampler_name, world):
+    """dist.sample_sharded: every rank samples its shard with the batch's ONE seed and its Philox
+    element offset, so the concatenated shards equal the whole batch sampled in one call, bit for
+    bit (ragged shards at B = 7; the reference draws one stream per batch, sde_score_model.py:537,557).
+    Ranks are emulated in one process through RANK / WORLD_SIZE (no process group: gather=False)."""
+    from toycrystals_amd.dist import sample_sharded
+    from toycrystals_amd.models.sde_score_model import (CondUNetTiny, VPSDE, sample_probability_flow_ode,
+                                                        sample_reverse_sde_euler_maruyama)
+    fn = sample_reverse_sde_euler_maruyama if sampler_name == "sde" else sample_probability_flow_ode
+    torch.manual_seed(0)
+    model = CondUNetTiny(4, 4, 32).cuda().eval()
+    sde = VPSDE(0.1, 30.0)
+    B = 7
+    y_cat = (torch.arange(B) % 4).cuda()
+    y_cont = torch.zeros(B, 4, device="cuda")
+    y_cont[:, 1] = torch.linspace(0, 1.0, B, device="cuda")
+    kw = dict(n_steps=3, guidance_scale=1.5, t_end=0.005)
+    full = fn(model, sde, y_cat, y_cont, (B, 1, 64, 64), seed=11, **kw)
+    parts = []
+    for r in range(world):
+        monkeypatch.setenv("RANK", str(r))
+        monkeypatch.setenv("WORLD_SIZE", str(world))
+        parts.append(sample_sharded(fn, model, sde, y_cat, y_cont, (B, 1, 64, 64), base_seed=11, gather=False, **kw))
+    assert sum(p.shape[0] for p in parts) == B
+    assert torch.equal(torch.cat(parts), full)

@@ -394,9 +394,9 @@ __device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t sid, uint
     return sqrtf(-2.0f * logf(u1)) * cosf(kTwoPi * u2);
 }
 
-__global__ void k_randn(float* out, size_t n, uint64_t seed, uint64_t sid) {
+__global__ void k_randn(float* out, size_t n, uint64_t seed, uint64_t sid, uint64_t e_off) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        out[i] = philox_normal(seed, sid, i);
+        out[i] = philox_normal(seed, sid, e_off + i);
 }
 
 // ---------------------------------------------------------------- fused out-conv gather + update
@@ -953,9 +953,10 @@ extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, con
                           x_inout, eps_out, ws, ws_bytes, (hipStream_t)stream, 0);
 }
 
-extern "C" int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
-                                 int H, int W, int n_steps, float guidance, const float* scal_table, const float* noise,
-                                 uint64_t seed, int flags, void* ws, size_t ws_bytes, void* stream) {
+extern "C" int tcx_sde_sample_shard(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
+                                    int H, int W, int n_steps, float guidance, const float* scal_table,
+                                    const float* noise, uint64_t seed, int flags, uint64_t e_base, void* ws,
+                                    size_t ws_bytes, void* stream) {
     TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_sde_sample: bad args");
     TCX_REQUIRE((flags & ~TCX_SAMPLE_X0_HAT) == 0, "tcx_sde_sample: unknown flags %d", flags);
     const int fmode = (flags & TCX_SAMPLE_X0_HAT) ? 5 : 2;
@@ -981,11 +982,11 @@ extern "C" int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y
                     TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, y_cat + b0, y_cont + (size_t)b0 * net->y_cont_dim,
                                            b1 - b0, H, W, guidance, 1, row,
                                            noise ? noise + (size_t)i * img + e : nullptr, seed, (uint64_t)i, x + e,
-                                           nullptr, wbase + l * lws, lws, lst(l), e));
+                                           nullptr, wbase + l * lws, lws, lst(l), e_base + e));
                 } else {  // final projection -> image written over x
                     TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, y_cat + b0, y_cont + (size_t)b0 * net->y_cont_dim,
                                            b1 - b0, H, W, guidance, fmode, row, nullptr, seed, 0, nullptr, x + e,
-                                           wbase + l * lws, lws, lst(l), e));
+                                           wbase + l * lws, lws, lst(l), e_base + e));
                 }
             }
         }
@@ -995,16 +996,24 @@ extern "C" int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y
         }
         return TCX_OK;
     }
+    hipStream_t st = (hipStream_t)stream;
     for (int i = 0; i < n_steps; ++i) {
         const float* row = scal_table + (size_t)i * TCX_SCAL;
-        TCX_TRY(tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 1, row,
-                              noise ? noise + (size_t)i * img : nullptr, seed, (uint64_t)i, x, nullptr, ws, ws_bytes,
-                              stream));
+        TCX_TRY(unet_eval_impl(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 1, row,
+                               noise ? noise + (size_t)i * img : nullptr, seed, (uint64_t)i, x, nullptr, ws, ws_bytes,
+                               st, e_base));
     }
     // final projection -> image written over x
     const float* row = scal_table + (size_t)n_steps * TCX_SCAL;
-    return tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, fmode, row, nullptr, seed, 0,
-                         nullptr, x, ws, ws_bytes, stream);
+    return unet_eval_impl(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, fmode, row, nullptr, seed, 0,
+                          nullptr, x, ws, ws_bytes, st, e_base);
+}
+
+extern "C" int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
+                                 int H, int W, int n_steps, float guidance, const float* scal_table, const float* noise,
+                                 uint64_t seed, int flags, void* ws, size_t ws_bytes, void* stream) {
+    return tcx_sde_sample_shard(net, x, y_cat, y_cont, B, H, W, n_steps, guidance, scal_table, noise, seed, flags, 0,
+                                ws, ws_bytes, stream);
 }
 
 extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
@@ -1084,10 +1093,14 @@ extern "C" int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_ca
     return tcx_ode_sample_ex(net, x, y_cat, y_cont, B, H, W, n_steps, guidance, scal_table, 0, ws, ws_bytes, stream);
 }
 
-extern "C" int tcx_randn(float* out, size_t n, uint64_t seed, uint64_t stream_id, void* stream) {
+extern "C" int tcx_randn_at(float* out, size_t n, uint64_t seed, uint64_t stream_id, uint64_t e_off, void* stream) {
     TCX_REQUIRE(out, "tcx_randn: null pointer");
     if (n == 0) return TCX_OK;
     const int blocks = (int)std::min<size_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_randn, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, n, seed, stream_id);
+    hipLaunchKernelGGL(k_randn, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, n, seed, stream_id, e_off);
     return check_launch("tcx_randn");
+}
+
+extern "C" int tcx_randn(float* out, size_t n, uint64_t seed, uint64_t stream_id, void* stream) {
+    return tcx_randn_at(out, n, seed, stream_id, 0, stream);
 }

@@ -11,6 +11,8 @@ if _PKG_ROOT not in sys.path:
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from toycrystals_amd.dist import all_reduce_, broadcast_, dist_backend, local_device  # noqa: E402
+
 
 def pick_device(name: str) -> torch.device:
     """The reference falls back to CPU without CUDA; this build has no CPU path, so it refuses."""
@@ -22,15 +24,25 @@ def pick_device(name: str) -> torch.device:
 
 
 def init_dp():
-    """One process per GPU under torchrun (backend nccl = RCCL over xGMI); (rank, world, device)."""
+    """One process per GPU under torchrun (backend nccl = RCCL over xGMI; TCX_DIST_BACKEND=gloo lets
+    ranks share one GPU, toycrystals_amd.dist); (rank, world, device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return 0, 1, None
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", rank=rank, world_size=world)
-    return rank, world, torch.device("cuda", local)
+    device = local_device(local)
+    torch.cuda.set_device(device)
+    dist.init_process_group(dist_backend(), rank=rank, world_size=world)
+    return rank, world, device
+
+
+def lead_only_rng(device):
+    """Context for work only rank 0 does between training steps (sample grids): its torch CPU and
+    device generator draws are rolled back afterwards, so every rank's generators stay in lockstep
+    (the shuffle permutation and the --global-draws noise of the next steps are the same on all
+    ranks, and equal the one-GPU run's)."""
+    return torch.random.fork_rng(devices=[device])
 
 
 def shutdown_dp(world: int) -> None:
@@ -43,7 +55,7 @@ def allreduce_scalar_mean(v: float, world: int, device) -> float:
     if world <= 1:
         return v
     t = torch.tensor([v], dtype=torch.float64, device=device)
-    dist.all_reduce(t)
+    all_reduce_(t)
     return float(t.item()) / world
 
 
@@ -59,6 +71,6 @@ def broadcast_from_lead(tensors, world: int, device):
     out = []
     for i, (shape, dtype) in enumerate(meta[0]):
         buf = tensors[i].to(device).contiguous() if dist.get_rank() == 0 else torch.empty(shape, dtype=dtype, device=device)
-        dist.broadcast(buf, src=0)
+        broadcast_(buf, src=0)
         out.append(buf.cpu())
     return out

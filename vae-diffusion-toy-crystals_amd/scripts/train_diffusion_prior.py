@@ -203,7 +203,7 @@ def main() -> int:
                 q = torch.clamp((t.float() / args.T * 4).long(), 0, 3)
                 bucket_sum.index_add_(0, q, per_s)
                 bucket_n.index_add_(0, q, torch.ones_like(per_s))
-            opt.zero_grad(set_to_none=True)
+            grad_ar.zero_grad()  # grads = zeroed views into the all-reduce buckets
             loss.backward()
             grad_ar.finish()
             opt.step()
@@ -213,8 +213,9 @@ def main() -> int:
         if lead:
             print(f"epoch {epoch + 1:02d}/{args.epochs} diffusion_loss={avg:.6f}")
             torch.save(prior.state_dict(), "checkpoints/diffusion_prior_last.pt")
-            save_diffusion_samples(vae=vae, prior=prior, sched=sched, out_path="results/diffusion_samples.png",
-                                   device=device, z_mean=z_mean, z_std=z_std, ddim_steps=args.ddim_steps)
+            with _common.lead_only_rng(device):  # the other ranks do not draw: keep the streams in step
+                save_diffusion_samples(vae=vae, prior=prior, sched=sched, out_path="results/diffusion_samples.png",
+                                       device=device, z_mean=z_mean, z_std=z_std, ddim_steps=args.ddim_steps)
             bucket_avg = (bucket_sum / torch.clamp(bucket_n, min=1)).detach().cpu().tolist()
             print("  bucket loss (low t -> high t):", [f"{v:.3f}" for v in bucket_avg])
     if lead:

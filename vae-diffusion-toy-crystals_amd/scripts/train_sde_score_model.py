@@ -156,7 +156,7 @@ def main() -> int:
                 draws = (u[sl], eps[sl], drop[sl] if drop is not None else None)
             loss = diffusion_loss_eps(model=model, sde=sde, x0=x0, y_cat=y_cat, y_cont=y_cont,
                                       p_uncond=args.p_uncond, t_power=args.t_power, draws=draws)
-            opt.zero_grad(set_to_none=True)
+            grad_ar.zero_grad()  # grads = zeroed views into the all-reduce buckets
             loss.backward()
             grad_ar.finish()
             opt.step()
@@ -174,8 +174,9 @@ def main() -> int:
             if ((epoch + 1) % args.sample_every == 0) or (epoch == args.epochs - 1):
                 out_path = os.path.join(results_dir, f"sde_samples_epoch_{epoch + 1:03d}.png")
                 sample_model = ema_model if (ema_model is not None and args.sample_from_ema == 1) else model
-                save_sde_samples(model=sample_model, sde=sde, out_path=out_path, device=device,
-                                 steps=args.sample_steps, cfg=args.cfg, t_end=args.t_end)
+                with _common.lead_only_rng(device):  # the other ranks do not draw: keep the streams in step
+                    save_sde_samples(model=sample_model, sde=sde, out_path=out_path, device=device,
+                                     steps=args.sample_steps, cfg=args.cfg, t_end=args.t_end)
                 print(f"  saved: {out_path}")
     if lead:
         import matplotlib

@@ -203,7 +203,7 @@ def main() -> int:
             kl_used, kl_raw = kl_stats(mu, logvar, free_bits=args.free_bits)
             beta = args.beta * min(1.0, (epoch + 1) / 5.0)
             loss = recon + beta * kl_used
-            opt.zero_grad(set_to_none=True)
+            grad_ar.zero_grad()  # grads = zeroed views into the all-reduce buckets
             loss.backward()
             grad_ar.finish()
             opt.step()

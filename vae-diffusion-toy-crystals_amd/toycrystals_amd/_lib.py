@@ -120,7 +120,10 @@ _SIGS = {
                                   c_fp, c_fp, c_u64, c_int, c_fp, c_size, c_fp]),
     "tcx_ode_sample_ex": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_float,
                                   c_fp, c_int, c_fp, c_size, c_fp]),
+    "tcx_sde_sample_shard": (c_int, [ctypes.POINTER(TcxUnet), c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_float,
+                                     c_fp, c_fp, c_u64, c_int, c_u64, c_fp, c_size, c_fp]),
     "tcx_randn": (c_int, [c_fp, c_size, c_u64, c_u64, c_fp]),
+    "tcx_randn_at": (c_int, [c_fp, c_size, c_u64, c_u64, c_u64, c_fp]),
     "tcx_linear": (c_int, [c_fp, c_int, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_linear_workspace": (c_size, [c_int, c_int, c_int, c_int]),
     "tcx_linear_ws": (c_int, [c_fp, c_int, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp,

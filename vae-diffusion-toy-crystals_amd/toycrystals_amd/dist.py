@@ -1,9 +1,16 @@
 """Data-parallel helpers (one process per GPU, torch.distributed; backend "nccl" is RCCL on ROCm).
 
 Sampling shards over independent images (GroupNorm is per sample, CFG pairs stay on one rank),
-so the data path has no collective: each rank samples a contiguous slice of the batch with its
-own noise stream; `gather_shards` optionally collects the images (a B*16 KB all-gather at the
-end).  SURVEY.md §8(e).
+so the data path has no collective: each rank samples a contiguous slice of the batch, with the
+ONE seed of the whole batch and its slice's Philox element offset, so an N-rank run produces the
+1-rank images bit for bit; `gather_shards` optionally collects them (a B*16 KB all-gather at the
+end).  Training is batch-DP with bucketed gradient all-reduces (`BucketedGradAllReduce`).
+SURVEY.md §8(e).
+
+Backend: "nccl" (RCCL over xGMI) unless TCX_DIST_BACKEND overrides it.  "gloo" lets several ranks
+share ONE GPU (RCCL refuses two ranks per device), which is how the world-2 tests run the real
+training scripts on a one-GPU box; gloo collectives on device tensors are staged through host
+memory here (`all_reduce_`, `broadcast_`, `all_gather_`), so the data path is the same code.
 """
 from __future__ import annotations
 
@@ -12,6 +19,67 @@ from typing import Optional, Tuple
 
 import torch
 import torch.distributed as dist
+
+
+def dist_backend() -> str:
+    """The process-group backend of this job: TCX_DIST_BACKEND, default "nccl" (RCCL)."""
+    b = os.environ.get("TCX_DIST_BACKEND", "nccl").strip().lower()
+    if b not in ("nccl", "gloo"):
+        raise ValueError(f"TCX_DIST_BACKEND must be nccl or gloo, got {b!r}")
+    return b
+
+
+def local_device(local_rank: int) -> torch.device:
+    """This rank's GPU.  Under gloo several ranks may share one device (ranks map round-robin onto
+    the visible GPUs); RCCL needs one GPU per rank."""
+    n = torch.cuda.device_count()
+    if n < 1:
+        raise SystemExit("no GPU visible: this build runs on the MI355X only")
+    if dist_backend() == "nccl" and local_rank >= n:
+        raise SystemExit(f"LOCAL_RANK {local_rank} but only {n} GPU(s): RCCL needs one GPU per rank "
+                         f"(TCX_DIST_BACKEND=gloo shares a GPU between ranks)")
+    return torch.device("cuda", local_rank % n)
+
+
+def _host_staged(t: torch.Tensor, group=None) -> bool:
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+class _Done:
+    """Completed-work handle for a collective that ran synchronously."""
+
+    def wait(self) -> bool:
+        return True
+
+
+def all_reduce_(t: torch.Tensor, op=None, group=None, async_op: bool = False):
+    """In-place all-reduce (sum by default) of a device tensor on either backend."""
+    op = dist.ReduceOp.SUM if op is None else op
+    if _host_staged(t, group):
+        h = t.detach().cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+        return _Done() if async_op else None
+    return dist.all_reduce(t, op=op, group=group, async_op=async_op)
+
+
+def broadcast_(t: torch.Tensor, src: int = 0, group=None) -> None:
+    if _host_staged(t, group):
+        h = t.detach().cpu()
+        dist.broadcast(h, src=src, group=group)
+        t.copy_(h)
+        return
+    dist.broadcast(t, src=src, group=group)
+
+
+def all_gather_(bufs, t: torch.Tensor, group=None) -> None:
+    if _host_staged(t, group):
+        hs = [torch.empty(b.shape, dtype=b.dtype) for b in bufs]
+        dist.all_gather(hs, t.detach().cpu(), group=group)
+        for b, h in zip(bufs, hs):
+            b.copy_(h)
+        return
+    dist.all_gather(bufs, t, group=group)
 
 
 def rank_world() -> Tuple[int, int]:
@@ -30,7 +98,8 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 def rank_seed(base_seed: int, rank: int) -> int:
-    """Distinct Philox key per rank (64-bit golden-ratio stride)."""
+    """Distinct Philox key per rank (64-bit golden-ratio stride), for per-rank streams that are not
+    meant to reproduce a one-GPU run (e.g. --global-draws 0 training draws)."""
     return (base_seed + 0x9E3779B97F4A7C15 * (rank + 1)) & ((1 << 63) - 1)
 
 
@@ -41,7 +110,7 @@ def gather_shards(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor
     pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local
     bufs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(bufs, pad, group=group)
+    all_gather_(bufs, pad, group=group)
     parts = []
     for r in range(world):
         s, e = shard_range(n_total, r, world)
@@ -51,12 +120,18 @@ def gather_shards(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor
 
 def sample_sharded(sampler, model, sde, y_cat: torch.Tensor, y_cont: torch.Tensor, img_shape, *,
                    base_seed: int = 0, gather: bool = True, **kw) -> torch.Tensor:
-    """Run `sampler` (e.g. sample_reverse_sde_euler_maruyama) on this rank's slice of the batch."""
+    """Run `sampler` (sample_reverse_sde_euler_maruyama / sample_probability_flow_ode) on this
+    rank's slice [s, e) of the batch with the batch's one seed and Philox element offset s*H*W:
+    the gathered images equal a one-GPU run of the whole batch with the same seed bit for bit
+    (the reference draws one noise stream for the whole batch, sde_score_model.py:537,557)."""
     rank, world = rank_world()
     B = img_shape[0]
     s, e = shard_range(B, rank, world)
+    per_img = 1
+    for d in img_shape[1:]:
+        per_img *= int(d)
     local = sampler(model, sde, y_cat[s:e], y_cont[s:e], (e - s,) + tuple(img_shape[1:]),
-                    seed=rank_seed(base_seed, rank), **kw)
+                    seed=int(base_seed), elem_offset=s * per_img, **kw)
     if gather and world > 1:
         return gather_shards(local, B)
     return local
@@ -69,7 +144,7 @@ def allreduce_grads_(params, group=None) -> None:
         return
     world = dist.get_world_size(group)
     flat = torch.cat([g.reshape(-1) for g in grads])
-    dist.all_reduce(flat, group=group)
+    all_reduce_(flat, group=group)
     flat.div_(world)
     off = 0
     for g in grads:
@@ -82,23 +157,25 @@ class BucketedGradAllReduce:
     """Gradient averaging overlapped with the backward pass (batch-DP training).
 
     Parameters are grouped, in reverse registration order (roughly the order backward produces
-    their gradients), into buckets of about `bucket_mb` MB.  A post-accumulate-grad hook per
-    parameter copies the fresh gradient into its bucket's flat buffer; once a bucket is complete
-    AND every bucket before it has been launched, its all-reduce is launched asynchronously (RCCL
-    runs it on its own stream, ordered after the producing kernels) while the rest of the backward
-    pass is still being computed.  Launching strictly in bucket order keeps every rank's sequence
-    of collectives identical even if the ranks' graphs produce gradients in different orders.
-    `finish()` launches what is left, waits, divides by the world size and points every `p.grad`
-    at its slice of the averaged buffer.  Same result as `allreduce_grads_` (one flat bucket after
-    backward); the 412 MB of FiLM-prior gradients no longer serialise behind the backward pass.
+    their gradients), into buckets of about `bucket_mb` MB, each ONE flat device buffer.  Gradients
+    live in the buckets: `zero_grad()` zeroes the buffers and points every `p.grad` at its slice
+    (gradient-as-bucket-view), so autograd accumulates each fresh gradient straight into the bucket
+    (`grad += new` in place) and nothing is copied.  A post-accumulate-grad hook per parameter
+    counts arrivals; once a bucket is complete AND every bucket before it has been launched, its
+    all-reduce is launched asynchronously (RCCL runs it on its own stream, ordered after the
+    producing kernels) while the rest of the backward pass is still being computed.  Launching
+    strictly in bucket order keeps every rank's sequence of collectives identical even if the
+    ranks' graphs produce gradients in different orders.  `finish()` launches what is left, waits
+    and divides by the world size; the averaged gradients are then already in `p.grad`.
 
     Gradient presence: each bucket carries one extra slot per parameter (1 if this rank produced
     a gradient for it, summed by the same all-reduce).  A parameter no rank produced a gradient for
-    keeps `p.grad = None` — as in a single-process run, where torch.optim.Adam (and the fused Adam)
+    gets `p.grad = None` — as in a single-process run, where torch.optim.Adam (and the fused Adam)
     then skips it; one that only some ranks produced is averaged with zeros from the others (the
     global-batch mean).
 
-    Usage per step: ``opt.zero_grad(set_to_none=True); loss.backward(); ar.finish(); opt.step()``.
+    Usage per step: ``ar.zero_grad(); loss.backward(); ar.finish(); opt.step()``.  At world 1 it
+    is a plain ``zero_grad(set_to_none=True)`` and `finish()` does nothing.
     """
 
     def __init__(self, params, bucket_mb: float = 25.0, group=None) -> None:
@@ -116,7 +193,7 @@ class BucketedGradAllReduce:
                 cur, cur_bytes = [], 0
         if cur:
             self._add_bucket(cur)
-        self.pending = [0] * len(self.buckets)
+        self.arrived = [set() for _ in self.buckets]
         self.works = [None] * len(self.buckets)
         self.next_launch = 0
         self.hooks = []
@@ -134,21 +211,48 @@ class BucketedGradAllReduce:
             off += p.numel()
         self.buckets.append((ps, flat, n))
 
+    def _view(self, p) -> torch.Tensor:
+        bi, off, _ = self.where[id(p)]
+        return self.buckets[bi][1][off:off + p.numel()].view_as(p)
+
+    def zero_grad(self) -> None:
+        """Start a step: every gradient a zeroed view into its bucket (world 1: grads set to None)."""
+        if self.world <= 1:
+            for p in self.params:
+                p.grad = None
+            return
+        for bi, (ps, flat, n) in enumerate(self.buckets):
+            flat.zero_()
+            for p in ps:
+                p.grad = self._view(p)
+            self.arrived[bi] = set()
+            self.works[bi] = None
+        self.next_launch = 0
+
     def _launch(self, bi) -> None:
-        self.works[bi] = dist.all_reduce(self.buckets[bi][1], group=self.group, async_op=True)
+        ps, flat, n = self.buckets[bi]
+        if len(self.arrived[bi]) == len(ps):
+            flat[n:].fill_(1.0)
+        else:  # some parameter got no gradient on this rank: presence 0 in its slot (zeros in its data)
+            pres = torch.tensor([1.0 if id(p) in self.arrived[bi] else 0.0 for p in ps], dtype=flat.dtype)
+            flat[n:].copy_(pres)
+        self.works[bi] = all_reduce_(flat, group=self.group, async_op=True)
 
     def _launch_ready(self) -> None:
         while (self.next_launch < len(self.buckets)
-               and self.pending[self.next_launch] == len(self.buckets[self.next_launch][0])):
+               and len(self.arrived[self.next_launch]) == len(self.buckets[self.next_launch][0])):
             self._launch(self.next_launch)
             self.next_launch += 1
 
     def _on_grad(self, p) -> None:
-        bi, off, j = self.where[id(p)]
-        ps, flat, n = self.buckets[bi]
-        flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
-        flat[n + j] = 1.0
-        self.pending[bi] += 1
+        bi, _, _ = self.where[id(p)]
+        g = p.grad
+        view = self._view(p)
+        if g is not None and g.data_ptr() != view.data_ptr():
+            # the step was not started by zero_grad() (grad was None): adopt the fresh gradient
+            view.copy_(g)
+            p.grad = view
+        self.arrived[bi].add(id(p))
         self._launch_ready()
 
     def finish(self) -> None:
@@ -156,12 +260,8 @@ class BucketedGradAllReduce:
             return
         missing = set()
         for bi in range(self.next_launch, len(self.buckets)):
-            ps, flat, n = self.buckets[bi]
-            for j, p in enumerate(ps):
-                if p.grad is None:  # no gradient on this rank: zeros in its slot, presence 0
-                    _, off, _ = self.where[id(p)]
-                    flat[off:off + p.numel()].zero_()
-                    flat[n + j] = 0.0
+            for p in self.buckets[bi][0]:
+                if id(p) not in self.arrived[bi]:
                     missing.add(id(p))
             self._launch(bi)
         for bi, (ps, flat, n) in enumerate(self.buckets):
@@ -176,10 +276,9 @@ class BucketedGradAllReduce:
                 counts.update({id(p): c[j] for j, p in enumerate(ps) if id(p) in missing})
         for bi, (ps, flat, n) in enumerate(self.buckets):
             for p in ps:
-                _, off, _ = self.where[id(p)]
                 keep = id(p) not in missing or counts[id(p)] > 0
-                p.grad = flat[off:off + p.numel()].view_as(p) if keep else None
-            self.pending[bi] = 0
+                p.grad = self._view(p) if keep else None
+            self.arrived[bi] = set()
             self.works[bi] = None
         self.next_launch = 0
 

@@ -546,7 +546,8 @@ def sample_reverse_sde_euler_maruyama(model: CondUNetTiny, sde: VPSDE, y_cat: to
                                       guidance_scale: float = 0.0, t_end: float = 1e-3, *,
                                       noise: Optional[torch.Tensor] = None,
                                       seed: Optional[int] = None,
-                                      return_x0_hat: bool = False) -> torch.Tensor:
+                                      return_x0_hat: bool = False,
+                                      elem_offset: int = 0) -> torch.Tensor:
     """Reverse-time SDE via Euler-Maruyama, t: 1 -> t_end (sde_score_model.py:507-569).
 
     The whole loop runs natively (tcx_sde_sample): per step ONE fused CFG-doubled U-Net
@@ -556,6 +557,9 @@ def sample_reverse_sde_euler_maruyama(model: CondUNetTiny, sde: VPSDE, y_cat: to
     `seed` (default: drawn from torch's global CPU generator, so torch.manual_seed governs it).
     `return_x0_hat=True` returns the projection x0_hat = (x - sigma eps)/max(alpha, 1e-6) of :566
     itself, before the reference's (x0_hat + 1)/2 map and clamp (:568-569).
+    `elem_offset`: Philox element offset of x[0] in a larger batch (a data-parallel shard, see
+    dist.sample_sharded): rows [s, e) of a batch sampled with elem_offset = s*H*W equal those rows of
+    the whole batch sampled in one call with the same seed.
     """
     device, B, H, W, t_end, y_cat, y_cont = _sampler_prologue(model, y_cat, y_cont, img_shape, t_end)
     pk = model.tcx_pack(device)
@@ -579,10 +583,10 @@ def sample_reverse_sde_euler_maruyama(model: CondUNetTiny, sde: VPSDE, y_cat: to
         if noise is not None:
             x.copy_(noise[0].view_as(x))
         else:
-            check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
-        check(L.tcx_sde_sample_ex(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g,
-                                  ptr(tab), ptr(zs) if zs is not None else None, seed, flags, ptr(ws), nbytes, st),
-              "tcx_sde_sample")
+            check(L.tcx_randn_at(ptr(x), x.numel(), seed, 0, int(elem_offset), st), "tcx_randn")
+        check(L.tcx_sde_sample_shard(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g,
+                                     ptr(tab), ptr(zs) if zs is not None else None, seed, flags, int(elem_offset),
+                                     ptr(ws), nbytes, st), "tcx_sde_sample")
     pk.run(H, W, launch)
     return x
 
@@ -593,9 +597,11 @@ def sample_probability_flow_ode(model: CondUNetTiny, sde: VPSDE, y_cat: torch.Te
                                 guidance_scale: float = 0.0, t_end: float = 1e-3, *,
                                 x_init: Optional[torch.Tensor] = None,
                                 seed: Optional[int] = None,
-                                return_x0_hat: bool = False) -> torch.Tensor:
+                                return_x0_hat: bool = False,
+                                elem_offset: int = 0) -> torch.Tensor:
     """Deterministic probability-flow ODE with Heun steps (sde_score_model.py:452-504).
-    `return_x0_hat=True`: the unclamped projection of :500 instead of the image of :503-504."""
+    `return_x0_hat=True`: the unclamped projection of :500 instead of the image of :503-504.
+    `elem_offset`: Philox element offset of x_T[0] in a larger batch (as for the reverse SDE)."""
     device, B, H, W, t_end, y_cat, y_cont = _sampler_prologue(model, y_cat, y_cont, img_shape, t_end)
     pk = model.tcx_pack(device)
     tab = step_table(sde, n_steps, t_end).to(device)
@@ -612,7 +618,7 @@ def sample_probability_flow_ode(model: CondUNetTiny, sde: VPSDE, y_cat: torch.Te
         if x_init is not None:
             x.copy_(x_init.to(device=device, dtype=torch.float32).view_as(x))
         else:
-            check(L.tcx_randn(ptr(x), x.numel(), seed, 0, st), "tcx_randn")
+            check(L.tcx_randn_at(ptr(x), x.numel(), seed, 0, int(elem_offset), st), "tcx_randn")
         check(L.tcx_ode_sample_ex(ctypes.byref(pk.net), ptr(x), ptr(y_cat), ptr(y_cont), B, H, W, int(n_steps), g,
                                   ptr(tab), TCX_SAMPLE_X0_HAT if return_x0_hat else 0, ptr(ws), nbytes, st),
               "tcx_ode_sample")
