@@ -256,3 +256,17 @@ def test_torch_oracle_trained_sde300_one_image(golden):
     ref = g["x0_unclamped"][:1]
     err = np.abs(x0 - ref).max()
     assert err < 1e-5, err
+
+
+def test_config1_fixture_is_consistent(golden):
+    """tests/golden/config1_vae_5k_b128.npz (the reference's CPU train_vae run, config 1): 39 steps
+    of 128 distinct items from 5,000, standard-normal draws, and the logged epoch average is the
+    mean of the logged steps (what the reference script prints, train_vae.py:314-331)."""
+    import numpy as np
+    g = golden("config1_vae_5k_b128")
+    assert g["steps"].shape == (39, 4) and g["eps"].shape == (39, 128, 32)
+    order = g["order"]
+    assert order.shape == (39 * 128,) and len(set(order.tolist())) == order.size and order.max() < 5000
+    assert abs(float(g["eps"].mean())) < 0.01 and abs(float(g["eps"].std()) - 1.0) < 0.01
+    assert np.allclose(g["epoch"], g["steps"].mean(axis=0))
+    assert np.all(g["steps"][:, 2] >= 32 * 0.05 - 1e-6)  # kl_used >= free bits x z_dim

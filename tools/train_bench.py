@@ -67,7 +67,7 @@ def bench_score():
 def bench_vae():
     from toycrystals_amd.models.vae import CondVAE
     torch.manual_seed(0)
-    B = 128
+    B = int(os.environ.get("B_VAE", "128"))
     m = CondVAE(z_dim=32, n_types=4, y_cont_dim=4, cond_drop=0.1).cuda().train()
     opt = Adam(m.parameters(), lr=2e-3)
     x = torch.rand(B, 1, 64, 64, device="cuda")
@@ -90,7 +90,7 @@ def bench_prior():
     from toycrystals_amd._lib import check, lib, ptr, stream_ptr
     from toycrystals_amd.models.diffusion_prior import DiffusionPriorFiLM, DiffusionSchedule
     torch.manual_seed(0)
-    B, T = 256, 1000
+    B, T = int(os.environ.get("B_PRIOR", "256")), 1000
     m = DiffusionPriorFiLM(32, 4, 4, t_emb_dim=64, width=1024, n_blocks=8, y_cat_emb_dim=64).cuda().train()
     opt = Adam(m.parameters(), lr=1e-4)
     sched = DiffusionSchedule.linear(T, 1e-4, 0.05, torch.device("cuda"))

@@ -147,6 +147,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--cond", dest="uncond", action="store_false", help="Train conditional VAE.")
     p.add_argument("--free-bits", type=float, default=0.05, help="Free bits threshold in nats per latent dim (0 disables).")
     p.set_defaults(uncond=False)
+    # additive (not in the reference): replay a recorded reference run
+    p.add_argument("--replay-draws", type=str, default="",
+                   help="npz with a reference run's DataLoader item order ('order') and reparameterisation draws "
+                        "('eps' [steps, B, z]) (tests/golden/make_config1_golden.py): train on exactly those "
+                        "batches and draws and log every step to results/vae_steps.jsonl (parity runs)")
     # additive (not in the reference): batch-DP draw semantics
     p.add_argument("--global-draws", type=int, default=1, choices=[0, 1],
                    help="1: every rank draws the reparameterisation eps and the condition-dropout mask for the "
@@ -169,7 +174,16 @@ def main() -> int:
     else:  # the reference's in-memory renderer (:259-260): non-rot-only, generator seed --seed
         ds = ToyCrystalsDataset(n_samples=args.n_samples, img_size=args.img_size, seed=args.seed,
                                 device=device).materialize()
-    dl = DeviceBatches(ds, args.batch_size, device, shuffle=True, drop_last=True, rank=rank, world=world)
+    replay = None
+    if args.replay_draws:
+        import numpy as np
+        z = np.load(args.replay_draws, allow_pickle=False)
+        replay = {"order": torch.from_numpy(z["order"].astype(np.int64)), "eps": torch.from_numpy(z["eps"])}
+        if args.uncond or args.cond_drop > 0.0:
+            raise SystemExit("--replay-draws covers the conditional VAE with --cond-drop 0 (reparameterise draws only)")
+    dl = DeviceBatches(ds, args.batch_size, device, shuffle=True, drop_last=True, rank=rank, world=world,
+                       fixed_order=None if replay is None else replay["order"])
+    step_log = open(os.path.join("results", "vae_steps.jsonl"), "w", encoding="utf-8") if (replay and lead) else None
     if args.uncond:
         model = VAE(z_dim=args.z_dim).to(device)
     else:
@@ -188,9 +202,13 @@ def main() -> int:
     for epoch in range(args.epochs):
         model.train()
         tot = torch.zeros(4, device=device, dtype=torch.float64)
-        for x, y_cat, y_cont in dl:
+        for step, (x, y_cat, y_cont) in enumerate(dl):
             draws = None
-            if args.global_draws:
+            if replay is not None:
+                per = x.shape[0]
+                k = epoch * len(dl) + step
+                draws = (replay["eps"][k, rank * per:(rank + 1) * per].to(device), None)
+            elif args.global_draws:
                 # reference order (vae.py:57-60 then :65-67): reparam eps, then the keep mask
                 Bg, per = args.batch_size, x.shape[0]
                 sl = slice(rank * per, (rank + 1) * per)
@@ -208,6 +226,11 @@ def main() -> int:
             grad_ar.finish()
             opt.step()
             tot += torch.stack([loss.detach(), recon.detach(), kl_used.detach(), kl_raw.detach()]).double()
+            if step_log is not None:
+                import json
+                step_log.write(json.dumps({"epoch": epoch + 1, "step": step + 1, "loss": float(loss.item()),
+                                           "recon": float(recon.item()), "kl_used": float(kl_used.item()),
+                                           "kl_raw": float(kl_raw.item())}) + "\n")
         nb = max(len(dl), 1)
         avg = [_common.allreduce_scalar_mean(v / nb, world, device) for v in tot.tolist()]
         loss_hist.append(avg[0])
@@ -216,6 +239,8 @@ def main() -> int:
         klr_hist.append(avg[3])
         if lead:
             print(f"epoch {epoch + 1:02d}/{args.epochs} loss={avg[0]:.4f} recon={avg[1]:.4f} kl={avg[2]:.6f}")
+            if step_log is not None:
+                step_log.flush()
             torch.save(model.state_dict(), "checkpoints/vae_last.pt")
     if lead:
         x0, y0_cat, y0_cont = next(iter(dl))

@@ -41,7 +41,8 @@ class DeviceBatches:
 
     def __init__(self, ds: ToyCrystalsDiskDataset, batch_size: int, device, shuffle: bool = True,
                  drop_last: bool = True, rank: int = 0, world: int = 1,
-                 generator: Optional[torch.Generator] = None) -> None:
+                 generator: Optional[torch.Generator] = None,
+                 fixed_order: Optional[torch.Tensor] = None) -> None:
         if batch_size % world != 0:
             raise ValueError(f"global batch {batch_size} must be divisible by world size {world}")
         self.device = torch.device(device)
@@ -58,6 +59,12 @@ class DeviceBatches:
         self.batch_size, self.shuffle, self.drop_last = int(batch_size), shuffle, drop_last
         self.rank, self.world = rank, world
         self.generator = generator
+        # a recorded item order (replay of a reference run's DataLoader permutation): used for
+        # every epoch instead of a fresh shuffle
+        self.fixed_order = None if fixed_order is None else torch.as_tensor(fixed_order, dtype=torch.int64)
+        if self.fixed_order is not None and self.fixed_order.numel() < len(self) * self.batch_size:
+            raise ValueError(f"fixed_order holds {self.fixed_order.numel()} items, an epoch needs "
+                             f"{len(self) * self.batch_size}")
 
     def __len__(self) -> int:
         if self.drop_last:
@@ -65,7 +72,10 @@ class DeviceBatches:
         return (self.N + self.batch_size - 1) // self.batch_size
 
     def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
-        order = torch.randperm(self.N, generator=self.generator) if self.shuffle else torch.arange(self.N)
+        if self.fixed_order is not None:
+            order = self.fixed_order
+        else:
+            order = torch.randperm(self.N, generator=self.generator) if self.shuffle else torch.arange(self.N)
         order = order.to(self.device)
         L = lib()
         st = stream_ptr(self.device)
