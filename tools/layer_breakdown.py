@@ -4,8 +4,11 @@ import collections, csv, sys
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if 'tcx' in r['Kernel_Name']]
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 seq, cur = [], []
+# an evaluation starts at k_cond (per-evaluation conditioning) or, when the sampler hoisted it
+# (k_cond_maps once per call), at the first conv
+starts = 'k_cond(' if any('k_cond(' in r['Kernel_Name'] for r in rows) else 'k_conv_first'
 for r in rows:
-    if 'k_cond' in r['Kernel_Name']:
+    if starts in r['Kernel_Name']:
         if cur:
             seq.append(cur)
         cur = []

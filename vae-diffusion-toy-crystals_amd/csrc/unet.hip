@@ -115,6 +115,96 @@ __global__ __launch_bounds__(CT) void k_cond(CondArgs a, const float* __restrict
     }
 }
 
+// Sampler form of the conditioning (round 3): the reference recomputes timestep_embedding + time_mlp
+// and ConditionEmbedding for every U-Net call (sde_score_model.py:243-252), but over one sampling
+// call t takes only the n_t values of the step table and the condition rows never change.  One
+// launch per call computes them all: block i < n_t the time map of t = tvals[i * tstride] (time_ch
+// values), block n_t + r the condition map of image r (r == B: the null token with y_cont = 0, the
+// unconditional half of every CFG batch).  Same per-value arithmetic as k_cond (cond_mv), so the
+// first conv's folded bias (k_conv_first FOLD form) is bit-identical to the per-evaluation path.
+__global__ __launch_bounds__(CT) void k_cond_maps(CondArgs a, const float* __restrict__ tvals, int tstride, int n_t,
+                                                  const int64_t* __restrict__ y_cat, const float* __restrict__ y_cont,
+                                                  int B, float* __restrict__ tmaps, float* __restrict__ cmaps) {
+    __shared__ float te[256], h1[256], te2[256], yv[16], g1[256], c2[256], u[512], ce[256];
+    __shared__ float red[16 * 256];
+    const int E = a.E, half = E / 2;
+    const int j = threadIdx.x;
+    if ((int)blockIdx.x < n_t) {  // uniform per block
+        const float tv = tvals[(size_t)blockIdx.x * tstride];
+        if (j < E) {
+            const int k = j < half ? j : j - half;
+            const float fr = expf((-kLn1e4 * (float)k) / (float)(half > 1 ? half - 1 : 1));
+            const float arg = (kTwoPi * tv) * fr;
+            te[j] = j < half ? cosf(arg) : sinf(arg);
+        }
+        __syncthreads();
+        cond_mv(a.time_w1t, a.time_b1, te, E, E, h1, red, true);
+        cond_mv(a.time_w2t, a.time_b2, h1, E, E, te2, red, false);
+        cond_mv(a.ttm_wt, a.ttm_b, te2, E, a.time_ch, tmaps + (size_t)blockIdx.x * a.time_ch, red, false);
+        return;
+    }
+    const int r = blockIdx.x - n_t;
+    const bool null_c = r >= B;
+    if (j < a.ycd) {  // as k_cond: y[1] = sin(theta), y[2] = cos(sin(theta)) (the reference's view quirk)
+        float v = null_c ? 0.f : y_cont[(size_t)r * a.ycd + j];
+        const float th = null_c ? 0.f : y_cont[(size_t)r * a.ycd + 1];
+        if (j == 1) v = sinf(th);
+        if (j == 2) v = cosf(sinf(th));
+        yv[j] = v;
+    }
+    __syncthreads();
+    cond_mv(a.cmlp_w1t, a.cmlp_b1, yv, a.ycd, E, g1, red, true);
+    cond_mv(a.cmlp_w2t, a.cmlp_b2, g1, E, E, c2, red, false);
+    if (j < E) {
+        long long yc = null_c ? a.n_types : y_cat[r];
+        yc = yc < 0 ? 0 : (yc > a.n_types ? a.n_types : yc);
+        u[j] = silu_f(a.cat_emb[(size_t)yc * E + j]);
+        u[E + j] = silu_f(c2[j]);
+    }
+    __syncthreads();
+    cond_mv(a.cout_wt, a.cout_b, u, 2 * E, E, ce, red, false);
+    cond_mv(a.tcm_wt, a.tcm_b, ce, E, a.cond_ch, cmaps + (size_t)r * a.cond_ch, red, false);
+}
+
+// The first-conv bias of every (step, image) of a sampling call: the fold of k_cond (conv_b +
+// sum_c maps[c] * map_wsum[co][c], time channels first, the same fmaf order), written once per call
+// as bias_tab[n_t][B + 1][C0] (row B: the null token) so an evaluation only reads its rows.
+__global__ __launch_bounds__(256) void k_bias_table(const float* __restrict__ tmaps, const float* __restrict__ cmaps,
+                                                    const float* __restrict__ map_wsum, const float* __restrict__ conv_b,
+                                                    int time_ch, int cond_ch, int C0, int B, int n_t,
+                                                    float* __restrict__ bias_tab) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)n_t * (B + 1) * C0) return;
+    const int co = (int)(i % C0);
+    const int r = (int)((i / C0) % (B + 1));
+    const int step = (int)(i / ((size_t)C0 * (B + 1)));
+    const int nm = time_ch + cond_ch;
+    const float* tm = tmaps + (size_t)step * time_ch;
+    const float* cm = cmaps + (size_t)r * cond_ch;
+    float s = conv_b[co];
+    for (int c = 0; c < time_ch; ++c) s = fmaf(tm[c], map_wsum[co * nm + c], s);
+    for (int c = 0; c < cond_ch; ++c) s = fmaf(cm[c], map_wsum[co * nm + time_ch + c], s);
+    bias_tab[i] = s;
+}
+
+// One evaluation's view of the table: its images' bias rows and the null-token row.
+struct CondTab {
+    const float* bias_img;   // [B][C0] of this evaluation's images (null: per-evaluation k_cond)
+    const float* bias_null;  // [C0] the null-token row (CFG's unconditional half)
+};
+
+__device__ __forceinline__ const float* cond_bias_row(const CondTab& ct, int row, int B, int cfg, int C0) {
+    return (cfg && row < B) ? ct.bias_null : ct.bias_img + (size_t)(row % B) * C0;
+}
+
+// generic first-conv path: gather the rows into the per-evaluation bias buffer
+__global__ __launch_bounds__(256) void k_fold_bias(CondTab ct, int C0, int B, int cfg, int Bt, float* __restrict__ bias_b) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= Bt * C0) return;
+    const int row = i / C0, co = i - row * C0;
+    bias_b[i] = cond_bias_row(ct, row, B, cfg, C0)[co];
+}
+
 // First conv of down1 (17 -> C0, 3x3 circular) with the 16 constant map channels already folded
 // into bias_b: y[b,p,co] = bias_b[b][co] + sum_tap w0[co][tap] * x[b % bmod][wrap(p + tap)].
 // Output-write bound (C0 floats per input float): a 64-pixel x C0 tile is built in LDS (small, so
@@ -125,7 +215,7 @@ constexpr int FIRST_PX = 64;
 __global__ __launch_bounds__(256) void k_conv_first(const float* __restrict__ x, int bmod, int H, int W, int C0,
                                                     const float* __restrict__ w0, int kpad,
                                                     const float* __restrict__ bias_b, float* __restrict__ y,
-                                                    double* __restrict__ gn) {
+                                                    double* __restrict__ gn, CondTab ct, int Bimg, int cfg) {
     extern __shared__ __attribute__((aligned(16))) float fs[];  // tile[64][C0+4] | w[9][C0] | red[4][C0][2] (dbl)
     const int LD = C0 + 4;
     float* tile = fs;
@@ -150,7 +240,7 @@ __global__ __launch_bounds__(256) void k_conv_first(const float* __restrict__ x,
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) xv[dy * 3 + dx] = xb[wrap_idx(yy + dy - 1, H) * W + wrap_idx(xx + dx - 1, W)];
     const int cq = C0 / 4;
-    const float* bb = bias_b + (size_t)b * C0;
+    const float* bb = ct.bias_img ? cond_bias_row(ct, b, Bimg, cfg, C0) : bias_b + (size_t)b * C0;
     for (int c = qtr * cq; c < (qtr + 1) * cq; c += 4) {
         float4 a = *reinterpret_cast<const float4*>(bb + c);
 #pragma unroll
@@ -600,11 +690,12 @@ int gn_tab(const tcx_unet* net, const Plan& P, int idx, int HW, int C, const dou
 // conv's staging prologue from [Bt][C] scale/shift tables (tcx_gn_finalize), with the statistics
 // coming from the producing conv's epilogue.
 int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const float* t, int t_per_sample,
-              const int64_t* y_cat, const float* y_cont, int cfg, hipStream_t st) {
+              const int64_t* y_cat, const float* y_cont, int cfg, hipStream_t st, CondTab ct = {}) {
     const int Bt = P.Bt, H = P.H, W = P.W, C = P.C, C2 = P.C2;
     const int H1 = H / 2, W1 = W / 2, H2 = H / 4, W2 = W / 4;
-    // conditioning -> per-batch first-conv bias
-    {
+    // conditioning -> per-batch first-conv bias (sampler calls: maps precomputed once per call,
+    // k_cond_maps, and folded into the bias by the first conv itself)
+    if (!ct.bias_img) {
         CondArgs a{};
         a.time_w1t = net->time_w1t; a.time_b1 = net->time_b1; a.time_w2t = net->time_w2t; a.time_b2 = net->time_b2;
         a.ttm_wt = net->ttm_wt; a.ttm_b = net->ttm_b; a.tcm_wt = net->tcm_wt; a.tcm_b = net->tcm_b;
@@ -672,12 +763,17 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     {
         const tcx_conv& c0 = net->down1_0;
         if ((H * W) % FIRST_PX == 0 && C % 16 == 0 && c0.kpad == 32) {
-            const size_t shm = ((size_t)FIRST_PX * (C + 4) + 9 * (size_t)C) * sizeof(float) + 8 * (size_t)C * sizeof(double);
+            const size_t shm = ((size_t)FIRST_PX * (C + 4) + 9 * (size_t)C) * sizeof(float) +
+                               8 * (size_t)C * sizeof(double);
             hipLaunchKernelGGL(k_conv_first, dim3(H * W / FIRST_PX, Bt), dim3(256), shm, st, x, B, H, W, C, c0.w,
-                               c0.kpad, P.bias0, P.a64, gn);
+                               c0.kpad, P.bias0, P.a64, gn, ct, B, cfg);
             TCX_TRY(check_launch("k_conv_first"));
             ns = H * W / FIRST_PX;
         } else {
+            if (ct.bias_img) {
+                hipLaunchKernelGGL(k_fold_bias, dim3(cdiv(Bt * C, 256)), dim3(256), 0, st, ct, C, B, cfg, Bt, P.bias0);
+                TCX_TRY(check_launch("k_fold_bias"));
+            }
             TCX_TRY(tcx_conv2d(x, nullptr, Bt, B, H, W, 1, 0, c0.w, nullptr, P.bias0, nullptr, P.a64, c0.cout,
                                c0.cout_pad, c0.kpad, 3, 1, 1, 1, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, st));
             ns = std::max(1, H * W / 512);
@@ -909,7 +1005,7 @@ namespace {
 int unet_eval_impl(const tcx_unet* net, const float* x, float* x2, const float* t, int t_per_sample,
                    const int64_t* y_cat, const float* y_cont, int B, int H, int W, float guidance, int mode,
                    const float* scal, const float* z, uint64_t seed, uint64_t step, float* x_inout, float* eps_out,
-                   void* ws, size_t ws_bytes, hipStream_t st, size_t e_base) {
+                   void* ws, size_t ws_bytes, hipStream_t st, size_t e_base, CondTab ct = {}) {
     TCX_TRY(validate(net, B, H, W));
     TCX_REQUIRE(x && t && y_cat && y_cont && ws, "tcx_unet_eval: null pointer");
     TCX_REQUIRE(mode >= 0 && mode <= 5, "tcx_unet_eval: bad mode");
@@ -930,8 +1026,10 @@ int unet_eval_impl(const tcx_unet* net, const float* x, float* x2, const float* 
         const int Bt = cfg ? 2 * bc : bc;
         Plan P = make_plan(net, Bt, H, W, base);
         const size_t e0 = (size_t)c0 * HW;
+        CondTab ctc = ct;
+        if (ct.bias_img) ctc.bias_img = ct.bias_img + (size_t)c0 * net->base_ch;
         TCX_TRY(unet_body(net, P, x + e0, bc, t_per_sample ? t + c0 : t, t_per_sample, y_cat + c0,
-                          y_cont + (size_t)c0 * net->y_cont_dim, cfg, st));
+                          y_cont + (size_t)c0 * net->y_cont_dim, cfg, st, ctc));
         StepArgs a{};
         a.r = P.r; a.out_b = net->out_b; a.B = bc; a.H = H; a.W = W; a.cfg = cfg; a.guidance = guidance;
         a.mode = mode; a.scal = scal; a.x = x + e0; a.x_inout = x_inout ? x_inout + e0 : nullptr;
@@ -940,6 +1038,54 @@ int unet_eval_impl(const tcx_unet* net, const float* x, float* x2, const float* 
         TCX_TRY(launch_step(a, st));
     }
     return TCX_OK;
+}
+
+// The sampler's conditioning tables (k_cond_maps), one stream-ordered allocation per sampling call:
+// tmaps [n_t][time_ch] for the step table's t values, cmaps [B + 1][cond_ch] (row B: null token).
+// TCX_COND_HOIST=0 keeps the per-evaluation k_cond (A/B).
+struct CondMaps {
+    float* buf = nullptr;
+    hipStream_t st = nullptr;
+    int time_ch = 0, cond_ch = 0, C0 = 0, B = 0, n_t = 0;
+    ~CondMaps() {
+        if (buf) (void)hipFreeAsync(buf, st);
+    }
+    float* tmaps() const { return buf; }
+    float* cmaps() const { return buf + (size_t)n_t * time_ch; }
+    float* bias() const { return cmaps() + (size_t)(B + 1) * cond_ch; }
+    CondTab at(int step, int b0) const {
+        if (!buf) return CondTab{};
+        const float* row0 = bias() + (size_t)step * (B + 1) * C0;
+        return CondTab{row0 + (size_t)b0 * C0, row0 + (size_t)B * C0};
+    }
+};
+
+int make_cond_maps(const tcx_unet* net, const float* scal_table, int n_t, const int64_t* y_cat, const float* y_cont,
+                   int B, hipStream_t st, CondMaps& cm) {
+    static const bool on = [] {
+        const char* e = getenv("TCX_COND_HOIST");
+        return !(e && e[0] == '0');
+    }();
+    if (!on) return TCX_OK;
+    cm.st = st; cm.time_ch = net->time_ch; cm.cond_ch = net->cond_ch; cm.C0 = net->base_ch; cm.B = B; cm.n_t = n_t;
+    const size_t nbias = (size_t)n_t * (B + 1) * net->base_ch;
+    const size_t n = (size_t)n_t * net->time_ch + (size_t)(B + 1) * net->cond_ch + nbias;
+    TCX_REQUIRE(hipMallocAsync(reinterpret_cast<void**>(&cm.buf), n * sizeof(float), st) == hipSuccess,
+                "tcx_sample: conditioning table allocation");
+    CondArgs a{};
+    a.time_w1t = net->time_w1t; a.time_b1 = net->time_b1; a.time_w2t = net->time_w2t; a.time_b2 = net->time_b2;
+    a.ttm_wt = net->ttm_wt; a.ttm_b = net->ttm_b; a.tcm_wt = net->tcm_wt; a.tcm_b = net->tcm_b;
+    a.cat_emb = net->cat_emb; a.cmlp_w1t = net->cmlp_w1t; a.cmlp_b1 = net->cmlp_b1;
+    a.cmlp_w2t = net->cmlp_w2t; a.cmlp_b2 = net->cmlp_b2; a.cout_wt = net->cout_wt; a.cout_b = net->cout_b;
+    a.map_wsum = net->map_wsum; a.conv_b = net->down1_0.b;
+    a.E = net->emb_dim; a.n_types = net->n_types; a.ycd = net->y_cont_dim;
+    a.time_ch = net->time_ch; a.cond_ch = net->cond_ch; a.C0 = net->base_ch;
+    hipLaunchKernelGGL(k_cond_maps, dim3(n_t + B + 1), dim3(CT), 0, st, a, scal_table, TCX_SCAL, n_t, y_cat, y_cont, B,
+                       cm.tmaps(), cm.cmaps());
+    TCX_TRY(check_launch("k_cond_maps"));
+    hipLaunchKernelGGL(k_bias_table, dim3((unsigned)((nbias + 255) / 256)), dim3(256), 0, st, cm.tmaps(), cm.cmaps(),
+                       net->map_wsum, net->down1_0.b, net->time_ch, net->cond_ch, net->base_ch, B, n_t, cm.bias());
+    return check_launch("k_bias_table");
 }
 
 }  // namespace
@@ -959,8 +1105,11 @@ extern "C" int tcx_sde_sample_shard(const tcx_unet* net, float* x, const int64_t
                                     size_t ws_bytes, void* stream) {
     TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_sde_sample: bad args");
     TCX_REQUIRE((flags & ~TCX_SAMPLE_X0_HAT) == 0, "tcx_sde_sample: unknown flags %d", flags);
+    TCX_TRY(validate(net, B, H, W));
     const int fmode = (flags & TCX_SAMPLE_X0_HAT) ? 5 : 2;
     const size_t img = (size_t)B * H * W;
+    CondMaps cmap;
+    TCX_TRY(make_cond_maps(net, scal_table, n_steps + 1, y_cat, y_cont, B, (hipStream_t)stream, cmap));
     const int L = std::min(lanes_setting(), B);
     const int rows = guidance > 0.f ? 2 * B : B;
     LaneSync* ls = L > 1 ? lane_sync() : nullptr;
@@ -982,11 +1131,11 @@ extern "C" int tcx_sde_sample_shard(const tcx_unet* net, float* x, const int64_t
                     TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, y_cat + b0, y_cont + (size_t)b0 * net->y_cont_dim,
                                            b1 - b0, H, W, guidance, 1, row,
                                            noise ? noise + (size_t)i * img + e : nullptr, seed, (uint64_t)i, x + e,
-                                           nullptr, wbase + l * lws, lws, lst(l), e_base + e));
+                                           nullptr, wbase + l * lws, lws, lst(l), e_base + e, cmap.at(i, b0)));
                 } else {  // final projection -> image written over x
                     TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, y_cat + b0, y_cont + (size_t)b0 * net->y_cont_dim,
                                            b1 - b0, H, W, guidance, fmode, row, nullptr, seed, 0, nullptr, x + e,
-                                           wbase + l * lws, lws, lst(l), e_base + e));
+                                           wbase + l * lws, lws, lst(l), e_base + e, cmap.at(i, b0)));
                 }
             }
         }
@@ -1001,12 +1150,12 @@ extern "C" int tcx_sde_sample_shard(const tcx_unet* net, float* x, const int64_t
         const float* row = scal_table + (size_t)i * TCX_SCAL;
         TCX_TRY(unet_eval_impl(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 1, row,
                                noise ? noise + (size_t)i * img : nullptr, seed, (uint64_t)i, x, nullptr, ws, ws_bytes,
-                               st, e_base));
+                               st, e_base, cmap.at(i, 0)));
     }
     // final projection -> image written over x
     const float* row = scal_table + (size_t)n_steps * TCX_SCAL;
     return unet_eval_impl(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, fmode, row, nullptr, seed, 0,
-                          nullptr, x, ws, ws_bytes, st, e_base);
+                          nullptr, x, ws, ws_bytes, st, e_base, cmap.at(n_steps, 0));
 }
 
 extern "C" int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
@@ -1028,7 +1177,10 @@ extern "C" int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y
                                  size_t ws_bytes, void* stream) {
     TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_ode_sample: bad args");
     TCX_REQUIRE((flags & ~TCX_SAMPLE_X0_HAT) == 0, "tcx_ode_sample: unknown flags %d", flags);
+    TCX_TRY(validate(net, B, H, W));
     const int fmode = (flags & TCX_SAMPLE_X0_HAT) ? 5 : 2;
+    CondMaps cmap;  // stage 2 of step i evaluates at t_{i+1}: table row i + 1
+    TCX_TRY(make_cond_maps(net, scal_table, n_steps + 1, y_cat, y_cont, B, (hipStream_t)stream, cmap));
     // Scratch for d and x_e lives at the end of the workspace.
     const size_t img = (size_t)B * H * W;
     const size_t need = tcx_unet_workspace_size(net, guidance > 0.f ? 2 * B : B, H, W);
@@ -1059,12 +1211,12 @@ extern "C" int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y
                 char* w = wbase + l * lws;
                 if (i < n_steps) {
                     TCX_TRY(unet_eval_impl(net, x + e, xe + e, row, 0, yc, yv, b1 - b0, H, W, guidance, 3, row, nullptr,
-                                           0, 0, x + e, d + e, w, lws, lst(l), e));
+                                           0, 0, x + e, d + e, w, lws, lst(l), e, cmap.at(i, b0)));
                     TCX_TRY(unet_eval_impl(net, xe + e, nullptr, row + TCX_SCAL, 0, yc, yv, b1 - b0, H, W, guidance, 4,
-                                           row, nullptr, 0, 0, x + e, d + e, w, lws, lst(l), e));
+                                           row, nullptr, 0, 0, x + e, d + e, w, lws, lst(l), e, cmap.at(i + 1, b0)));
                 } else {
                     TCX_TRY(unet_eval_impl(net, x + e, nullptr, row, 0, yc, yv, b1 - b0, H, W, guidance, fmode, row,
-                                           nullptr, 0, 0, nullptr, x + e, w, lws, lst(l), e));
+                                           nullptr, 0, 0, nullptr, x + e, w, lws, lst(l), e, cmap.at(i, b0)));
                 }
             }
         }
@@ -1074,17 +1226,18 @@ extern "C" int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y
         }
         return TCX_OK;
     }
+    hipStream_t st = (hipStream_t)stream;
     for (int i = 0; i < n_steps; ++i) {
         const float* row = scal_table + (size_t)i * TCX_SCAL;
-        TCX_TRY(tcx_unet_eval(net, x, xe, row, 0, y_cat, y_cont, B, H, W, guidance, 3, row, nullptr, 0, 0, x, d, ws,
-                              need, stream));
+        TCX_TRY(unet_eval_impl(net, x, xe, row, 0, y_cat, y_cont, B, H, W, guidance, 3, row, nullptr, 0, 0, x, d, ws,
+                               need, st, 0, cmap.at(i, 0)));
         const float* row_n = row + TCX_SCAL;  // t_{i+1}
-        TCX_TRY(tcx_unet_eval(net, xe, nullptr, row_n, 0, y_cat, y_cont, B, H, W, guidance, 4, row, nullptr, 0, 0, x,
-                              d, ws, need, stream));
+        TCX_TRY(unet_eval_impl(net, xe, nullptr, row_n, 0, y_cat, y_cont, B, H, W, guidance, 4, row, nullptr, 0, 0, x,
+                               d, ws, need, st, 0, cmap.at(i + 1, 0)));
     }
     const float* row = scal_table + (size_t)n_steps * TCX_SCAL;
-    return tcx_unet_eval(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, fmode, row, nullptr, 0, 0, nullptr,
-                         x, ws, need, stream);
+    return unet_eval_impl(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, fmode, row, nullptr, 0, 0, nullptr,
+                          x, ws, need, st, 0, cmap.at(n_steps, 0));
 }
 
 extern "C" int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,
