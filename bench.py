@@ -190,6 +190,11 @@ def main() -> int:
     torch.cuda.synchronize(device)
     elapsed = timed(lambda i: run(i))
     L.tcx_set_sample_lanes(prev_lanes)
+    # the precision the evaluator actually ran (bf16 falls back to f16x3 where the split attention does
+    # not apply, a split run to fp32 after a range overflow): a line labelled with another is invalid
+    from toycrystals_amd._lib import used_conv_precision
+    if used_conv_precision() != args.precision:
+        raise SystemExit(f"bench: requested {args.precision} but the sampler ran in {used_conv_precision()}")
 
     # Roofline pass: the same K passes on ONE stream with the conv launches bracketed by HIP events
     # (with kernels of several streams co-running, a per-launch event duration no longer times a

@@ -380,15 +380,6 @@ typedef struct tcx_prior {
     const float* out_norm_b;
 } tcx_prior;
 
-/* Diagnostics: copy the skinny-linear kernel's per-workgroup timestamps (written only when the
- * environment sets TCX_SK_VAR with bit 64): [n][2 waves][5] s_memrealtime ticks (100 MHz) at entry,
- * after the first k block, after the last MFMA, after the barrier, at exit.  Returns n copied. */
-int tcx_skinny_stamps(unsigned long long* out, int n_workgroups);
-/* Diagnostics: the 64-px 3x3 split conv's per-workgroup timestamps (written only when the
- * environment sets TCX_CONV3L_DBG=1 or 2): [n][5] = s_memrealtime ticks at entry, after the prologue,
- * after the last tap, at exit, and (XCC_ID << 32) | HW_ID.  Returns 0. */
-int tcx_conv3l_stamps(unsigned long long* out, int n_workgroups);
-
 /* Scratch bytes for tcx_prior_forward (n_steps = 0) or tcx_prior_ddim_sample (n_steps > 0). */
 size_t tcx_prior_workspace(const tcx_prior* net, int B, int n_steps);
 /* eps_pred = DiffusionPriorFiLM.forward(z_t, t, y_cat, y_cont) (diffusion_prior.py:108-127), eval mode.

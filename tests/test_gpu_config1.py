@@ -15,7 +15,8 @@ decrease; observed 1.6e-5 / 3.6e-6, r03_b), sampled final parameters at 1e-3 of 
 step moves a parameter by up to lr).  The KL terms are gated in absolute nats: with free bits 0.05 the
 gradient of kl_used is zero for every latent dim below the threshold, so which dims sit above it is
 decided by rounding-level differences late in the epoch (observed |d kl_used| 4e-3 of 1.6, |d kl_raw|
-1.3e-2 of 0.7 at step 38, while beta * kl is 1 % of the loss): gates 1e-2 and 3e-2 nats."""
+1.3e-2 of 0.7 at step 38 on the r03_b box; 1.66e-2 / 1.66e-2 on the r03_i box, where the loss still
+agreed to 1.6e-5; beta * kl is 1 % of the loss): gates 5e-2 nats for both (3 % of kl_used)."""
 import json
 import os
 import subprocess
@@ -52,7 +53,7 @@ def test_config1_train_vae_5k_b128_vs_reference_cpu_run(tmp_path, golden):
     assert rel[:, 0].max() < 1e-4 and rel[:, 1].max() < 1e-4
     dkl = np.abs(got[:, 2:] - ref[:, 2:]).max(axis=0)
     print(f"kl_used max abs diff {dkl[0]:.3e} nats, kl_raw {dkl[1]:.3e} nats")
-    assert dkl[0] < 1e-2 and dkl[1] < 3e-2
+    assert dkl[0] < 5e-2 and dkl[1] < 5e-2
     sd = torch.load(tmp_path / "checkpoints" / "vae_last.pt", map_location="cpu", weights_only=True)
     worst = (0.0, "")
     for k, v in sd.items():

@@ -1,7 +1,7 @@
 """GPU: the non-default split-path conv variants stay parity-green.
 
-The kernel variant is chosen once per process from the environment (csrc/conv3l.hip TCX_CONV3L / TCX_CONV3L_GLDS / TCX_CONV3L_GLDS_PRO / TCX_CONV3L16, csrc/conv3g.hip TCX_CONV3G,
-csrc/conv3h.hip halo_nw / halo_rt / halo_pipe, csrc/conv4s2h.hip TCX_NO_DSHALO), so each variant runs in ONE child process
+The kernel variant is chosen once per process from the environment (csrc/conv3l.hip TCX_CONV3L,
+csrc/conv3g.hip TCX_CONV3G; the measured-slower variants were removed in round 3), so each variant runs in ONE child process
 (sequential, one GPU process at a time besides this one) that checks the 3x3 and 4x4/s2 U-Net
 conv shapes against the fp64 numpy oracle at the fp32 gate (2e-5 of the output scale, as
 test_gpu_h2.py).  The default variants are covered by test_gpu_h2.py in this process."""
@@ -52,17 +52,7 @@ assert worst <= 2e-5, worst
 
 @pytest.mark.parametrize("env", [
     {"TCX_CONV3L": "0"},                          # k_conv3g (B fragments from global) at 32/64-px rows
-    {"TCX_CONV3L_GLDS": "0"},                     # k_conv3l register-staged (not LDS-DMA) for h2 sources
-    {"TCX_CONV3L_GLDS_PRO": "0"},                 # k_conv3l's register-staged GroupNorm+SiLU prologue
-    {"TCX_CONV3L16": "0"},                        # k_conv3g (not k_conv3lg) at 16-px rows
-    {"TCX_CONV3L16": "2"},                        # k_conv3lg's prologue form at 16-px rows too
-    {"TCX_CONV3G": "0"},                          # k_conv3p (the round-1 default) on every 3x3 row width
-    {"TCX_CONV3G": "0", "TCX_HALO_PIPE": "0"},    # unpipelined k_conv3h (4 waves, two workgroups per CU)
-    {"TCX_CONV3G": "0", "TCX_HALO_PNW": "8"},     # k_conv3p with 8 waves, 256-pixel tiles
-    {"TCX_CONV3G": "0", "TCX_HALO_NW": "8"},      # k_conv3h, 8 waves, grouped halo staging
-    {"TCX_CONV3G": "0", "TCX_HALO_NW": "4", "TCX_HALO_RT": "2"},  # k_conv3h, 64 pixels per wave
-    {"TCX_CONV3G": "0", "TCX_HALO_NW": "0"},      # k_conv3w wide waves
-    {"TCX_CONV3G": "0", "TCX_NO_DSHALO": "1", "TCX_NO_HALO": "1"},  # every conv through the im2col kernel
+    {"TCX_CONV3G": "0"},                          # k_conv3p (plain packed weights) on every 3x3 row width
 ])
 def test_conv_variant_vs_oracle(env):
     e = dict(os.environ)

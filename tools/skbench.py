@@ -1,5 +1,5 @@
 """Skinny-M linear microbenchmark: tcx_linear_ws at the prior's DDIM shapes, HIP-event timed
-(profiling helper; knobs via TCX_SK_VAR / TCX_NO_SKINNY)."""
+(profiling helper; TCX_NO_SKINNY=1 for the split-K GEMM)."""
 import json
 import os
 import sys
@@ -79,47 +79,10 @@ def bench_trivial(n, iters=200):
     return {"trivial_kernel_n": n, "us": round(e0.elapsed_time(e1) * 1e3 / (2 * iters), 2)}
 
 
-def stamps(M, N, K):
-    """one launch with TCX_SK_VAR bit 64 set: per-workgroup phase times (us, 100 MHz ticks)"""
-    import ctypes
-    import numpy as np
-    L = lib()
-    w = torch.randn(N, K, device="cuda") / K ** 0.5
-    npad, kpad = (N + 31) // 32 * 32, (K + 31) // 32 * 32
-    wpk = torch.empty(npad, kpad, device="cuda")
-    check(L.tcx_pack_conv_weight(w.data_ptr(), wpk.data_ptr(), N, K, 1, npad, kpad, stream_ptr()), "pack")
-    wps = [wpk.clone() for _ in range(8)]
-    b = torch.randn(N, device="cuda")
-    x = torch.randn(M, K, device="cuda")
-    y = torch.empty(M, N, device="cuda")
-    nb = int(L.tcx_linear_workspace(M, N, K, 0))
-    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device="cuda")
-    for i in range(9):  # the last launch (from a cold copy) is the one stamped
-        check(L.tcx_linear_ws(x.data_ptr(), K, None, 0, wps[i % 8].data_ptr(), b.data_ptr(), None, y.data_ptr(), M,
-                              N, npad, kpad, 0, ws.data_ptr(), nb, stream_ptr()), "linear")
-    torch.cuda.synchronize()
-    n = (N + 15) // 16 * max(1, (K + 1023) // 1024)
-    buf = (ctypes.c_ulonglong * (n * 10))()
-    got = L.tcx_skinny_stamps(ctypes.cast(buf, ctypes.c_void_p), n)
-    a = np.array(buf[:got * 10], dtype=np.float64).reshape(got, 2, 5) / 100.0  # us
-    t0 = a[:, :, 0].min()
-    a = a - t0
-    out = {"M": M, "N": N, "K": K, "wgs": got}
-    for i, nm in enumerate(["entry", "first_block", "mfma_done", "barrier", "exit"]):
-        v = a[:, :, i]
-        out[nm] = [round(float(np.percentile(v, p)), 2) for p in (0, 50, 90, 100)]
-    print(json.dumps(out), flush=True)
-
-
 if __name__ == "__main__":
-    if os.environ.get("SK_STAMPS"):
-        for M, N, K in [(36, 4096, 1024), (36, 1024, 4096), (36, 32, 1024)]:
-            stamps(M, N, K)
-        sys.exit(0)
     if os.environ.get("SK_TRIVIAL"):
         for n in (1, 1152, 1 << 20):
             print(json.dumps(bench_trivial(n)), flush=True)
         sys.exit(0)
-    var = os.environ.get("TCX_SK_VAR", "default")
     for M, N, K in [(36, 4096, 1024), (36, 1024, 4096), (36, 32, 1024)]:
-        print(json.dumps({"var": var, "copies": os.environ.get("SK_COPIES", "8"), **bench(M, N, K)}), flush=True)
+        print(json.dumps({"copies": os.environ.get("SK_COPIES", "8"), **bench(M, N, K)}), flush=True)

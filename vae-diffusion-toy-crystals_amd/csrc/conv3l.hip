@@ -51,15 +51,9 @@ __device__ __forceinline__ float l_silu(float v, float sc, float sh) {
     return y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * y));
 }
 
-// diagnostic timestamps (TCX_CONV3L_DBG=1, W = 64 without prologue only): per workgroup, wave 0,
-// s_memrealtime (100 MHz) at entry, after the prologue barrier, after the last tap, at exit, and the
-// hardware id (XCC / SE / CU / slot) of the workgroup
-constexpr int L_NSTAMP = 8192;
-__device__ unsigned long long l_stamps[L_NSTAMP][5];
-
-// PRO: 0 = every source h2; 1 = every source fp32 + GroupNorm table; 2 = per source at run time.
-// DBG: 0 product; 1 timestamps; 2 timestamps and no output stores; 3-6 ablations (launch3l)
-template <int W, int PRO, int DBG = 0>
+// PRO: 0 = every source h2; 1 = every source fp32 + GroupNorm table; 2 = per source at run time
+// (only PRO 2, the mixed two-source prologue, is launched: k_conv3lg below serves PRO 0 and 1)
+template <int W, int PRO>
 __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
     constexpr int RT = 2, NT = L_NT, BN = 32 * NT, NTHR = 64 * L_NW;
     constexpr int W2 = W + 2;
@@ -98,13 +92,6 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
     const __amdgpu_buffer_rsrc_t r1 = mk_rsrc(p.x1, p.bytes1);
     const __amdgpu_buffer_rsrc_t r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
     const __amdgpu_buffer_rsrc_t rw = mk_rsrc(reinterpret_cast<const float*>(p.wf), p.bytesw);
-    auto stamp = [&](int slot) {
-        if constexpr (DBG != 0) {
-            if (tid == 0 && blockIdx.x < L_NSTAMP) l_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();
-        }
-    };
-    stamp(0);
-
     if (PRO != 0 && (gn1 || gn2)) {
         for (int c = tid; c < Cin; c += NTHR) {
             const bool s1 = c < p.C1;
@@ -294,7 +281,6 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
         unit_write(i, 0);
     }
     __syncthreads();
-    stamp(1);
     rd_b(0, 0);
     rd_a(0, 0, 0);
 
@@ -305,7 +291,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
         constexpr int hb = decltype(HBc)::value;
         const int c = 9 * j + t;
         const bool more = j + 1 < cpt;
-        if (DBG != 6) rd_b(s ^ 1, c + 1);
+        rd_b(s ^ 1, c + 1);
         if (t != 8) rd_a(1, t, hb);  // A1(8) was read during tap 7
         __builtin_amdgcn_sched_barrier(0);
         mf(0, s);
@@ -321,17 +307,15 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
         }
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
-        if constexpr (t < UPT && DBG != 4) unit_load(more ? j + 1 : j, t);
-        if constexpr (st && DBG != 4) {
+        if constexpr (t < UPT) unit_load(more ? j + 1 : j, t);
+        if constexpr (st) {
             if constexpr (PRO == 2) unit_transform(more ? j + 1 : j, t - 2);
             unit_write(t - 2, hb ^ 1);
         }
         if constexpr (s == 0) {  // c even: pair c/2 + 1 into the ring, load pair c/2 + 2, barrier
-            if constexpr (DBG != 5) {
-                wr_pair((c >> 1) + 1);
-                ld_pair((c >> 1) + 2);
-            }
-            if constexpr (DBG != 3) __syncthreads();
+            wr_pair((c >> 1) + 1);
+            ld_pair((c >> 1) + 2);
+            __syncthreads();
         }
     };
     auto nine = [&](int j, auto E) {  // E = (9 j) & 1 = j & 1: register set of tap 0 = halo buffer
@@ -354,34 +338,11 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
     }
 
     __syncthreads();  // LDS -> epilogue reduction scratch
-    stamp(2);
-    if constexpr (DBG == 2) {  // timing only: one value per lane keeps the accumulators live
-        float v = 0.f;
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int n = 0; n < NT; ++n)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v += acc[rt][n][r];
-        if (v == 12345.f) p.y[tid] = v;
-    } else {
-        double* red = reinterpret_cast<double*>(sm);
-        conv_epi_store_rt<NT, 1, RT * L_NW, RT>(p, acc, m0, n0, RT * wv, lane, red);
-        if (p.gn) {
-            __syncthreads();
-            conv_epi_gn<NT, RT * L_NW>(p, m0, n0, tid, NTHR, red);
-        }
-    }
-    if constexpr (DBG != 0) {
+    double* red = reinterpret_cast<double*>(sm);
+    conv_epi_store_rt<NT, 1, RT * L_NW, RT>(p, acc, m0, n0, RT * wv, lane, red);
+    if (p.gn) {
         __syncthreads();
-        stamp(3);
-        if (tid == 0 && blockIdx.x < L_NSTAMP) {
-            unsigned hw;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            unsigned xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            l_stamps[blockIdx.x][4] = ((unsigned long long)xcc << 32) | hw;
-        }
+        conv_epi_gn<NT, RT * L_NW>(p, m0, n0, tid, NTHR, red);
     }
 }
 
@@ -748,50 +709,11 @@ constexpr size_t conv3lg_lds_bytes() {
 
 template <int W>
 int launch3l(const ConvParams& p, hipStream_t st) {
-    const size_t shm = conv3l_lds_bytes(W, p.Cin);
-    static bool attr[3] = {};
     const bool has1 = p.sc1 != nullptr, has2 = p.C2 > 0 && p.sc2 != nullptr;
-    const int pro = !has1 && !has2 ? 0 : ((has1 && (p.C2 == 0 || has2)) ? 1 : 2);
-    using K = void (*)(ConvParams);
-    const K ks[3] = {&k_conv3l<W, 0>, &k_conv3l<W, 1>, &k_conv3l<W, 2>};
-    K kc = ks[pro];
-    static const bool glds = [] {
-        const char* e = getenv("TCX_CONV3L_GLDS");
-        return !(e && e[0] == '0');
-    }();
-    // the prologue form of k_conv3lg (transform spread over taps 5-8, 3 units per thread at 32-px
-    // rows): 2-4 % faster than the register-staged k_conv3l at 64^2 (profiles/r02_zp_*), even at 32^2
-    // (r02_zu_*); default; TCX_CONV3L_GLDS_PRO=0 keeps k_conv3l for single-source prologues
-    static const bool glds_pro = [] {
-        const char* e = getenv("TCX_CONV3L_GLDS_PRO");
-        return !(e && e[0] == '0');
-    }();
-    static const int dbg = [] {
-        const char* e = getenv("TCX_CONV3L_DBG");
-        return e ? atoi(e) : 0;
-    }();
-    // diagnostics (wrong results except 1 and 2): 1 stamps, 2 no output stores, 3 no barriers in the
-    // tap loop, 4 no halo staging in the loop, 5 no B pair staging, 6 no B fragment reads
-    if (W == 64 && pro == 0 && dbg == 1) kc = &k_conv3l<64, 0, 1>;
-    if (W == 64 && pro == 0 && dbg == 2) kc = &k_conv3l<64, 0, 2>;
-    if (W == 64 && pro == 0 && dbg == 3) kc = &k_conv3l<64, 0, 3>;
-    if (W == 64 && pro == 0 && dbg == 4) kc = &k_conv3l<64, 0, 4>;
-    if (W == 64 && pro == 0 && dbg == 5) kc = &k_conv3l<64, 0, 5>;
-    if (W == 64 && pro == 0 && dbg == 6) kc = &k_conv3l<64, 0, 6>;
-    if (dbg) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)conv3l_lds_bytes(W, 384));
-    }
-    if (!attr[pro]) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)conv3l_lds_bytes(W, 384)) != hipSuccess) {
-            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3l_lds_bytes(W, 384));
-            return TCX_EHIP;
-        }
-        attr[pro] = true;
-    }
     const int grid = (p.M / L_TP) * p.n_nblk;
-    if ((pro == 0 || (pro == 1 && p.C2 == 0 && glds_pro)) && glds && dbg == 0) {  // the LDS-DMA form
+    using K = void (*)(ConvParams);
+    if ((!has1 && !has2) || (has1 && p.C2 == 0)) {  // PRO 0 (h2 sources) or 1 (one fp32 source): LDS-DMA form
+        const int pro = has1 ? 1 : 0;
         static bool attr_g[2] = {};
         const K kg = pro ? &k_conv3lg<W, 1> : &k_conv3lg<W, 0>;
         if (!attr_g[pro]) {
@@ -805,7 +727,18 @@ int launch3l(const ConvParams& p, hipStream_t st) {
         hipLaunchKernelGGL(kg, dim3(grid), dim3(64 * L_NW), conv3lg_lds_bytes<W>(), st, p);
         return check_launch("tcx_conv2d_h2(halo 3lg)");
     }
-    hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * L_NW), shm, st, p);
+    // two sources, one of them with a GroupNorm prologue: the register-staged k_conv3l
+    static bool attr = false;
+    const K kc = &k_conv3l<W, 2>;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)conv3l_lds_bytes(W, 384)) != hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3l_lds_bytes(W, 384));
+            return TCX_EHIP;
+        }
+        attr = true;
+    }
+    hipLaunchKernelGGL(kc, dim3(grid), dim3(64 * L_NW), conv3l_lds_bytes(W, p.Cin), st, p);
     return check_launch("tcx_conv2d_h2(halo 3l)");
 }
 
@@ -827,14 +760,7 @@ bool conv3l_takes(const ConvParams& p) {
     if (p.W == 32 || p.W == 64) return true;
     // 16-px rows: the LDS-DMA kernel for h2 sources (mid.net.0: 2 % faster than k_conv3g); its
     // GroupNorm prologue form is 9 % slower than k_conv3g's there (profiles/r02_zt_*), so that stays
-    // (TCX_CONV3L16=0: k_conv3g for both, =2: k_conv3lg for both)
-    static const int on16 = [] {
-        const char* e = getenv("TCX_CONV3L16");
-        return e ? atoi(e) : 1;
-    }();
-    const bool has2 = p.C2 > 0 && p.sc2 != nullptr;
-    if (p.W != 16 || on16 == 0 || has2) return false;
-    return p.sc1 == nullptr ? true : (on16 == 2 && p.C2 == 0);
+    return p.W == 16 && p.sc1 == nullptr && !(p.C2 > 0 && p.sc2 != nullptr);
 }
 
 // 16-px rows (the mid block, one 256-pixel tile per 16x16 image): only the LDS-DMA form exists
@@ -856,19 +782,8 @@ int launch3lg16(const ConvParams& p, hipStream_t st) {
 }
 
 int launch_conv3l(const ConvParams& p, hipStream_t st) {
-    if (p.W == 16) return p.sc1 ? launch3lg16<1>(p, st) : launch3lg16<0>(p, st);
+    if (p.W == 16) return launch3lg16<0>(p, st);
     return p.W == 64 ? launch3l<64>(p, st) : launch3l<32>(p, st);
 }
 
 }  // namespace tcx
-
-// diagnostics: the timestamps of the last TCX_CONV3L_DBG launch, [n][5] (entry, prologue done, last
-// tap done, exit, (XCC << 32) | HW_ID)
-extern "C" int tcx_conv3l_stamps(unsigned long long* out, int n_workgroups) {
-    TCX_REQUIRE(out && n_workgroups >= 0, "tcx_conv3l_stamps: bad args");
-    const int n = n_workgroups < tcx::L_NSTAMP ? n_workgroups : tcx::L_NSTAMP;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tcx::l_stamps), (size_t)n * 5 * sizeof(unsigned long long), 0,
-                            hipMemcpyDeviceToHost) != hipSuccess)
-        return tcx::check_launch("tcx_conv3l_stamps");
-    return TCX_OK;
-}

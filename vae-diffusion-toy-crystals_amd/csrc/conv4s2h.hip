@@ -233,8 +233,7 @@ int launch_ds(const ConvParams& p, hipStream_t st) {
 
 // Host dispatch (conv.hip): true when the stride-2 halo kernel covers this conv.
 bool conv4s2h_applies(const ConvParams& p, int cout_pad) {
-    static const bool off = getenv("TCX_NO_DSHALO") != nullptr;
-    return !off && p.ks == 4 && p.stride == 2 && p.pad_y == 1 && p.pad_x == 1 && p.Hi == p.H && p.Wi == p.W &&
+    return p.ks == 4 && p.stride == 2 && p.pad_y == 1 && p.pad_x == 1 && p.Hi == p.H && p.Wi == p.W &&
            (p.Wo == 16 || p.Wo == 32 || p.Wo == 64) && p.H == 2 * p.Ho && p.W == 2 * p.Wo &&
            p.HoWo % 128 == 0 && cout_pad % 96 == 0 && p.Cin % 16 == 0 && p.C2 == 0 && p.x2 == nullptr &&
            p.kpad == 16 * p.Cin && p.osy == 1 && p.osx == 1;

@@ -615,17 +615,8 @@ int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const fl
     TCX_REQUIRE(x && y && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_upsample2x_h2: bad args");
     TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x_h2: scale/shift pair");
     if ((size_t)Bt * H * W * C == 0) return TCX_OK;
-    static const bool g8 = [] {
-        const char* e = getenv("TCX_UPS8");  // 0: the quad form (A/B)
-        return !(e && e[0] == '0');
-    }();
-    if (g8) {
-        const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 8), UPG * 256));
-        hipLaunchKernelGGL(k_upsample2x_g8, grid, dim3(256), 0, st, x, (char*)y, H, W, C, scale, shift, ovf, bf);
-        return check_launch("tcx_upsample2x_h2");
-    }
-    const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 4), UPK * 256));
-    hipLaunchKernelGGL(k_upsample2x<true>, grid, dim3(256), 0, st, x, (float*)y, Bt, H, W, C, scale, shift, ovf, bf);
+    const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 8), UPG * 256));
+    hipLaunchKernelGGL(k_upsample2x_g8, grid, dim3(256), 0, st, x, (char*)y, H, W, C, scale, shift, ovf, bf);
     return check_launch("tcx_upsample2x_h2");
 }
 

@@ -33,18 +33,6 @@ __device__ __attribute__((aligned(16))) float sk_zero4[4] = {0.f, 0.f, 0.f, 0.f}
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// diagnostic timestamps (TCX_SK_VAR bit 64): per workgroup, waves 0 and 7, s_memrealtime (100 MHz)
-// at entry / after the first k block's MFMAs / after the last MFMA / after the barrier / at exit
-constexpr int SK_NSTAMP = 4096;
-__device__ unsigned long long sk_stamps[SK_NSTAMP][2][5];
-
-__device__ __forceinline__ void sk_stamp(bool on, int wv, int slot) {
-    if (on && (wv == 0 || wv == SK_WAVES - 1) && (threadIdx.x & 63) == 0) {
-        const int g = blockIdx.y * gridDim.x + blockIdx.x;
-        if (g < SK_NSTAMP) sk_stamps[g][wv ? 1 : 0][slot] = __builtin_amdgcn_s_memrealtime();
-    }
-}
-
 struct SkArgs {
     const float* x;
     int ldx, K;
@@ -52,7 +40,6 @@ struct SkArgs {
     int kpad, M, N;
     float* part;   // S > 1: partial planes
     int direct;    // S == 1: apply e here
-    int var;       // TCX_SK_VAR: bit 1 rotate the K slices (default on), bit 64 timestamps (diagnostics)
     SkEpi e;
 };
 
@@ -64,14 +51,12 @@ __global__ __launch_bounds__(512) void k_skinny(SkArgs a) {
     constexpr int KC = 16 * NB;  // k values per wave
     __shared__ float red[SK_WAVES][16 * MT][17];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const bool dbg = a.var & 64;
-    sk_stamp(dbg, wv, 0);
     const int r = lane & 15, q = lane >> 4;
     const int n0 = blockIdx.x * 16;
     const int sidx = blockIdx.y;
     // wave -> K slice rotated by the column tile: the 8 waves of the 32 CUs of an XCD then read
     // different activation lines at any moment instead of all hammering the same L2 channel
-    const int slice = a.var & 1 ? (wv + blockIdx.x) & (SK_WAVES - 1) : wv;
+    const int slice = (wv + blockIdx.x) & (SK_WAVES - 1);
     const int kw0 = sidx * SK_WAVES * KC + slice * KC;
     const int kend = min(a.K, kw0 + KC);
     const int K = a.K;
@@ -111,11 +96,6 @@ __global__ __launch_bounds__(512) void k_skinny(SkArgs a) {
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xf[u][t].z, wf[u].z, acc[t], 0, 0, 0);
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xf[u][t].w, wf[u].w, acc[t], 0, 0, 0);
             }
-            if (u == 0 && dbg) {
-                __builtin_amdgcn_sched_barrier(0);
-                sk_stamp(dbg, wv, 1);
-                __builtin_amdgcn_sched_barrier(0);
-            }
         }
     }
     // D: col = n0 + (lane & 15), row = 16 t + 4 (lane >> 4) + reg
@@ -123,9 +103,7 @@ __global__ __launch_bounds__(512) void k_skinny(SkArgs a) {
     for (int t = 0; t < MT; ++t)
 #pragma unroll
         for (int e = 0; e < 4; ++e) red[wv][16 * t + 4 * q + e][r] = acc[t][e];
-    sk_stamp(dbg, wv, 2);
     __syncthreads();
-    sk_stamp(dbg, wv, 3);
     const int M = a.M, N = a.N;
     for (int o = tid; o < M * 16; o += 64 * SK_WAVES) {
         const int m = o >> 4, c = o & 15, n = n0 + c;
@@ -144,7 +122,6 @@ __global__ __launch_bounds__(512) void k_skinny(SkArgs a) {
         if (a.e.z) a.e.z[i] = ddim_z(a.e.z[i], v, a.e.abar_t, a.e.abar_prev, a.e.last);
         else a.e.y[i] = v;
     }
-    sk_stamp(dbg, wv, 4);
 }
 
 // ---- f16x3 skinny linear: x, W in h2 storage; one wave = 16 columns x a K slice of 32 NC values
@@ -350,8 +327,6 @@ int launch_src(const float* x, int ldx, int K, int nb, int s, const float* w, in
     SkArgs a{};
     a.x = x; a.ldx = ldx; a.K = K; a.w = w; a.kpad = kpad; a.M = M; a.N = N; a.part = part;
     a.direct = direct != nullptr;
-    static const int var = getenv("TCX_SK_VAR") ? atoi(getenv("TCX_SK_VAR")) : 1;
-    a.var = var;
     if (direct) a.e = *direct;
     hipLaunchKernelGGL(sk_kernel(cdiv(M, 16), nb), dim3(cdiv(N, 16), s), dim3(64 * SK_WAVES), 0, st, a);
     return check_launch("skinny linear");
@@ -623,15 +598,6 @@ int skinny_reduce_ln(const float* part, int S, int M, int N, const SkEpi& e, con
 }
 
 }  // namespace tcx
-
-extern "C" int tcx_skinny_stamps(unsigned long long* out, int n_workgroups) {
-    TCX_REQUIRE(out && n_workgroups >= 0, "tcx_skinny_stamps: bad args");
-    const int n = std::min(n_workgroups, tcx::SK_NSTAMP);
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tcx::sk_stamps), (size_t)n * 10 * sizeof(unsigned long long), 0,
-                            hipMemcpyDeviceToHost) != hipSuccess)
-        return tcx::check_launch("tcx_skinny_stamps");
-    return n;
-}
 
 extern "C" size_t tcx_linear_h2_bytes(int n, int k) {
     if (n <= 0 || k <= 0) return 0;

@@ -655,15 +655,6 @@ int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2
     return TCX_OK;
 }
 
-// TCX_PIX8=0 keeps the LDS-tile head kernel (A/B measurements)
-bool first8_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("TCX_PIX8");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 // TCX_ATTN_SPLIT=0 keeps the split evaluator's attention on fp32 MFMA (A/B measurements)
 bool attn_split_enabled() {
     static const bool on = [] {
@@ -860,7 +851,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     {
         TCX_TRY(gn_tab(net, P, 10, P.P0, C, gn, ns, st));
         TCX_REQUIRE(C % 4 == 0, "head: C %% 4");
-        if (P.P0 % HP8 == 0 && (C == 96 || C == 64 || C == 128 || C == 32) && first8_enabled()) {
+        if (P.P0 % HP8 == 0 && (C == 96 || C == 64 || C == 128 || C == 32)) {
             const dim3 g8(Bt * P.P0 / HP8);
             if (C == 96) hipLaunchKernelGGL(k_head8<3>, g8, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
             else if (C == 64) hipLaunchKernelGGL(k_head8<2>, g8, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
@@ -907,8 +898,8 @@ int launch_step(const StepArgs& a, hipStream_t st) {
 // producer -> consumer hand-offs inside the 256 MB Infinity Cache; measured at B = 128
 // (profiles/r01_w_chunk_ab.txt) it LOSES: 59.9 img/s unchunked vs 56.6 / 49.3 / 37.2 at
 // Bc = 64 / 32 / 16 (the smaller conv grids lose more than the memory-bound passes gain), so the
-// default is one pass.  TCX_BATCH_CHUNK=<images> selects chunking (e.g. to bound the workspace).
-// Independently of that knob, a pass is capped so that its largest activation (2*Bc*H*W*C fp32)
+// default is one pass (the chunking knob was removed in round 3).
+// A pass is capped so that its largest activation (2*Bc*H*W*C fp32)
 // stays below 2 GiB: the conv kernels address their operands with 32-bit buffer offsets (the
 // 256x256 configuration at base_ch 96: at most 84 images, i.e. 2*42 with CFG, per pass).
 int max_pass_rows(const tcx_unet* net, int H, int W) {
@@ -918,13 +909,7 @@ int max_pass_rows(const tcx_unet* net, int H, int W) {
 }
 
 int chunk_images(int B, int cap_images) {
-    static const int env = [] {
-        const char* e = getenv("TCX_BATCH_CHUNK");
-        return e ? atoi(e) : -1;
-    }();
-    int c = env < 0 ? 0 : env;
-    c = (c <= 0 || c >= B) ? B : c;
-    return std::max(1, std::min(c, cap_images));
+    return std::max(1, std::min(B, cap_images));
 }
 
 // Concurrent sampling lanes (TCX_LANES = L > 1, default 1): the batch is split into L contiguous

@@ -129,8 +129,6 @@ _SIGS = {
     "tcx_linear_ws": (c_int, [c_fp, c_int, c_fp, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp,
                               c_size, c_fp]),
     "tcx_layernorm_film": (c_int, [c_fp, c_fp, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_float, c_fp]),
-    "tcx_skinny_stamps": (c_int, [c_fp, c_int]),
-    "tcx_conv3l_stamps": (c_int, [c_fp, c_int]),
     "tcx_prior_workspace": (c_size, [ctypes.POINTER(TcxPrior), c_int, c_int]),
     "tcx_prior_forward": (c_int, [ctypes.POINTER(TcxPrior), c_fp, c_fp, c_fp, c_fp, c_int, c_fp, c_fp, c_fp, c_size,
                                   c_fp]),
@@ -213,6 +211,21 @@ def set_conv_precision(name: str) -> None:
 
 def conv_precision() -> str:
     return _conv_precision
+
+
+# the precision the score U-Net evaluator actually ran its last call in ("bf16" falls back to f16x3
+# where the split attention does not apply, any split run to fp32 after a range overflow); bench.py
+# reports this, not the requested one
+_used_precision = None
+
+
+def note_used_precision(name: str) -> None:
+    global _used_precision
+    _used_precision = name
+
+
+def used_conv_precision():
+    return _used_precision
 
 
 class TcxError(RuntimeError):

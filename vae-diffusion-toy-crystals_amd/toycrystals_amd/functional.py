@@ -239,7 +239,10 @@ class Conv2dFn(torch.autograd.Function):
         x1, x2, w, b, resid = _c(x1), _c(x2), _c(w), _c(b), _c(resid)
         Cout, Cin, ks, _ = w.shape
         wpk, kpad, cpad = _pack_conv(w)
-        keep = []
+        # the split forward's h2 records of x are kept for the weight gradient (one activation-sized
+        # buffer per split conv until backward; INTEGRATION.md "Training memory note") unless the
+        # weight gradients run on fp32 MFMA (TCX_WGRAD_FP32=1), which does not read them
+        keep = [] if _WGRAD_SPLIT else None
         y = _conv_fwd(x1, x2, wpk, kpad, cpad, b, None, resid, Cout, ks, stride, pad, circular, keep=keep)
         ctx.save_for_backward(x1, x2, w)
         ctx.xrec = keep[0] if keep else None  # the split path's h2 records of x for the weight gradient

@@ -123,6 +123,7 @@ class _UNetPack:
         net.heads = model.attn.num_heads
         # the f16x3 split convs need every conv source channel count % 32 (base_ch % 32 == 0)
         self.split_ok = model.base_ch % 32 == 0
+        self._warned_bf16 = False
         self.ovf = torch.zeros(4, device=device, dtype=torch.int32)
         net.h2_ovf = self.ovf.data_ptr()
         net.precision = 0
@@ -232,6 +233,11 @@ class _UNetPack:
         prec = _lib.conv_precision()
         split = prec in ("f16x3", "bf16") and self.split_ok and ((H // 4) * (W // 4)) % 32 == 0
         bf = split and prec == "bf16" and ((H // 4) * (W // 4)) % 256 == 0
+        if prec == "bf16" and not bf and not self._warned_bf16:
+            self._warned_bf16 = True
+            warnings.warn(f"libtcx: bf16 precision needs (H/4)*(W/4) % 256 == 0 (the split attention); "
+                          f"{H}x{W} runs in {'f16x3' if split else 'fp32'}")
+        _lib.note_used_precision("bf16" if bf else ("f16x3" if split else "fp32"))
         if bf:
             saved = {}
             for name, (wh, ws, whf) in self._bf16_packs().items():
@@ -253,6 +259,7 @@ class _UNetPack:
         launch()
         if split and int(self.ovf[0].item()) != 0:
             warnings.warn("libtcx: an activation left the f16 range of the split path; recomputed in fp32")
+            _lib.note_used_precision("fp32")
             self.net.precision = 0
             launch()
         self.net.precision = 0
