@@ -301,6 +301,29 @@ def test_weight_scale_extremes():
         assert float(np.abs(got - ref).max()) <= 2e-6 * float(np.abs(ref).max())
 
 
+@pytest.mark.parametrize("B,Ci,Co,H,resid,out_h2", [
+    (2, 192, 192, 16, True, False),   # proj: residual, fp32 out (k_lin1x1)
+    (2, 192, 576, 16, False, True),   # qkv: h2 out (k_lin1x1)
+    (4, 96, 288, 8, False, False),    # 3 chunks (odd count), 3 column blocks
+    (1, 32, 96, 16, False, True),     # one chunk
+    (3, 64, 96, 8, True, False),      # M = 192, not whole 128-row tiles: im2col kernel
+])
+def test_conv1x1_h2_vs_oracle(B, Ci, Co, H, resid, out_h2):
+    """1x1 split convs (csrc/lin1x1.hip where M % 128 == 0 and Cout pads to 96k) against the fp64
+    oracle at the fp32 conv's gate, with bias, residual and h2 output as the attention block uses them."""
+    x = rng.standard_normal((B, Ci, H, H))
+    w = rng.standard_normal((Co, Ci, 1, 1)) / np.sqrt(Ci)
+    b = rng.standard_normal(Co)
+    r = rng.standard_normal((B, Co, H, H)) if resid else None
+    ref = nn_np.conv2d(x, w, b, stride=1, padding=0, mode="zeros")
+    if resid:
+        ref = ref + r
+    got = run_conv_h2(x, w, b, 1, 0, False, resid=r, out_h2=out_h2)
+    err = float(np.abs(got - ref).max()) / max(1.0, float(np.abs(ref).max()))
+    print(f"1x1 h2 err {err:.2e}")
+    assert err <= (2e-5 if not out_h2 else 2e-5 + 2.0 ** -21)
+
+
 @pytest.mark.parametrize("inplace", [True, False])
 def test_gn_apply_h2(inplace):
     B, HW, C = 2, 256, 96
@@ -323,14 +346,39 @@ def test_gn_apply_h2(inplace):
     assert int(ovf.item()) == 0
 
 
-def test_upsample_h2():
-    B, H, W, C = 2, 8, 8, 96
+@pytest.mark.parametrize("B,H,W,C", [(2, 8, 8, 96), (2, 16, 16, 192), (2, 32, 32, 96), (1, 12, 20, 32), (1, 6, 64, 64)])
+def test_upsample_h2(B, H, W, C):
+    """h2 upsample (the banded LDS kernel where H % 4 == 0 and W C <= 3072 — us1 / us2 of the 64^2
+    U-Net —, else k_upsample2x_g8) against the fp32 upsample: the h2 decode bound."""
     x = dev(rng.standard_normal((B, H, W, C)))
     y = torch.empty((B, 2 * H, 2 * W, C), device="cuda")
     y32 = torch.empty_like(y)
     chk(L().tcx_upsample2x_h2(x.data_ptr(), y.data_ptr(), B, H, W, C, None, None, None, st()))
     chk(L().tcx_upsample2x(x.data_ptr(), y32.data_ptr(), B, H, W, C, None, None, st()))
     dec_ok(from_h2(y).cpu().numpy(), y32.cpu().numpy())
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 32, 32, 96), (2, 16, 16, 192), (1, 6, 64, 64)])
+def test_upsample_h2_fused_gn_silu(B, H, W, C):
+    """The evaluator's us1 input: GroupNorm+SiLU tables applied by the upsample while it stages its
+    source (no apply pass).  Bit-identical to the in-place fp32 apply pass followed by the plain h2
+    upsample (same fmaf order), and within the h2 decode bound of apply + fp32 upsample."""
+    x = rng.standard_normal((B, H, W, C)).astype(np.float32) * 2.0
+    sc = dev(rng.uniform(0.5, 1.5, (B, C)))
+    sh = dev(rng.standard_normal((B, C)))
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    y = torch.empty((B, 2 * H, 2 * W, C), device="cuda")
+    chk(L().tcx_upsample2x_h2(dev(x).data_ptr(), y.data_ptr(), B, H, W, C, sc.data_ptr(), sh.data_ptr(),
+                              ovf.data_ptr(), st()))
+    a = dev(x)
+    chk(L().tcx_gn_apply_tab(a.data_ptr(), a.data_ptr(), B, H * W, C, sc.data_ptr(), sh.data_ptr(), 1, st()))
+    y2 = torch.empty_like(y)
+    chk(L().tcx_upsample2x_h2(a.data_ptr(), y2.data_ptr(), B, H, W, C, None, None, None, st()))
+    assert torch.equal(y, y2)
+    y32 = torch.empty_like(y)
+    chk(L().tcx_upsample2x(a.data_ptr(), y32.data_ptr(), B, H, W, C, None, None, st()))
+    dec_ok(from_h2(y).cpu().numpy(), y32.cpu().numpy())
+    assert int(ovf.item()) == 0
 
 
 @pytest.mark.parametrize("Bt,N,C,heads", [(2, 256, 192, 4), (1, 4096, 192, 4), (2, 1024, 64, 4)])

@@ -1,0 +1,6 @@
+// k_conv3g instantiated for rows of 32 pixels (conv3g.hpp; split per width for parallel builds)
+#include "conv3g.hpp"
+
+namespace tcx {
+int launch3g_w32(const ConvParams& p, hipStream_t st) { return launch3g<32>(p, st); }
+}  // namespace tcx

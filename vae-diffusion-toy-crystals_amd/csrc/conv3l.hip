@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 namespace tcx {
 namespace {
@@ -383,6 +384,21 @@ __device__ __forceinline__ f32x8 sload8(const float* ptr) {
 constexpr int WAIT_VM0 = 0x0F70;    // s_waitcnt vmcnt(0)
 constexpr int WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
 
+// GroupNorm-prologue transform schedules (k_conv3lg PRO 1), two task slots per MFMA gap: 0-7 value k, 8-11 channel pair k - 8, 12 the
+// write-back, -1 none.  S1: one unit over both row blocks' 18 gaps; S2: one unit in one row block's 9
+// gaps (the odd chunk's tap 6 carries two units)
+constexpr int kTvS1[36] = {0, -1, 1, -1, 8, -1, 2, -1, 3, -1, 9, -1, -1, -1, -1, -1, -1, -1,
+                           4, -1, 5, -1, 10, -1, 6, -1, 7, -1, 11, 12, -1, -1, -1, -1, -1, -1};
+constexpr int kTvS2[18] = {0, -1, 1, 8, 2, -1, 3, 9, 4, -1, 5, 10, 6, -1, 7, 11, 12, -1};
+template <int SCH, int G, int SLOT>
+struct TvCode {
+    static constexpr int value = SCH == 1 ? kTvS1[2 * G + SLOT] : kTvS2[2 * G + SLOT];
+};
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+
 template <int W, int PRO>
 __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     constexpr int RT = 2, NT = L_NT, NTHR = 64 * L_NW;
@@ -400,6 +416,12 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     auto sw = [](int col) { return W == 16 ? (col >> 1) & 3 : (col >> 2) & 3; };
     extern __shared__ __attribute__((aligned(16))) float sm[];
     char* const smc = reinterpret_cast<char*>(sm);
+    // LDS-DMA destinations from a base the optimiser cannot fold to a constant: a compile-time LDS
+    // address reaches instruction selection as a constant local->flat->local cast whose null check
+    // hipcc cannot encode ("Operand has incorrect register class")
+    int lz;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(lz));
+    char* const smd = smc + lz;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
@@ -453,14 +475,14 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         for (int q = 0; q < NIH; ++q) {
             if (q < q0 || q >= q1) continue;
             const int i = 2 * q + hw;
-            if (i < NI) lds_dma16(rs, smc + buf * HB + i * 1024, halo_voff(i), cc);
+            if (i < NI) lds_dma16(rs, smd + buf * HB + i * 1024, halo_voff(i), cc);
         }
     };
     // weight waves: pair k (12 KB) -> ring slot k & 1; wave w moves KB [6 w, 6 w + 6)
     auto pair_issue = [&](int k) {
         k = k < npair ? k : npair - 1;
         const int base = (nblk * nch + 2 * k) * NT * 2048 + wv * 6144;
-        char* const d = smc + RING + (k & 1) * L_PAIR + wv * 6144;
+        char* const d = smd + RING + (k & 1) * L_PAIR + wv * 6144;
 #pragma unroll
         for (int i = 0; i < 6; ++i) lds_dma16(rw, d + i * 1024, lane * 16, base + i * 1024);
     };
@@ -536,39 +558,62 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
             tsh[k] = c[k];
         }
     };
-    // MFMAs of row block rt with the transform of unit i (buffer buf) one value per gap
-    auto mf_transform = [&](int rt, int s, int i, int buf, bool live) {
-        char* const d = smc + buf * HB + tdst[i];
-        const float4 x0 = *reinterpret_cast<const float4*>(d);
+    // A unit's 8 values spread over the 18 MFMA gaps of a tap (rb 0: gaps 0-8, rb 1: 9-17).
+    // Per gap at most one value (fma, exp2, add, rcp, mul: 5 VALU, two of them 8-cycle transcendentals)
+    // or one channel pair's h2 split (cvt_pk, 2 cvt back, 2 sub, cvt_pk); the write-back of the two
+    // 16-B pieces after the last split.  Out-of-range values are caught by a running max of |v|
+    // (v_max3: half an instruction per value) checked once per unit (a NaN source stays NaN in either
+    // precision, so only finite overflow matters).
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    struct TUnit {
+        float x[8], v[8];
+        unsigned hi[4], lo[4];
+        float m;
+    };
+    auto tu_load = [&](TUnit& u, int i, int buf) {
+        const float4 x0 = *reinterpret_cast<const float4*>(smc + buf * HB + tdst[i]);
         const float4 x1 = *reinterpret_cast<const float4*>(smc + buf * HB + (tdst[i] ^ 16));
-        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        unsigned sp[8];
-        bool bad = false;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const int g = k / 3, n = k - 3 * (k / 3);
+        u.x[0] = x0.x; u.x[1] = x0.y; u.x[2] = x0.z; u.x[3] = x0.w;
+        u.x[4] = x1.x; u.x[5] = x1.y; u.x[6] = x1.z; u.x[7] = x1.w;
+        u.m = 0.f;
+    };
+    auto tu_val = [&](TUnit& u, int k) { u.v[k] = l_silu(u.x[k], tsc[k], tsh[k]); };
+    auto tu_pair = [&](TUnit& u, int q) {
+        const f32x2 v = {u.v[2 * q], u.v[2 * q + 1]};
+        const f16x2 h = __builtin_convertvector(v, f16x2);
+        const f32x2 r = v - __builtin_convertvector(h, f32x2);
+        const f16x2 l = __builtin_convertvector(r, f16x2);
+        u.hi[q] = __builtin_bit_cast(unsigned, h);
+        u.lo[q] = __builtin_bit_cast(unsigned, l);
+        u.m = fmaxf(u.m, fmaxf(fabsf(v[0]), fabsf(v[1])));
+    };
+    auto tu_store = [&](TUnit& u, int i, int buf, bool live) {
+        *reinterpret_cast<uint4*>(smc + buf * HB + tdst[i]) = make_uint4(u.hi[0], u.hi[1], u.hi[2], u.hi[3]);
+        *reinterpret_cast<uint4*>(smc + buf * HB + (tdst[i] ^ 16)) = make_uint4(u.lo[0], u.lo[1], u.lo[2], u.lo[3]);
+        h2_flag(p.ovf, !(u.m < kH2Max) && live && ((tval >> i) & 1));
+    };
+    // one task (compile-time code C) of a gap
+    auto tu_task = [&](TUnit& u, auto C, int i, int buf, bool live) {
+        constexpr int code = decltype(C)::value;
+        if constexpr (code >= 0 && code < 8) tu_val(u, code);
+        else if constexpr (code >= 8 && code < 12) tu_pair(u, code - 8);
+        else if constexpr (code == 12) tu_store(u, i, buf, live);
+    };
+    // the 9 MFMAs of row block rt with the tasks of gaps [G0, G0 + 9) of schedule SCH on unit u
+    auto mf_tasks = [&](int rt, int s, TUnit& u, auto SCH, auto G0, int i, int buf, bool live) {
+        constexpr int sch = decltype(SCH)::value, g0 = decltype(G0)::value;
+        static_for([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            constexpr int g = k / 3, n = k - 3 * (k / 3);
             const h8& aa = g == 1 ? a_l[rt] : a_h[rt];
             const h8& bb = g == 0 ? b_l[s][n] : b_h[s][n];
             acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa, bb, acc[rt][n], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            if (k < 8) {
-                const float v = l_silu(xs[k], tsc[k], tsh[k]);
-                bad = bad || h2_bad(v);
-                sp[k] = split1(v);
-            }
+            tu_task(u, std::integral_constant<int, TvCode<sch, g0 + k, 0>::value>{}, i, buf, live);
+            tu_task(u, std::integral_constant<int, TvCode<sch, g0 + k, 1>::value>{}, i, buf, live);
             __builtin_amdgcn_sched_barrier(0);
-        }
-        unsigned h[4], l[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            h[k] = (sp[2 * k] & 0xffffu) | (sp[2 * k + 1] << 16);
-            l[k] = (sp[2 * k] >> 16) | (sp[2 * k + 1] & 0xffff0000u);
-        }
-        *reinterpret_cast<float4*>(d) =
-            make_float4(__uint_as_float(h[0]), __uint_as_float(h[1]), __uint_as_float(h[2]), __uint_as_float(h[3]));
-        *reinterpret_cast<float4*>(smc + buf * HB + (tdst[i] ^ 16)) =
-            make_float4(__uint_as_float(l[0]), __uint_as_float(l[1]), __uint_as_float(l[2]), __uint_as_float(l[3]));
-        h2_flag(p.ovf, bad && live && ((tval >> i) & 1));  // after the last chunk: no raw data
+        }, std::make_integer_sequence<int, 9>{});
     };
     // the whole chunk's transform at once (prologue)
     auto transform_all = [&](int buf) {
@@ -628,9 +673,13 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         // odd: units 0 and 1 in tap 6, then 7, 8); the h2 is published by a barrier at the end of tap
         // 8 (an extra one in an odd chunk), so A0 of the next chunk's tap 0 is read after it
         constexpr int TR = hb ? 6 : 5;  // first transform tap
-        constexpr bool tr = PRO == 1 && t >= TR && (hb ? (t == 6 ? 0 : t - 5) : t - 5) < TU;
-        constexpr int u0 = hb ? (t == 6 ? 0 : t - 5) : t - 5;  // unit in the row-block-0 gaps
-        constexpr bool tr1 = PRO == 1 && hb && t == 6;         // unit 1 in the row-block-1 gaps
+        constexpr bool tr = PRO == 1 && t >= TR && (hb ? (t == 6 ? 0 : t - 5) : t - 5) < TU;  // unit u0
+        constexpr int u0 = hb ? (t == 6 ? 0 : t - 5) : t - 5;
+        constexpr bool tr1 = PRO == 1 && hb && t == 6;  // and unit u1 = 1 (odd chunk's tap 6)
+        constexpr int u1 = 1;
+        constexpr bool pre_a0 = PRO == 0;  // tap 8 prefetches A0 of the next chunk
+        // (measured r03_l: moving the transform to taps 5-6 / 6-7 so that tap 8 prefetches A0 and the
+        // odd chunk's extra barrier goes, two units per tap, was 0-2 % slower per layer)
         const bool more = j + 1 < cpt;
         // LDS-DMA issue first thing in the tap (right after the barrier that freed the target): a
         // pair issued at the start of odd tap 2k-3 has two taps of latency cover before its wait
@@ -644,20 +693,31 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
             if (more) halo_issue(j + 1, hb ^ 1, q0, q1);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (PRO == 1 && t == 0) rd_a(0, 0, hb);  // published at the end of the last tap
+        if constexpr (!pre_a0 && t == 0) rd_a(0, 0, hb);  // published at the end of the last tap
         rd_b(s ^ 1, c + 1);
         if (t != 8) rd_a(1, t, hb);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (tr) mf_transform(0, s, u0, hb ^ 1, more);
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I9 = std::integral_constant<int, 9>;
+        TUnit ua, ub;
+        if constexpr (tr) {
+            tu_load(ua, u0, hb ^ 1);
+            if constexpr (tr1) tu_load(ub, u1, hb ^ 1);
+        }
+        if constexpr (tr1) mf_tasks(0, s, ua, I2{}, I0{}, u0, hb ^ 1, more);
+        else if constexpr (tr) mf_tasks(0, s, ua, I1{}, I0{}, u0, hb ^ 1, more);
         else mf(0, s);
         __builtin_amdgcn_sched_barrier(0);
         if (t == 8) {
-            if constexpr (PRO == 0) rd_a(0, 0, hb ^ 1);
+            if constexpr (pre_a0) rd_a(0, 0, hb ^ 1);
         } else {
             rd_a(0, t + 1, hb);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (tr1) mf_transform(1, s, 1, hb ^ 1, more);
+        if constexpr (tr1) mf_tasks(1, s, ub, I2{}, I0{}, u1, hb ^ 1, more);
+        else if constexpr (tr) mf_tasks(1, s, ua, I1{}, I9{}, u0, hb ^ 1, more);
         else mf(1, s);
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
@@ -716,13 +776,14 @@ int launch3l(const ConvParams& p, hipStream_t st) {
         const int pro = has1 ? 1 : 0;
         static bool attr_g[2] = {};
         const K kg = pro ? &k_conv3lg<W, 1> : &k_conv3lg<W, 0>;
-        if (!attr_g[pro]) {
+        const int ai = pro;
+        if (!attr_g[ai]) {
             if (hipFuncSetAttribute(reinterpret_cast<const void*>(kg), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)conv3lg_lds_bytes<W>()) != hipSuccess) {
                 set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3lg_lds_bytes<W>());
                 return TCX_EHIP;
             }
-            attr_g[pro] = true;
+            attr_g[ai] = true;
         }
         hipLaunchKernelGGL(kg, dim3(grid), dim3(64 * L_NW), conv3lg_lds_bytes<W>(), st, p);
         return check_launch("tcx_conv2d_h2(halo 3lg)");

@@ -85,9 +85,14 @@ __device__ __forceinline__ void store4_h2(char* base, size_t pix, int q, const f
     *reinterpret_cast<uint2*>(g + 16) = lo;
 }
 
-// Raise the overflow flag (rare: a plain per-lane atomic on the taken branch only).
+// Raise the overflow flag (rare: a plain per-lane atomic on the taken branch only).  The pointer is
+// cast to the global address space so the atomic is one global_atomic_or: on a generic pointer the
+// compiler expands it into a run-time LDS / scratch / global address-space switch (whose LDS-aperture
+// compare it could not encode inside the k_conv3lg tap loop).
 __device__ __forceinline__ void h2_flag(unsigned* ovf, bool bad) {
-    if (bad && ovf) atomicOr(ovf, 1u);
+    if (bad && ovf)
+        __hip_atomic_fetch_or((__attribute__((address_space(1))) unsigned*)ovf, 1u, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Decode 4 channels [4q, 4q+4) of one pixel record (tests / conversions).

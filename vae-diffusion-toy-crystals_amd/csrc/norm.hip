@@ -314,6 +314,102 @@ __global__ __launch_bounds__(256) void k_upsample2x_g8(const float* __restrict__
     h2_flag(ovf, bad && !bf);
 }
 
+// Banded bilinear x2 upsample -> h2 (us1 / us2 of sde_score_model.py:217-222, 256, 261): one workgroup
+// per (image, band of UB_ROWS output rows).  The band's UB_SRC source rows (its UB_ROWS / 2 rows and one
+// clamped halo row either side) are read from HBM once, put through the optional GroupNorm+SiLU of
+// the source ONCE per element (the fused form of k_upsample2x_g8 recomputed it for each of the 4 taps
+// of every output, 16x per element) and held in LDS as fp32; every output quad then reads its 4
+// taps from LDS.  Same fmaf order as k_upsample2x_g8 (bit-identical outputs), and with the tables it
+// equals the in-place apply pass followed by the plain upsample bit for bit, minus that pass.
+constexpr int UB_MAXWC = 3072;             // W * C of one source row (72 KB of LDS for an 8-row band)
+// ROWS output rows per band (ROWS / 2 + 2 source rows staged); G8: one 8-channel group per item (two
+// 16-B stores) instead of one 4-channel quad (two 8-B stores)
+template <int ROWS, bool G8>
+__global__ __launch_bounds__(256, 2) void k_upsample2x_band(const float* __restrict__ x, char* __restrict__ y, int H,
+                                                           int W, int C, const float* __restrict__ tsc,
+                                                           const float* __restrict__ tsh, unsigned* ovf, int bf) {
+    constexpr int SRC = ROWS / 2 + 2;
+    extern __shared__ __attribute__((aligned(16))) float ub[];  // [SRC][W][C]
+    const int nband = 2 * H / ROWS;
+    const int b = blockIdx.x / nband, band = blockIdx.x - (blockIdx.x / nband) * nband;
+    const int ys0 = band * (ROWS / 2) - 1;  // source row of LDS row 0 (before clamping)
+    const int WC = W * C, WC4 = WC / 4, C4 = C / 4;
+    // phase 1: SRC source rows (clamped), GroupNorm+SiLU once per element, into LDS
+    constexpr int NL = (SRC * UB_MAXWC / 4 + 255) / 256;
+    f4v v[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < SRC * WC4) {
+            const int r = i / WC4, e = i - (i / WC4) * WC4;
+            const int ysrc = min(max(ys0 + r, 0), H - 1);
+            v[k] = *reinterpret_cast<const f4v*>(x + ((size_t)b * H + ysrc) * WC + 4 * e);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < SRC * WC4) {
+            if (tsc) {
+                const int c4 = (i - (i / C4) * C4) * 4;
+                const f4v s4 = *reinterpret_cast<const f4v*>(tsc + (size_t)b * C + c4);
+                const f4v h4 = *reinterpret_cast<const f4v*>(tsh + (size_t)b * C + c4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[k][e] = silu_f(fmaf(v[k][e], s4[e], h4[e]));
+            }
+            *reinterpret_cast<f4v*>(ub + 4 * i) = v[k];
+        }
+    }
+    __syncthreads();
+    // phase 2: output items (oy, ox, quad or group), channel index fastest
+    bool bad = false;
+    constexpr int CW = G8 ? 8 : 4;  // channels per item
+    const int CI = C / CW;
+    const int nq = ROWS * 2 * W * CI;
+    for (int i = threadIdx.x; i < nq; i += 256) {
+        const int q = i % CI, rest = i / CI;
+        const int ox = rest % (2 * W), ry = rest / (2 * W);
+        const int oy = band * ROWS + ry;
+        float sy = 0.5f * ((float)oy + 0.5f) - 0.5f;
+        sy = sy < 0.f ? 0.f : sy;
+        const int y0 = (int)sy;
+        const int y1 = y0 + (y0 < H - 1 ? 1 : 0);
+        const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
+        float sx = 0.5f * ((float)ox + 0.5f) - 0.5f;
+        sx = sx < 0.f ? 0.f : sx;
+        const int x0 = (int)sx, x1 = x0 + (x0 < W - 1 ? 1 : 0);
+        const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
+        const float* r0 = ub + (y0 - ys0) * WC + CW * q;
+        const float* r1 = ub + (y1 - ys0) * WC + CW * q;
+        const size_t pix = ((size_t)b * 2 * H + oy) * 2 * W + ox;
+        uint2 hi[2], lo[2];
+#pragma unroll
+        for (int h = 0; h < CW / 4; ++h) {
+            const f4v va = *reinterpret_cast<const f4v*>(r0 + x0 * C + 4 * h);
+            const f4v vb = *reinterpret_cast<const f4v*>(r0 + x1 * C + 4 * h);
+            const f4v vc = *reinterpret_cast<const f4v*>(r1 + x0 * C + 4 * h);
+            const f4v vd = *reinterpret_cast<const f4v*>(r1 + x1 * C + 4 * h);
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o[e] = fmaf(ly1, fmaf(lx1, vd[e], lx0 * vc[e]), ly0 * fmaf(lx1, vb[e], lx0 * va[e]));
+                bad = bad || h2_bad(o[e]);
+            }
+            split4x(make_float4(o[0], o[1], o[2], o[3]), hi[h], lo[h], bf != 0);
+        }
+        if constexpr (G8) {
+            char* gp = y + pix * C * 4 + 32 * (size_t)q;
+            *reinterpret_cast<uint4*>(gp) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
+            *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo[0].x, lo[0].y, lo[1].x, lo[1].y);
+        } else {
+            char* gp = y + pix * C * 4 + 32 * (size_t)(q >> 1) + 8 * (q & 1);
+            *reinterpret_cast<uint2*>(gp) = hi[0];
+            *reinterpret_cast<uint2*>(gp + 16) = lo[0];
+        }
+    }
+    h2_flag(ovf, bad && !bf);
+}
+
 // LayerNorm over rows of width Wd (+ optional FiLM h*(1+gamma)+beta), one wave per row.
 // gamma = gb[row][i] (+ gt[i]), beta = gb[row][Wd + i] (+ gt[Wd + i]): gt is one row broadcast over
 // all rows (the prior DDIM's per-step time half of the FiLM projection, prior.hip).
@@ -609,12 +705,41 @@ extern "C" int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, in
 }
 
 namespace tcx {
+// the banded upsample covers this source shape (its band of source rows fits the LDS)
+// TCX_UPB (temporary A/B): 0 = k_upsample2x_g8 only, 1 = 8-row quads, 2 = 8-row groups, 3 = 4-row groups
+static int upb() {
+    static const int v = [] {
+        const char* e = getenv("TCX_UPB");
+        return e ? atoi(e) : 2;
+    }();
+    return v;
+}
+bool upsample_band_ok(int H, int W, int C) { return upb() != 0 && H % 4 == 0 && W * C <= UB_MAXWC && C % 8 == 0; }
+
 // h2 (f16x3) or bf16 (bf != 0) records out of the upsample / GroupNorm apply (unet.hip, and the C ABI below)
 int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
                   unsigned* ovf, int bf, hipStream_t st) {
     TCX_REQUIRE(x && y && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_upsample2x_h2: bad args");
     TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x_h2: scale/shift pair");
     if ((size_t)Bt * H * W * C == 0) return TCX_OK;
+    if (upsample_band_ok(H, W, C)) {  // the banded LDS form (the 64^2 U-Net's us1 / us2)
+        const int v = upb();
+        const int rows = v == 3 ? 4 : 8;
+        const size_t shm = (size_t)(rows / 2 + 2) * W * C * sizeof(float);
+        using K = void (*)(const float*, char*, int, int, int, const float*, const float*, unsigned*, int);
+        const K k = v == 1 ? &k_upsample2x_band<8, false> : (v == 2 ? &k_upsample2x_band<8, true> : &k_upsample2x_band<4, true>);
+        static bool attr[4] = {};
+        if (!attr[v]) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(6 * UB_MAXWC * sizeof(float))) != hipSuccess) {
+                set_error("tcx_upsample2x_h2: cannot enable %zu B of dynamic LDS", 6 * UB_MAXWC * sizeof(float));
+                return TCX_EHIP;
+            }
+            attr[v] = true;
+        }
+        hipLaunchKernelGGL(k, dim3(Bt * (2 * H / rows)), dim3(256), shm, st, x, (char*)y, H, W, C, scale, shift, ovf, bf);
+        return check_launch("tcx_upsample2x_h2(band)");
+    }
     const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 8), UPG * 256));
     hipLaunchKernelGGL(k_upsample2x_g8, grid, dim3(256), 0, st, x, (char*)y, H, W, C, scale, shift, ovf, bf);
     return check_launch("tcx_upsample2x_h2");

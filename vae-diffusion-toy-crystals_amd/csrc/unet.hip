@@ -17,6 +17,7 @@
 namespace tcx {
 bool conv3g_covers(int H, int W, int Cin, int cout_pad);  // conv3g.hip
 // h2 / bf16 record writers (norm.hip, attention_split.hip): bf != 0 writes bf16 halves
+bool upsample_band_ok(int H, int W, int C);
 int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
                   unsigned* ovf, int bf, hipStream_t st);
 int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
@@ -834,11 +835,17 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     TCX_TRY(norm(7, P.b32, P.P1, C));
     TCX_TRY(conv_gn(net->up2_1, P.b32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, gn, &ns, st,
                     SC(7), SH(7), nullptr, nullptr, h2));
-    // us1: GN+SiLU of up2's output in place (1x per element; the upsample-side transform
-    // recomputed it for 4 taps per output and measured 3x slower), upsample into the free b64, conv
-    TCX_TRY(norm(8, P.a32, P.P1, C, false));
-    if (h2.on) TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, h2.ovf, h2.bf, st));
-    else TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, st));
+    // us1: GN+SiLU of up2's output, bilinear x2 into the free b64, conv.  Split path: the banded
+    // upsample applies the GroupNorm+SiLU once per source element while staging (no apply pass);
+    // fp32 path: the apply pass in place, then the plain upsample
+    if (h2.on && upsample_band_ok(H1, W1, C)) {
+        TCX_TRY(gn_tab(net, P, 8, P.P1, C, gn, ns, st));
+        TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, P.sc(8), P.sh(8), h2.ovf, h2.bf, st));
+    } else {
+        TCX_TRY(norm(8, P.a32, P.P1, C, false));
+        if (h2.on) TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, h2.ovf, h2.bf, st));
+        else TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, st));
+    }
     TCX_TRY(conv_gn(net->us1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, nullptr, &ns, st,
                     nullptr, nullptr, nullptr, nullptr, h2, 1));
     // up1 on cat[a64, silu(gn(h1))]
