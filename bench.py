@@ -239,13 +239,13 @@ def main() -> int:
 
     if args.precision == "f16x3":
         kname = ("split-path convs: k_conv3lg (3x3 at 16/32/64-px rows, LDS-DMA halo + weight ring, GN+SiLU "
-                 "prologue), k_conv3g (16-px GN+SiLU prologue), k_conv4s2h (4x4/s2 halo), k_conv<SPL> (1x1) — "
+                 "prologue), k_conv3g (16-px GN+SiLU prologue), k_conv4s2g (4x4/s2, LDS-DMA), k_lin1x1 (1x1) — "
                  "f16x3, 3 f16 MFMAs per fp32 MAC; all conv launches of the pass")
         peak = F16_PEAK_TFLOPS / SPLIT_PRODUCTS
         peak_basis = "2500 TFLOP/s dense f16 MFMA / 3 products per fp32 MAC; achieved in fp32-equivalent FLOPs"
     elif args.precision == "bf16":
-        kname = ("bf16 single-product convs (config 5): k_conv3g, k_conv4s2h, k_conv<SPL=2> — one "
-                 "v_mfma_f32_32x32x16_bf16 per MAC; all conv launches of the pass")
+        kname = ("bf16 single-product convs (config 5): k_conv3g (slim halo at 256-px rows), k_conv4s2g, "
+                 "k_lin1x1, k_conv<SPL=2> — one v_mfma_f32_32x32x16_bf16 per MAC; all conv launches of the pass")
         peak = F16_PEAK_TFLOPS
         peak_basis = "2500 TFLOP/s dense bf16 MFMA"
     else:

@@ -149,6 +149,12 @@ int tcx_conv2d_h2(const void* x1, const void* x2, int Bt, int bmod, int H, int W
  * Same byte size as wh (tcx_conv_weight_h2_frag_bytes). */
 size_t tcx_conv_weight_h2_frag_bytes(int cout_pad, int Cin);
 int tcx_pack_conv_weight_h2_frag(const void* wh, void* wf, int cout_pad, int kpad, int Cin, void* stream);
+/* The same for a 4x4 stride-2 h2 weight ([cout_pad][16 Cin], cout_pad % 96 == 0, Cin % 8 == 0), read by
+ * the LDS-DMA downsample kernel k_conv4s2g (ds1 / ds2, sde_score_model.py:208,210) in 16-deep k-steps
+ * of two taps x 8 channels: wf[cout_pad/96][2 Cin][3][hi, lo][64][16 B] (k-step 8 j + 2 dy + p holds
+ * taps (dy, 2p + lane/32) of channels 8j..8j+7).  Same byte size as wh. */
+size_t tcx_conv_weight_h2_frag4_bytes(int cout_pad, int Cin);
+int tcx_pack_conv_weight_h2_frag4(const void* wh, void* wf, int cout_pad, int kpad, int Cin, void* stream);
 
 /* ------------------------------------------------------------------ bf16 single-product path
  * Config 5 (256x256, "bf16 MFMA conv-as-GEMM", BASELINE.json configs[4]): the same record layout as

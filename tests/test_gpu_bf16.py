@@ -67,11 +67,16 @@ def pack_bf16(w):
 
 
 def pack_frag(wh, cpad, kpad, cin):
-    nb = int(L().tcx_conv_weight_h2_frag_bytes(cpad, cin))
-    if not nb or kpad != 9 * cin:
+    if kpad == 9 * cin:
+        nb, fn = int(L().tcx_conv_weight_h2_frag_bytes(cpad, cin)), L().tcx_pack_conv_weight_h2_frag
+    elif kpad == 16 * cin:
+        nb, fn = int(L().tcx_conv_weight_h2_frag4_bytes(cpad, cin)), L().tcx_pack_conv_weight_h2_frag4
+    else:
+        return None
+    if not nb:
         return None
     wf = torch.empty(nb // 4, device="cuda")
-    chk(L().tcx_pack_conv_weight_h2_frag(wh.data_ptr(), wf.data_ptr(), cpad, kpad, cin, st()))
+    chk(fn(wh.data_ptr(), wf.data_ptr(), cpad, kpad, cin, st()))
     return wf
 
 
@@ -85,7 +90,7 @@ def run_conv_bf16(x, w, b, stride, pad, x2=None, frag=True, tabs=None):
     y = torch.empty((B, Ho, Wo, co), device="cuda")
     xd = dev(nhwc(x)) if tabs is not None else to_bf16_records(dev(nhwc(x)))
     x2d = to_bf16_records(dev(nhwc(x2))) if x2 is not None else None
-    wf = pack_frag(wh, cpad, kpad, C1 + C2) if (frag and ks == 3) else None
+    wf = pack_frag(wh, cpad, kpad, C1 + C2) if (frag and ks in (3, 4)) else None
     p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     sc, sh = (dev(tabs[0]), dev(tabs[1])) if tabs is not None else (None, None)
     chk(L().tcx_conv2d_h2_pro(xd.data_ptr(), p(x2d), B, 0, H, W, C1, C2, wh.data_ptr(), p(wf), ws.data_ptr(),
@@ -103,9 +108,13 @@ def conv_ref(x, w, b, stride, pad):
     (2, 96, 0, 64, 96, 3, 1, True),      # k_conv3g, 64-px rows
     (2, 96, 96, 32, 96, 3, 1, True),     # k_conv3g, two sources, 32-px rows
     (1, 96, 0, 128, 96, 3, 1, True),     # k_conv3g, 128-px rows
+    (1, 96, 0, 256, 96, 3, 1, True),     # k_conv3g slim halo (hi pieces only), 256-px rows
+    (1, 96, 96, 256, 96, 3, 1, True),    # slim, two sources (up1_0 at 256^2)
     (2, 64, 0, 16, 96, 3, 1, True),      # k_conv3g, 16-px rows (mid block)
     (2, 64, 0, 16, 64, 3, 1, False),     # no fragment copy: the im2col kernel (no bf16 k_conv3p)
     (2, 96, 0, 64, 96, 4, 2, False),     # k_conv4s2h (ds1 at 64 -> 32)
+    (2, 96, 0, 64, 96, 4, 2, True),      # k_conv4s2g (LDS-DMA, fragment-ordered 4x4 weights)
+    (1, 96, 0, 128, 96, 4, 2, True),     # k_conv4s2g at Wo = 64 (config 5's ds2)
     (2, 192, 0, 16, 576, 1, 1, False),   # 1x1 (qkv): the im2col kernel
 ])
 def test_bf16_convs_vs_float64_on_rounded_operands(B, C1, C2, H, co, ks, stride, frag):
@@ -122,9 +131,11 @@ def test_bf16_convs_vs_float64_on_rounded_operands(B, C1, C2, H, co, ks, stride,
     assert err < 5e-6
 
 
-def test_bf16_conv3g_gn_prologue_vs_float64():
-    """the prologue applies silu(x*scale+shift) in fp32 and rounds the result to bf16 in registers"""
-    B, C, H = 2, 96, 64
+@pytest.mark.parametrize("B,H", [(2, 64), (1, 256)])
+def test_bf16_conv3g_gn_prologue_vs_float64(B, H):
+    """the prologue applies silu(x*scale+shift) in fp32 and rounds the result to bf16 in registers
+    (64-px rows: two halo units per thread; 256-px rows: the slim halo, 7 units per thread)"""
+    C = 96
     x = rng.standard_normal((B, C, H, H)).astype(np.float32)
     sc = (0.5 + rng.random((B, C))).astype(np.float32)
     sh = rng.standard_normal((B, C)).astype(np.float32) * 0.2

@@ -59,12 +59,18 @@ def pack_h2(w):
 
 
 def pack_frag(wh, cpad, kpad, cin):
-    """Fragment-ordered copy for k_conv3g (None where it does not apply: the call then runs k_conv3p)."""
-    nb = int(L().tcx_conv_weight_h2_frag_bytes(cpad, cin))
-    if not nb or kpad != 9 * cin:
+    """Fragment-ordered copy for k_conv3g / k_conv3l* (3x3) or k_conv4s2g (4x4/s2); None where it does
+    not apply (the call then runs k_conv3p / k_conv4s2h / the im2col kernel)."""
+    if kpad == 9 * cin:
+        nb, fn = int(L().tcx_conv_weight_h2_frag_bytes(cpad, cin)), L().tcx_pack_conv_weight_h2_frag
+    elif kpad == 16 * cin:
+        nb, fn = int(L().tcx_conv_weight_h2_frag4_bytes(cpad, cin)), L().tcx_pack_conv_weight_h2_frag4
+    else:
+        return None
+    if not nb:
         return None
     wf = torch.empty(nb // 4, device="cuda")
-    chk(L().tcx_pack_conv_weight_h2_frag(wh.data_ptr(), wf.data_ptr(), cpad, kpad, cin, st()))
+    chk(fn(wh.data_ptr(), wf.data_ptr(), cpad, kpad, cin, st()))
     return wf
 
 
@@ -85,7 +91,7 @@ def run_conv_h2(x, w, b, stride, pad, circular, x2=None, act=0, resid=None, bmod
     rd = dev(nhwc(resid)) if resid is not None else None
     gnd = torch.zeros((Bt, -(-Ho * Wo // 128), co, 2), dtype=torch.float64, device="cuda") if gn else None
     ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
-    wf = pack_frag(wh, cpad, kpad, C1 + C2) if (frag and ks == 3) else None
+    wf = pack_frag(wh, cpad, kpad, C1 + C2) if (frag and ks in (3, 4)) else None
     chk(L().tcx_conv2d_h2_pro(xd.data_ptr(), x2d.data_ptr() if x2d is not None else None, Bt, bmod, H, W, C1, C2,
                               wh.data_ptr(), wf.data_ptr() if wf is not None else None, ws.data_ptr(),
                               bd.data_ptr() if bd is not None else None, None,
@@ -361,8 +367,10 @@ def test_upsample_h2(B, H, W, C):
 @pytest.mark.parametrize("B,H,W,C", [(2, 32, 32, 96), (2, 16, 16, 192), (1, 6, 64, 64)])
 def test_upsample_h2_fused_gn_silu(B, H, W, C):
     """The evaluator's us1 input: GroupNorm+SiLU tables applied by the upsample while it stages its
-    source (no apply pass).  Bit-identical to the in-place fp32 apply pass followed by the plain h2
-    upsample (same fmaf order), and within the h2 decode bound of apply + fp32 upsample."""
+    source (no apply pass), against the in-place fp32 apply pass (IEEE-division SiLU) followed by the
+    fp32 upsample: the h2 decode bound plus 8 fp32 ulps for the hardware exp2 / rcp SiLU, and 2^-21 of
+    the output scale (an output interpolated between SiLU values of opposite sign carries their
+    absolute, not its own relative, rounding)."""
     x = rng.standard_normal((B, H, W, C)).astype(np.float32) * 2.0
     sc = dev(rng.uniform(0.5, 1.5, (B, C)))
     sh = dev(rng.standard_normal((B, C)))
@@ -372,12 +380,11 @@ def test_upsample_h2_fused_gn_silu(B, H, W, C):
                               ovf.data_ptr(), st()))
     a = dev(x)
     chk(L().tcx_gn_apply_tab(a.data_ptr(), a.data_ptr(), B, H * W, C, sc.data_ptr(), sh.data_ptr(), 1, st()))
-    y2 = torch.empty_like(y)
-    chk(L().tcx_upsample2x_h2(a.data_ptr(), y2.data_ptr(), B, H, W, C, None, None, None, st()))
-    assert torch.equal(y, y2)
     y32 = torch.empty_like(y)
     chk(L().tcx_upsample2x(a.data_ptr(), y32.data_ptr(), B, H, W, C, None, None, st()))
-    dec_ok(from_h2(y).cpu().numpy(), y32.cpu().numpy())
+    got, ref = from_h2(y).cpu().numpy(), y32.cpu().numpy()
+    bound = np.abs(ref) * (2.0 ** -21 + 8 * 2.0 ** -23) + 2.0 ** -25 + 2.0 ** -21 * float(np.abs(ref).max())
+    assert np.all(np.abs(got - ref) <= bound), float(np.max(np.abs(got - ref) - bound))
     assert int(ovf.item()) == 0
 
 

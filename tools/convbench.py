@@ -63,9 +63,12 @@ def bench(name, H, C1, C2, Co, ks, s, pad, ups, reps=20, gn=os.environ.get("GN",
         check(L.tcx_pack_conv_weight_h2(wpk.data_ptr(), wh.data_ptr(), ws.data_ptr(), cpad, kpad, st))
 
         nfb = int(L.tcx_conv_weight_h2_frag_bytes(cpad, Cin)) if (ks == 3 and os.environ.get("TCX_CONV3G", "1") != "0") else 0
+        if ks == 4 and os.environ.get("FRAG4", "1") == "1":
+            nfb = int(L.tcx_conv_weight_h2_frag4_bytes(cpad, Cin))
         wf = torch.empty(max(nfb // 4, 4), device="cuda")
         if nfb:
-            check(L.tcx_pack_conv_weight_h2_frag(wh.data_ptr(), wf.data_ptr(), cpad, kpad, Cin, st))
+            pk = L.tcx_pack_conv_weight_h2_frag4 if ks == 4 else L.tcx_pack_conv_weight_h2_frag
+            check(pk(wh.data_ptr(), wf.data_ptr(), cpad, kpad, Cin, st))
         wfp = wf.data_ptr() if nfb else None
 
         def run():

@@ -35,7 +35,7 @@ def main():
         tot[k] = (n, rf, rw)
         print(f"{k[:60]:60s} {n:6d} {rf:20.2f} {rw:16.2f}")
     # the launches bench.py's roofline times: the implicit-GEMM convs (k_conv<...>, k_conv3g<...>, ...)
-    conv = [v for k, v in tot.items() if re.match(r"tcx::k_conv(3g|3h|3w|3p|3l|3lg|4s2h)?<", k)]
+    conv = [v for k, v in tot.items() if re.match(r"tcx::(k_conv(3g|3p|3l|3lg|4s2h|4s2g)?|k_lin1x1)<", k)]
     n = sum(v[0] for v in conv)
     if n:
         avg = sum(v[0] * (v[1] + v[2]) for v in conv) / n

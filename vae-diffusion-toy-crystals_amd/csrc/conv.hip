@@ -646,6 +646,7 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
                 "(tcx_pack_conv_weight_h2_frag) and a 3x3 stride-1 conv with W in {16, 32, 64, 128}, Cin %% 32 == 0, "
                 "Cin <= 384, Cout padded to 96k");
     if (!p.bf && conv3h_applies(p, cout_pad)) return launch_conv3h(p, cout_pad, (hipStream_t)stream);
+    if (conv4s2g_applies(p, cout_pad)) return launch_conv4s2g(p, cout_pad, (hipStream_t)stream);
     if (conv4s2h_applies(p, cout_pad)) return launch_conv4s2h(p, cout_pad, (hipStream_t)stream);
     if (lin1x1_applies(p, cout_pad)) return launch_lin1x1(p, cout_pad, (hipStream_t)stream);
     return launch_conv(p, cout_pad, 0, (hipStream_t)stream);

@@ -7,6 +7,7 @@ int launch3g_w16(const ConvParams& p, hipStream_t st);
 int launch3g_w32(const ConvParams& p, hipStream_t st);
 int launch3g_w64(const ConvParams& p, hipStream_t st);
 int launch3g_w128(const ConvParams& p, hipStream_t st);
+int launch3g_w256(const ConvParams& p, hipStream_t st);
 namespace {
 
 // Fragment-ordered copy of h2 conv weights for k_conv3g: wf[nblk][c = 9 j + t][n][hi, lo][lane][16 B]
@@ -43,14 +44,14 @@ bool conv3g_enabled() {
     return on;
 }
 
-bool conv3g_covers(int H, int W, int Cin, int cout_pad) {
-    if (!conv3g_enabled() || !(W == 16 || W == 32 || W == 64 || W == 128)) return false;
+bool conv3g_covers(int H, int W, int Cin, int cout_pad, bool bf) {
+    if (!conv3g_enabled() || !(W == 16 || W == 32 || W == 64 || W == 128 || (W == 256 && bf))) return false;
     const int tp = g_tp(g_nw(W));
     return H % (tp / W) == 0 && (H * W) % tp == 0 && Cin % 32 == 0 && Cin <= 384 && cout_pad % 96 == 0;
 }
 
 bool conv3g_applies(const ConvParams& p, int cout_pad) {
-    return p.wf != nullptr && conv3g_covers(p.H, p.W, p.Cin, cout_pad) && p.ks == 3 && p.stride == 1 && p.pad_y == 1 && p.pad_x == 1 &&
+    return p.wf != nullptr && conv3g_covers(p.H, p.W, p.Cin, cout_pad, p.bf) && p.ks == 3 && p.stride == 1 && p.pad_y == 1 && p.pad_x == 1 &&
            p.Hi == p.H && p.Wi == p.W && p.C1 % G_KC == 0 && (p.C2 == 0 || p.C2 == p.C1) && p.kpad == 9 * p.Cin &&
            p.osy == 1 && p.osx == 1;
 }
@@ -68,7 +69,8 @@ int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st) {
     else if (p.W == 64) rc = launch3g_w64(p, st);
     else if (p.W == 32) rc = launch3g_w32(p, st);
     else if (p.W == 16) rc = launch3g_w16(p, st);
-    else rc = launch3g_w128(p, st);
+    else if (p.W == 128) rc = launch3g_w128(p, st);
+    else rc = launch3g_w256(p, st);
     prof_end(st, 2.0 * (double)p.M * p.Cout * 9 * p.Cin);
     return rc;
 }

@@ -57,11 +57,18 @@ constexpr int G_NT = 3;     // 32-channel accumulator tiles per wave (96 output 
 __host__ __device__ constexpr int g_tp(int NW) { return 64 * NW; }
 __host__ __device__ constexpr int g_npx(int W, int NW) { return (g_tp(NW) / W + 2) * (W + 2); }
 __host__ __device__ constexpr int g_units(int W, int NW) { return (2 * g_npx(W, NW) + 64 * NW - 1) / (64 * NW); }
-// NW = 4 (two workgroups per CU) for rows of 32/64 pixels, NW = 8 (one per CU) for 128
-__host__ __device__ constexpr int g_nw(int W) { return W >= 128 ? 8 : 4; }
+// NW = 4 (two workgroups per CU) for rows of 16/32/64 pixels and the bf16 256-px rows, NW = 8 (one
+// per CU) for 128
+__host__ __device__ constexpr int g_nw(int W) { return W == 128 ? 8 : 4; }
+// "slim" halo (bf16 at 256-px rows, config 5): a bf16 product reads only the hi halves of the records,
+// so a halo slot holds the two 16-B hi pieces of the pixel's 16-channel chunk + 16 B pad (48 B: the
+// ds_read_b128 of 32 consecutive slots then lands on 3 p mod 16, distinct over every 16-lane group),
+// and the halo of a 256-px row (3 x 258 slots) fits twice in 74 KB: two workgroups per CU
+__host__ __device__ constexpr bool g_slim(int W, bool BF) { return BF && W == 256; }
+__host__ __device__ constexpr int g_pxf(int W, bool BF) { return g_slim(W, BF) ? 12 : G_PXF; }
 
-constexpr size_t conv3g_lds_bytes(int W, int NW, int Cin) {
-    return ((size_t)2 * g_npx(W, NW) * G_PXF + 2 * (size_t)Cin) * sizeof(float);
+constexpr size_t conv3g_lds_bytes(int W, int NW, int Cin, bool BF = false) {
+    return ((size_t)2 * g_npx(W, NW) * g_pxf(W, BF) + 2 * (size_t)Cin) * sizeof(float);
 }
 
 __device__ __forceinline__ float silu_split_src(float v, float sc, float sh) {
@@ -96,8 +103,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
     constexpr int NPX = g_npx(W, NW);
     constexpr int NU = 2 * NPX;        // 8-channel halo units per chunk
     constexpr int UPT = g_units(W, NW);
-    constexpr int HBUF = NPX * G_PXF;
-    static_assert(UPT <= 4, "halo units per thread: stores must finish by tap 5");
+    constexpr bool SLIM = g_slim(W, BF);
+    constexpr int PXF = g_pxf(W, BF);
+    constexpr int HBUF = NPX * PXF;
+    // units are loaded UPL per tap at taps 0 .. NLT-1 and stored two taps later (by tap 5)
+    constexpr int UPL = (UPT + 3) / 4;
+    constexpr int NLT = (UPT + UPL - 1) / UPL;
+    static_assert(NLT <= 4, "halo units per thread: stores must finish by tap 5");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* const Hs = sm;                   // [2][NPX][PXF]
     float* const Ts = sm + 2 * HBUF;        // [2][Cin]: scale, shift of this tile's image
@@ -169,15 +181,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
         return s1 ? gn1 : gn2;
     };
     auto unit_load = [&](int j, int i) {
+        if (i >= UPT) return;
         __amdgpu_buffer_rsrc_t rs;
         int cc;
-        src_of(j, rs, cc);
+        const bool gn = src_of(j, rs, cc);
         hv[i][0] = bld4(rs, hoff[i], cc);
-        hv[i][1] = bld4(rs, hoff[i], cc + 16);
+        // slim: an h2/bf16 record unit is its 16-B hi piece; an fp32 prologue source is 32 B
+        if (!SLIM || PRO == 1 || (PRO == 2 && gn)) hv[i][1] = bld4(rs, hoff[i], cc + 16);
     };
     // fp32 source with a GroupNorm table: silu(x*sc+sh) -> h2 in registers (zero padding stays 0)
     auto unit_transform = [&](int j, int i) {
         if constexpr (PRO == 0) return;
+        if (i >= UPT) return;
         __amdgpu_buffer_rsrc_t rs;
         int cc;
         const bool gn = src_of(j, rs, cc);
@@ -201,11 +216,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
         if (!BF) h2_flag(p.ovf, bad);
     };
     auto unit_write = [&](int i, int buf) {
+        if (i >= UPT) return;
         const int u = tid + NTHR * i;
         if (!((i + 1) * NTHR <= NU || u < NU)) return;
-        float* d = &Hs[buf * HBUF + (u < NPX ? u * G_PXF : (u - NPX) * G_PXF + 8)];
-        *reinterpret_cast<float4*>(d) = hv[i][0];
-        *reinterpret_cast<float4*>(d + 4) = hv[i][1];
+        if constexpr (SLIM) {  // hi piece of group g at 16 g
+            float* d = &Hs[buf * HBUF + (u < NPX ? u * PXF : (u - NPX) * PXF + 4)];
+            *reinterpret_cast<float4*>(d) = hv[i][0];
+        } else {
+            float* d = &Hs[buf * HBUF + (u < NPX ? u * PXF : (u - NPX) * PXF + 8)];
+            *reinterpret_cast<float4*>(d) = hv[i][0];
+            *reinterpret_cast<float4*>(d + 4) = hv[i][1];
+        }
     };
 
     // ---- fragments.  B: fragment-ordered weights [nblk][chunk c][n][hi, lo][lane][16 B]
@@ -213,7 +234,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
         const int mloc = (wv * RT + rt) * 32 + li;
-        abase[rt] = ((mloc / W) * W2 + (mloc % W)) * G_PXF + lh * 8;
+        abase[rt] = ((mloc / W) * W2 + (mloc % W)) * PXF + lh * (SLIM ? 4 : 8);
     }
     f32x16 acc[RT][NT];
 #pragma unroll
@@ -223,9 +244,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
     h8 a_h[RT], a_l[RT], b_h[2][NT], b_l[2][NT];
     auto rd_a = [&](int rt, int t, int hb) {
         const int dy = t / 3, dx = t - 3 * (t / 3);
-        const float* A = &Hs[hb * HBUF + abase[rt] + (dy * W2 + dx) * G_PXF];
+        const float* A = &Hs[hb * HBUF + abase[rt] + (dy * W2 + dx) * PXF];
         a_h[rt] = __builtin_bit_cast(h8, ld4(A));
-        a_l[rt] = __builtin_bit_cast(h8, ld4(A + 4));
+        if constexpr (!BF) a_l[rt] = __builtin_bit_cast(h8, ld4(A + 4));
     };
     const int bl = lane * 16;
     auto ld_b = [&](int s, int c) {
@@ -332,8 +353,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
             else rd_a(0, t + 1, hb);
         }
         __builtin_amdgcn_sched_barrier(0);
-        constexpr bool st = t >= 2 && t < UPT + 2;  // this tap stores halo unit t - 2 of chunk j+1
-        if constexpr (st && PRO == 1) {
+        constexpr bool st = t >= 2 && t < NLT + 2;  // this tap stores halo units UPL (t - 2) .. of chunk j+1
+        if constexpr (st && PRO == 1 && UPL == 1) {
             // GN+SiLU of the unit's 8 values interleaved one per MFMA gap with the row-block-1
             // MFMAs (~10 VALU per gap, under the ~5 issue slots x 2 waves an MFMA gap hides:
             // MI355X_MICROARCH.md issue costs), the h2 split after the last one
@@ -343,12 +364,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
         }
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
-        if constexpr (t < UPT) unit_load(more ? j + 1 : j, t);  // (not stored after the last chunk)
+        if constexpr (t < NLT) {  // (not stored after the last chunk)
+#pragma unroll
+            for (int q = 0; q < UPL; ++q) unit_load(more ? j + 1 : j, UPL * t + q);
+        }
         if constexpr (st) {
             // unconditional (after the last chunk the other buffer is dead): a branch here lets hipcc
             // sink the interleaved split of mf1_transform out of the MFMA gaps into it
-            if constexpr (PRO == 2) unit_transform(more ? j + 1 : j, t - 2);
-            unit_write(t - 2, hb ^ 1);
+#pragma unroll
+            for (int q = 0; q < UPL; ++q) {
+                if constexpr (PRO == 2 || (PRO == 1 && UPL > 1)) unit_transform(more ? j + 1 : j, UPL * (t - 2) + q);
+                unit_write(UPL * (t - 2) + q, hb ^ 1);
+            }
         }
         if (t == 1 || t == 6) __syncthreads();
     };
@@ -383,23 +410,34 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
 template <int W>
 int launch3g(const ConvParams& p, hipStream_t st) {
     constexpr int NW = g_nw(W);
-    const size_t shm = conv3g_lds_bytes(W, NW, p.Cin);
+    constexpr bool ONLY_BF = W == 256;  // the 256-px rows exist only in the slim bf16 form
+    if (ONLY_BF && !p.bf) {
+        set_error("tcx_conv2d_h2: 256-px rows on k_conv3g need bf16");
+        return TCX_EINVAL;
+    }
+    const size_t shm = conv3g_lds_bytes(W, NW, p.Cin, p.bf);
     static bool attr[12] = {};
     const bool has1 = p.sc1 != nullptr, has2 = p.C2 > 0 && p.sc2 != nullptr;
     const int pro = !has1 && !has2 ? 0 : ((has1 && (p.C2 == 0 || has2)) ? 1 : 2);
     using K = void (*)(ConvParams);
-    const K ks[12] = {&k_conv3g<W, NW, false, 0, false>, &k_conv3g<W, NW, false, 1, false>,
-                      &k_conv3g<W, NW, false, 2, false>, &k_conv3g<W, NW, true, 0, false>,
-                      &k_conv3g<W, NW, true, 1, false>,  &k_conv3g<W, NW, true, 2, false>,
-                      &k_conv3g<W, NW, false, 0, true>,  &k_conv3g<W, NW, false, 1, true>,
-                      &k_conv3g<W, NW, false, 2, true>,  &k_conv3g<W, NW, true, 0, true>,
-                      &k_conv3g<W, NW, true, 1, true>,   &k_conv3g<W, NW, true, 2, true>};
+    K ks[12] = {};
+    if constexpr (!ONLY_BF) {
+        const K k16[6] = {&k_conv3g<W, NW, false, 0, false>, &k_conv3g<W, NW, false, 1, false>,
+                          &k_conv3g<W, NW, false, 2, false>, &k_conv3g<W, NW, true, 0, false>,
+                          &k_conv3g<W, NW, true, 1, false>,  &k_conv3g<W, NW, true, 2, false>};
+        for (int i = 0; i < 6; ++i) ks[i] = k16[i];
+    }
+    const K kb[6] = {&k_conv3g<W, NW, false, 0, true>, &k_conv3g<W, NW, false, 1, true>,
+                     &k_conv3g<W, NW, false, 2, true>, &k_conv3g<W, NW, true, 0, true>,
+                     &k_conv3g<W, NW, true, 1, true>,  &k_conv3g<W, NW, true, 2, true>};
+    for (int i = 0; i < 6; ++i) ks[6 + i] = kb[i];
     const int ki = (p.bf ? 6 : 0) + (p.circular ? 3 : 0) + pro;
     const K kc = ks[ki];
     if (!attr[ki]) {
+        const size_t mx = conv3g_lds_bytes(W, NW, 384, p.bf);
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)conv3g_lds_bytes(W, NW, 384)) != hipSuccess) {
-            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3g_lds_bytes(W, NW, 384));
+                                (int)mx) != hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", mx);
             return TCX_EHIP;
         }
         attr[ki] = true;

@@ -49,11 +49,14 @@ int launch_conv3h(ConvParams& p, int cout_pad, hipStream_t st);
 bool conv3g_applies(const ConvParams& p, int cout_pad);
 // true when a 3x3 stride-1 circular conv of an H x W image with Cin inputs runs on k_conv3g (and so
 // can take the GroupNorm+SiLU prologue of tcx_conv2d_h2_pro)
-bool conv3g_covers(int H, int W, int Cin, int cout_pad);
+bool conv3g_covers(int H, int W, int Cin, int cout_pad, bool bf = false);
 int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st);
 // 1x1 split GEMM (lin1x1.hip): the attention block's qkv / proj convs.
 bool lin1x1_applies(const ConvParams& p, int cout_pad);
 int launch_lin1x1(ConvParams& p, int cout_pad, hipStream_t st);
+// LDS-DMA 4x4 stride-2 kernel (conv4s2g.hip): the U-Net downsamples with fragment-ordered weights.
+bool conv4s2g_applies(const ConvParams& p, int cout_pad);
+int launch_conv4s2g(ConvParams& p, int cout_pad, hipStream_t st);
 // Halo-staged 4x4 stride-2 kernel (conv4s2h.hip): the U-Net downsamples on the split path.
 bool conv4s2h_applies(const ConvParams& p, int cout_pad);
 int launch_conv4s2h(ConvParams& p, int cout_pad, hipStream_t st);

@@ -438,76 +438,71 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
     const int kblk = tile / p.ncblk, cblk = tile - (tile / p.ncblk) * p.ncblk;
     const int k0 = kblk * GBM, c0 = cblk * BN;
     const int tid = threadIdx.x;
-    const int px = tid & 31, q = tid >> 5;
+    // thread = (4 consecutive pixels 4 pxq .. 4 pxq + 3 of the 32-pixel chunk, k quad q of the A tile /
+    // co quad q of the B tile): the 4 pixels' halves of one k row are ONE 8-byte ds_write_b64 (the
+    // 2-byte stores of one pixel per thread bounded the kernel: DESIGN.md §3b); needs Wo % 4 == 0 so
+    // the 4 pixels share an output row
+    const int pxq = tid & 7, q = tid >> 3;
     const int chunk0 = split * p.cps;
     const int nch_all = (p.M + 31) / 32;
     const int chunk1 = min(chunk0 + p.cps, nch_all);
     const char* x1 = reinterpret_cast<const char*>(p.x1);
     const char* x2 = reinterpret_cast<const char*>(p.x2);
     const char* dyb = reinterpret_cast<const char*>(p.dy);
-    // per-thread im2col quads: k = k0 + 4 (q + 8 i) .. +3 share one tap and source (C1, C2 % 8 == 0)
-    int tdy[4], tdx[4], toff[4];
-    bool tsrc1[4], tkv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int k = k0 + 4 * (q + 8 * i);
-        const int kk = k < p.K ? k : 0;
-        const int tap = kk / p.Cin, ci = kk - (kk / p.Cin) * p.Cin;
-        tdy[i] = tap / p.ks;
-        tdx[i] = tap - (tap / p.ks) * p.ks;
-        tsrc1[i] = ci < p.C1;
-        const int c = ci < p.C1 ? ci : ci - p.C1;
-        toff[i] = (c >> 3) * 32 + (c & 4) * 2;  // byte offset of the quad's hi half in the pixel record
-        tkv[i] = k < p.K;
-    }
-    uint2 ah[4], al[4], bh[NT], bl[NT];
+    // this thread's im2col quad: k = k0 + 4 q .. +3 share one tap and source (C1, C2 % 8 == 0)
+    const int kq = k0 + 4 * q;
+    const bool tkv = kq < p.K;
+    const int kk = tkv ? kq : 0;
+    const int tap = kk / p.Cin, ci = kk - (kk / p.Cin) * p.Cin;
+    const int tdy = tap / p.ks, tdx = tap - (tap / p.ks) * p.ks;
+    const bool tsrc1 = ci < p.C1;
+    const int tcc = ci < p.C1 ? ci : ci - p.C1;
+    const int toff = (tcc >> 3) * 32 + (tcc & 4) * 2;  // byte offset of the quad's hi half in the pixel record
+    const int cq = c0 + 4 * q;                       // this thread's co quad of the B tile
+    const bool bq = q < BN / 4;
+    uint2 ah[4], al[4], bh[4], bl[4];
     auto load = [&](int c) {
-        const int m = c * 32 + px;
-        const bool mv = m < p.M;
-        const int mm = mv ? m : 0;
+        const int m0p = c * 32 + 4 * pxq;  // first of the 4 pixels (one output row: Wo % 4 == 0)
+        const bool mv = m0p < p.M;
+        const int mm = mv ? m0p : 0;
         const int b = mm / p.HoWo, r = mm - (mm / p.HoWo) * p.HoWo;
         const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
-        const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
+        int yy = oy * p.stride - p.pad + tdy;
+        bool oky = mv && tkv;
+        if (p.circular) yy = wrap_idx(yy, p.H);
+        else oky = oky && yy >= 0 && yy < p.H;
+        const size_t rowpix = ((size_t)b * p.H + (oky ? yy : 0)) * p.W;
+        const bool okb = mv && bq && cq < p.Cout;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            int yy = iy0 + tdy[i], xx = ix0 + tdx[i];
-            bool ok = mv && tkv[i];
-            if (p.circular) {
-                yy = wrap_idx(yy, p.H);
-                xx = wrap_idx(xx, p.W);
-            } else {
-                ok = ok && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
-            }
-            const size_t pix = ((size_t)b * p.H + (ok ? yy : 0)) * p.W + (ok ? xx : 0);
-            const char* a = tsrc1[i] ? x1 + pix * p.C1 * 4 + toff[i] : x2 + pix * p.C2 * 4 + toff[i];
-            ah[i] = ok ? *reinterpret_cast<const uint2*>(a) : make_uint2(0u, 0u);
-            al[i] = ok ? *reinterpret_cast<const uint2*>(a + 16) : make_uint2(0u, 0u);
-        }
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const int co = c0 + 4 * (q + 8 * j);
-            const bool ok = mv && co < p.Cout;
-            const char* d = dyb + ((size_t)mm * p.Cout + (co >> 3) * 8) * 4 + (co & 4) * 2;
-            bh[j] = ok ? *reinterpret_cast<const uint2*>(d) : make_uint2(0u, 0u);
-            bl[j] = ok ? *reinterpret_cast<const uint2*>(d + 16) : make_uint2(0u, 0u);
+        for (int e = 0; e < 4; ++e) {
+            int xx = (ox + e) * p.stride - p.pad + tdx;
+            bool ok = oky;
+            if (p.circular) xx = wrap_idx(xx, p.W);
+            else ok = ok && xx >= 0 && xx < p.W;
+            const size_t pix = rowpix + (ok ? xx : 0);
+            const char* a = tsrc1 ? x1 + pix * p.C1 * 4 + toff : x2 + pix * p.C2 * 4 + toff;
+            ah[e] = ok ? *reinterpret_cast<const uint2*>(a) : make_uint2(0u, 0u);
+            al[e] = ok ? *reinterpret_cast<const uint2*>(a + 16) : make_uint2(0u, 0u);
+            const char* d = dyb + ((size_t)(mm + e) * p.Cout + (cq >> 3) * 8) * 4 + (cq & 4) * 2;
+            bh[e] = okb ? *reinterpret_cast<const uint2*>(d) : make_uint2(0u, 0u);
+            bl[e] = okb ? *reinterpret_cast<const uint2*>(d + 16) : make_uint2(0u, 0u);
         }
     };
-    auto put4 = [&](_Float16* plane, int row0, const uint2 v) {  // 4 consecutive rows, this pixel
-        plane[(row0 + 0) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.x & 0xffffu));
-        plane[(row0 + 1) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.x >> 16));
-        plane[(row0 + 2) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.y & 0xffffu));
-        plane[(row0 + 3) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.y >> 16));
+    // row r (0..3) of the quad: half r of each pixel's uint2, the 4 pixels packed into one 8-B store
+    auto half = [](const uint2 v, int r) -> unsigned { return ((r < 2 ? v.x : v.y) >> (16 * (r & 1))) & 0xffffu; };
+    auto put = [&](_Float16* plane, const uint2 (&v)[4]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint2 w = make_uint2(half(v[0], r) | (half(v[1], r) << 16), half(v[2], r) | (half(v[3], r) << 16));
+            *reinterpret_cast<uint2*>(&plane[(4 * q + r) * RS + 4 * pxq]) = w;
+        }
     };
     auto store = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            put4(Ah[buf], 4 * (q + 8 * i), ah[i]);
-            put4(Al[buf], 4 * (q + 8 * i), al[i]);
-        }
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            put4(Bh[buf], 4 * (q + 8 * j), bh[j]);
-            put4(Bl[buf], 4 * (q + 8 * j), bl[j]);
+        put(Ah[buf], ah);
+        put(Al[buf], al);
+        if (bq) {
+            put(Bh[buf], bh);
+            put(Bl[buf], bl);
         }
     };
     f32x16 acc[NT];
@@ -831,6 +826,7 @@ extern "C" int tcx_conv_wgrad_h2(const void* x1, const void* x2, int Bt, int H, 
     p.Ho = (H + 2 * pad - ks) / stride + 1;
     p.Wo = (W + 2 * pad - ks) / stride + 1;
     TCX_REQUIRE(p.Ho > 0 && p.Wo > 0, "tcx_conv_wgrad_h2: empty output");
+    TCX_REQUIRE(p.Wo % 4 == 0, "tcx_conv_wgrad_h2: needs Wo %% 4 == 0 (4 pixels of a row per thread)");
     p.HoWo = p.Ho * p.Wo; p.M = Bt * p.HoWo;
     p.ks = ks; p.stride = stride; p.pad = pad; p.circular = circular;
     p.dy = (const float*)dy; p.Cout = Cout; p.K = ks * ks * p.Cin; p.comb = comb;

@@ -315,12 +315,12 @@ __global__ __launch_bounds__(256) void k_upsample2x_g8(const float* __restrict__
 }
 
 // Banded bilinear x2 upsample -> h2 (us1 / us2 of sde_score_model.py:217-222, 256, 261): one workgroup
-// per (image, band of UB_ROWS output rows).  The band's UB_SRC source rows (its UB_ROWS / 2 rows and one
-// clamped halo row either side) are read from HBM once, put through the optional GroupNorm+SiLU of
-// the source ONCE per element (the fused form of k_upsample2x_g8 recomputed it for each of the 4 taps
-// of every output, 16x per element) and held in LDS as fp32; every output quad then reads its 4
-// taps from LDS.  Same fmaf order as k_upsample2x_g8 (bit-identical outputs), and with the tables it
-// equals the in-place apply pass followed by the plain upsample bit for bit, minus that pass.
+// per (image, band of ROWS output rows).  The band's ROWS / 2 + 2 source rows (one clamped halo row
+// either side) are read from HBM once, put through the optional GroupNorm+SiLU of the source ONCE per
+// element (the fused form of k_upsample2x_g8 recomputes it for each of the 4 taps of every output,
+// 16x per element; SiLU here as in the conv prologues, y rcp(1 + exp2(-y log2 e))) and held in LDS as
+// fp32; every output 8-channel group then reads its 4 taps from LDS (same fmaf order as
+// k_upsample2x_g8) and is written as two 16-B pieces.
 constexpr int UB_MAXWC = 3072;             // W * C of one source row (72 KB of LDS for an 8-row band)
 // ROWS output rows per band (ROWS / 2 + 2 source rows staged); G8: one 8-channel group per item (two
 // 16-B stores) instead of one 4-channel quad (two 8-B stores)
@@ -355,7 +355,10 @@ __global__ __launch_bounds__(256, 2) void k_upsample2x_band(const float* __restr
                 const f4v s4 = *reinterpret_cast<const f4v*>(tsc + (size_t)b * C + c4);
                 const f4v h4 = *reinterpret_cast<const f4v*>(tsh + (size_t)b * C + c4);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[k][e] = silu_f(fmaf(v[k][e], s4[e], h4[e]));
+                for (int e = 0; e < 4; ++e) {  // SiLU as y rcp(1 + exp2(-y log2 e)), as the conv prologues
+                    const float yv = fmaf(v[k][e], s4[e], h4[e]);
+                    v[k][e] = yv * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * yv));
+                }
             }
             *reinterpret_cast<f4v*>(ub + 4 * i) = v[k];
         }
@@ -706,15 +709,7 @@ extern "C" int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, in
 
 namespace tcx {
 // the banded upsample covers this source shape (its band of source rows fits the LDS)
-// TCX_UPB (temporary A/B): 0 = k_upsample2x_g8 only, 1 = 8-row quads, 2 = 8-row groups, 3 = 4-row groups
-static int upb() {
-    static const int v = [] {
-        const char* e = getenv("TCX_UPB");
-        return e ? atoi(e) : 2;
-    }();
-    return v;
-}
-bool upsample_band_ok(int H, int W, int C) { return upb() != 0 && H % 4 == 0 && W * C <= UB_MAXWC && C % 8 == 0; }
+bool upsample_band_ok(int H, int W, int C) { return H % 2 == 0 && W * C <= UB_MAXWC && C % 8 == 0; }
 
 // h2 (f16x3) or bf16 (bf != 0) records out of the upsample / GroupNorm apply (unet.hip, and the C ABI below)
 int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
@@ -723,19 +718,18 @@ int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const fl
     TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x_h2: scale/shift pair");
     if ((size_t)Bt * H * W * C == 0) return TCX_OK;
     if (upsample_band_ok(H, W, C)) {  // the banded LDS form (the 64^2 U-Net's us1 / us2)
-        const int v = upb();
-        const int rows = v == 3 ? 4 : 8;
+        constexpr int rows = 4;  // 4 output rows per band: 48 KB of LDS, 4-5 workgroups per CU (r03_n: the
+                                 // 8-row bands and 4-channel items were 3-28 % slower)
         const size_t shm = (size_t)(rows / 2 + 2) * W * C * sizeof(float);
-        using K = void (*)(const float*, char*, int, int, int, const float*, const float*, unsigned*, int);
-        const K k = v == 1 ? &k_upsample2x_band<8, false> : (v == 2 ? &k_upsample2x_band<8, true> : &k_upsample2x_band<4, true>);
-        static bool attr[4] = {};
-        if (!attr[v]) {
+        const auto k = &k_upsample2x_band<4, true>;
+        static bool attr = false;
+        if (!attr) {
             if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)(6 * UB_MAXWC * sizeof(float))) != hipSuccess) {
-                set_error("tcx_upsample2x_h2: cannot enable %zu B of dynamic LDS", 6 * UB_MAXWC * sizeof(float));
+                                    (int)(4 * UB_MAXWC * sizeof(float))) != hipSuccess) {
+                set_error("tcx_upsample2x_h2: cannot enable %zu B of dynamic LDS", 4 * UB_MAXWC * sizeof(float));
                 return TCX_EHIP;
             }
-            attr[v] = true;
+            attr = true;
         }
         hipLaunchKernelGGL(k, dim3(Bt * (2 * H / rows)), dim3(256), shm, st, x, (char*)y, H, W, C, scale, shift, ovf, bf);
         return check_launch("tcx_upsample2x_h2(band)");

@@ -105,6 +105,22 @@ def _cout_pad(cout: int) -> int:
     return _round_up(cout, 32)
 
 
+def _pack_frag(L, wh, cpad, kpad, cin, ks, st):
+    """Fragment-ordered copy of a packed h2 / bf16 conv weight: 3x3 (tcx_pack_conv_weight_h2_frag) or
+    4x4 stride-2 (tcx_pack_conv_weight_h2_frag4); None where no fragment kernel covers the shape."""
+    if ks == 3 and kpad == 9 * cin:
+        nfb, fn = int(L.tcx_conv_weight_h2_frag_bytes(cpad, cin)), L.tcx_pack_conv_weight_h2_frag
+    elif ks == 4 and kpad == 16 * cin:
+        nfb, fn = int(L.tcx_conv_weight_h2_frag4_bytes(cpad, cin)), L.tcx_pack_conv_weight_h2_frag4
+    else:
+        return None
+    if not nfb:
+        return None
+    whf = torch.empty(nfb // 4, device=wh.device, dtype=torch.float32)
+    check(fn(wh.data_ptr(), whf.data_ptr(), cpad, kpad, cin, st), "pack conv weight frag")
+    return whf
+
+
 class _UNetPack:
     """Device-resident packed weights + the tcx_unet descriptor for one CondUNetTiny."""
 
@@ -162,12 +178,10 @@ class _UNetPack:
                 check(L.tcx_pack_conv_weight_h2(wpk.data_ptr(), wh.data_ptr(), whs.data_ptr(), cpad, kpad, st),
                       "pack conv weight h2")
                 self.keep.extend([wh, whs])
-                # fragment-ordered copy for the 3x3 kernel k_conv3g (its B fragments load straight from it)
-                nfb = int(L.tcx_conv_weight_h2_frag_bytes(cpad, cin)) if ks == 3 and kpad == 9 * cin else 0
-                if nfb:
-                    whf = torch.empty(nfb // 4, device=device, dtype=torch.float32)
-                    check(L.tcx_pack_conv_weight_h2_frag(wh.data_ptr(), whf.data_ptr(), cpad, kpad, cin, st),
-                          "pack conv weight h2 frag")
+                # fragment-ordered copy for the 3x3 kernels (k_conv3g / k_conv3l*) and the 4x4/s2
+                # downsample kernel k_conv4s2g (their B fragments are DMA'd / loaded straight from it)
+                whf = _pack_frag(L, wh, cpad, kpad, cin, ks, st)
+                if whf is not None:
                     self.keep.append(whf)
             return TcxConv(wpk.data_ptr(), dev(m.bias), cin, cout, ks, kpad, cpad, ptr(wh), ptr(whs), ptr(whf))
 
@@ -216,12 +230,7 @@ class _UNetPack:
                 ws = torch.empty(4, device=self.device, dtype=torch.float32)
                 check(L.tcx_pack_conv_weight_bf16(c.w, wh.data_ptr(), ws.data_ptr(), c.cout_pad, c.kpad, self._st),
                       "pack conv weight bf16")
-                whf = None
-                if c.whf:
-                    nfb = int(L.tcx_conv_weight_h2_frag_bytes(c.cout_pad, c.cin))
-                    whf = torch.empty(nfb // 4, device=self.device, dtype=torch.float32)
-                    check(L.tcx_pack_conv_weight_h2_frag(wh.data_ptr(), whf.data_ptr(), c.cout_pad, c.kpad, c.cin,
-                                                         self._st), "pack conv weight bf16 frag")
+                whf = _pack_frag(L, wh, c.cout_pad, c.kpad, c.cin, c.ks, self._st) if c.whf else None
                 packs[name] = (wh, ws, whf)
             self._bf = packs
         return self._bf
