@@ -51,10 +51,11 @@ SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 m
 # FETCH_SIZE x 2 (gfx950 reports half of 16-B/lane reads) + WRITE_SIZE, averaged over the conv
 # launches of an evaluation.  A counter pass cannot run inside this process, so the
 # measured value is carried here with its source; it applies to the f16x3 path it was taken on.
-TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 503.3e6}
-TRAFFIC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE over the default kernels (k_conv3lg 32/64 h2 and "
-                  "64 GN+SiLU prologue, k_conv3l 32 prologue, k_conv3g 16, k_conv4s2h, k_conv SPL), "
-                  "profiles/r02_zq_pmc_traffic.txt")
+TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 262.1e6}
+TRAFFIC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE, averaged over the 270 split-path conv launches "
+                  "(k_conv3lg 16/32/64 h2 and 32/64 GN+SiLU prologue, k_conv3g 16 prologue, k_conv4s2g, k_lin1x1) of "
+                  "two sampler steps, profiles/r03_r_pmc_traffic.txt (earlier rounds' 503 MB also averaged in the "
+                  "fp32 comparison pass's k_conv launches, ~1.2 GB each)")
 
 
 def _cpu_model() -> str:

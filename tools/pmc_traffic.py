@@ -39,7 +39,7 @@ def main():
     n = sum(v[0] for v in conv)
     if n:
         avg = sum(v[0] * (v[1] + v[2]) for v in conv) / n
-        print(f"\nconv launches (k_conv<>, k_conv3g<>, k_conv3l<>, k_conv3lg<>, k_conv3p<>, k_conv4s2h<>): {n}, average HBM bytes per launch (read x2 + write) = "
+        print(f"\nconv launches (k_conv<>, k_conv3g<>, k_conv3l<>, k_conv3lg<>, k_conv3p<>, k_conv4s2h<>, k_conv4s2g<>, k_lin1x1<>): {n}, average HBM bytes per launch (read x2 + write) = "
               f"{avg:.1f} MB")
 
 

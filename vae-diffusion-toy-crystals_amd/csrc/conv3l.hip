@@ -399,7 +399,9 @@ __device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, Is.
     (f(std::integral_constant<int, Is>{}), ...);
 }
 
-template <int W, int PRO>
+// PQ (PRO 1): the raw halo's DMA is spread over taps 0 .. PQ - 1 (r03_s: 3 taps ~1 % faster than 2 on the
+// prologue layers, 4 equal to 3; the wait stays at tap 4 / 5)
+template <int W, int PRO, int PQ = 3>
 __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     constexpr int RT = 2, NT = L_NT, NTHR = 64 * L_NW;
     constexpr int W2 = W + 2;
@@ -685,10 +687,10 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         // pair issued at the start of odd tap 2k-3 has two taps of latency cover before its wait
         if (wv < 2) {
             if constexpr (s == 1) pair_issue((c + 3) >> 1);
-        } else if constexpr (PRO == 0 ? t < 4 : t < 2) {
+        } else if constexpr (PRO == 0 ? t < 4 : t < PQ) {
             // halo of chunk j+1 into the other buffer (not after the last chunk): PRO 0 a quarter per
-            // tap over taps 0-3, PRO 1 half per tap over taps 0-1 (the raw data is waited for at tap 4/5)
-            constexpr int NQ = PRO == 0 ? 4 : 2;
+            // tap over taps 0-3, PRO 1 a third per tap over taps 0-2 (the raw data is waited for at tap 4/5)
+            constexpr int NQ = PRO == 0 ? 4 : PQ;
             constexpr int q0 = (NIH * t) / NQ, q1 = (NIH * (t + 1)) / NQ;
             if (more) halo_issue(j + 1, hb ^ 1, q0, q1);
         }
