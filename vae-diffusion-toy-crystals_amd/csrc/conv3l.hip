@@ -366,20 +366,9 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3l(ConvParams p) {
 // during the next two taps every wave rewrites its quarter of the units IN PLACE as h2 of
 // silu(x sc + sh) (per unit: two ds_read_b128, eight values one per MFMA gap, two ds_write_b128).
 // Waves 0-1 own the 8-channel group 0 of every slot, waves 2-3 group 1, so a wave's GroupNorm
-// scale/shift for the chunk are 16 wave-uniform values (scalar loads, no LDS table).
+// scale/shift for the chunk are 16 wave-uniform values (SGPRs, from the LDS copy of the image's tables).
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
-}
-typedef float f32x8 __attribute__((ext_vector_type(8)));
-// 8 wave-uniform floats by a scalar load (lgkmcnt, not the in-order vmcnt of the LDS-DMA stream;
-// hipcc emits a vector load for a uniform address in a kernel that also stores to global memory)
-__device__ __forceinline__ f32x8 sload8(const float* ptr) {
-    const unsigned long long a = (unsigned long long)ptr;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-    const unsigned long long u = ((unsigned long long)hi << 32) | lo;
-    f32x8 r;
-    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(u) : "memory");
-    return r;
 }
 constexpr int WAIT_VM0 = 0x0F70;    // s_waitcnt vmcnt(0)
 constexpr int WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
@@ -401,6 +390,9 @@ __device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, Is.
 
 // PQ (PRO 1): the raw halo's DMA is spread over taps 0 .. PQ - 1 (r03_s: 3 taps ~1 % faster than 2 on the
 // prologue layers, 4 equal to 3; the wait stays at tap 4 / 5)
+// PRO 1's GroupNorm tables: staged in LDS once per workgroup and read per chunk with broadcast
+// ds_reads issued at tap 8 and moved to SGPRs at tap 0 (r03_t: ~1 % faster than two scalar loads +
+// lgkmcnt(0) per chunk at tap 8, which also waited for every LDS read in flight)
 template <int W, int PRO, int PQ = 3>
 __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
     constexpr int RT = 2, NT = L_NT, NTHR = 64 * L_NW;
@@ -551,13 +543,23 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         tval |= hp0 < NPXS ? 1u << i : 0u;
     }
     float tsc[8], tsh[8];  // this wave's group of the chunk being transformed (wave-uniform)
-    auto load_tabs = [&](int j) {
-        const size_t o = (size_t)b * p.C1 + j * L_KC + 8 * tg;
-        const f32x8 a = sload8(p.sc1 + o), c = sload8(p.sh1 + o);
+    // tables in LDS after the ring ([sc | sh][Cin]); issue = 4 broadcast ds_read_b128 into tq, commit =
+    // readfirstlane into the SGPR copies
+    const float* const TsL = reinterpret_cast<const float*>(smc + RING + 2 * L_PAIR);
+    float4 tq[4];
+    auto issue_tabs = [&](int j) {
+        const float* t = TsL + j * L_KC + 8 * tg;
+        tq[0] = *reinterpret_cast<const float4*>(t);
+        tq[1] = *reinterpret_cast<const float4*>(t + 4);
+        tq[2] = *reinterpret_cast<const float4*>(t + p.C1);
+        tq[3] = *reinterpret_cast<const float4*>(t + p.C1 + 4);
+    };
+    auto commit_tabs = [&]() {
+        const float* q = reinterpret_cast<const float*>(tq);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            tsc[k] = a[k];
-            tsh[k] = c[k];
+            tsc[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, q[k])));
+            tsh[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, q[8 + k])));
         }
     };
     // A unit's 8 values spread over the 18 MFMA gaps of a tap (rb 0: gaps 0-8, rb 1: 9-17).
@@ -647,20 +649,28 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         }
     };
 
-    // ---- prologue: pairs 0, 1 and halo 0 in LDS
+    // ---- prologue: pairs 0, 1 and halo 0 in LDS (PRO 1: and the image's GroupNorm tables)
     if (wv < 2) {
         pair_issue(0);
         pair_issue(1);
     } else {
         halo_issue(0, 0, 0, NIH);
     }
+    if constexpr (PRO == 1) {
+        float* const Tw = reinterpret_cast<float*>(smc + RING + 2 * L_PAIR);
+        for (int c = tid; c < p.C1; c += NTHR) {
+            Tw[c] = p.sc1[(size_t)b * p.C1 + c];
+            Tw[p.C1 + c] = p.sh1[(size_t)b * p.C1 + c];
+        }
+    }
     __builtin_amdgcn_s_waitcnt(WAIT_VM0);
     barrier();
     if constexpr (PRO == 1) {
-        load_tabs(0);
+        issue_tabs(0);
+        commit_tabs();
         transform_all(0);
         barrier();
-        if (cpt > 1) load_tabs(1);
+        if (cpt > 1) issue_tabs(1);  // committed at tap 0 of chunk 0
     }
     rd_b(0, 0);
     rd_a(0, 0, 0);
@@ -696,6 +706,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (!pre_a0 && t == 0) rd_a(0, 0, hb);  // published at the end of the last tap
+        if constexpr (PRO == 1 && t == 0) commit_tabs();  // tables of chunk j + 1
         rd_b(s ^ 1, c + 1);
         if (t != 8) rd_a(1, t, hb);
         __builtin_amdgcn_sched_barrier(0);
@@ -724,7 +735,7 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
         __builtin_amdgcn_sched_barrier(0);
         if (t == 7) rd_a(1, 8, hb);
         if constexpr (PRO == 1 && t == 8) {
-            if (j + 2 < cpt) load_tabs(j + 2);
+            if (j + 2 < cpt) issue_tabs(j + 2);
             if constexpr (s == 1) barrier();  // odd chunk: publish the transformed halo
         }
         if constexpr (s == 0) {  // even tap: the barrier that publishes pair c/2 + 1 (and halo j+1:
@@ -765,8 +776,8 @@ __global__ __launch_bounds__(64 * L_NW, 2) void k_conv3lg(ConvParams p) {
 }
 
 template <int W>
-constexpr size_t conv3lg_lds_bytes() {
-    return (size_t)2 * ((l_npx(W) + 15) / 16) * 16 * 64 + 2 * (size_t)L_PAIR;
+constexpr size_t conv3lg_lds_bytes() {  // + the GroupNorm tables of PRO 1 ([2][Cin <= 384] floats)
+    return (size_t)2 * ((l_npx(W) + 15) / 16) * 16 * 64 + 2 * (size_t)L_PAIR + 2 * 384 * sizeof(float);
 }
 
 template <int W>

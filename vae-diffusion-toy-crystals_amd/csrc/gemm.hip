@@ -552,6 +552,139 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
     }
 }
 
+// (temporary A/B: the round-2 form with 2-byte LDS stores, TCX_WG_OLD=1)
+template <int NT>
+__global__ __launch_bounds__(256, 2) void k_wgrad_h2_old(WgParams p) {
+    constexpr int BN = 32 * NT;
+    constexpr int RS = 40;  // halves per LDS row: 32 pixels + 8 pad (80 B)
+    __shared__ __attribute__((aligned(16))) _Float16 Ah[2][GBM * RS];
+    __shared__ __attribute__((aligned(16))) _Float16 Al[2][GBM * RS];
+    __shared__ __attribute__((aligned(16))) _Float16 Bh[2][BN * RS];
+    __shared__ __attribute__((aligned(16))) _Float16 Bl[2][BN * RS];
+    const int split = blockIdx.y;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kblk = tile / p.ncblk, cblk = tile - (tile / p.ncblk) * p.ncblk;
+    const int k0 = kblk * GBM, c0 = cblk * BN;
+    const int tid = threadIdx.x;
+    const int px = tid & 31, q = tid >> 5;
+    const int chunk0 = split * p.cps;
+    const int nch_all = (p.M + 31) / 32;
+    const int chunk1 = min(chunk0 + p.cps, nch_all);
+    const char* x1 = reinterpret_cast<const char*>(p.x1);
+    const char* x2 = reinterpret_cast<const char*>(p.x2);
+    const char* dyb = reinterpret_cast<const char*>(p.dy);
+    // per-thread im2col quads: k = k0 + 4 (q + 8 i) .. +3 share one tap and source (C1, C2 % 8 == 0)
+    int tdy[4], tdx[4], toff[4];
+    bool tsrc1[4], tkv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = k0 + 4 * (q + 8 * i);
+        const int kk = k < p.K ? k : 0;
+        const int tap = kk / p.Cin, ci = kk - (kk / p.Cin) * p.Cin;
+        tdy[i] = tap / p.ks;
+        tdx[i] = tap - (tap / p.ks) * p.ks;
+        tsrc1[i] = ci < p.C1;
+        const int c = ci < p.C1 ? ci : ci - p.C1;
+        toff[i] = (c >> 3) * 32 + (c & 4) * 2;  // byte offset of the quad's hi half in the pixel record
+        tkv[i] = k < p.K;
+    }
+    uint2 ah[4], al[4], bh[NT], bl[NT];
+    auto load = [&](int c) {
+        const int m = c * 32 + px;
+        const bool mv = m < p.M;
+        const int mm = mv ? m : 0;
+        const int b = mm / p.HoWo, r = mm - (mm / p.HoWo) * p.HoWo;
+        const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+        const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int yy = iy0 + tdy[i], xx = ix0 + tdx[i];
+            bool ok = mv && tkv[i];
+            if (p.circular) {
+                yy = wrap_idx(yy, p.H);
+                xx = wrap_idx(xx, p.W);
+            } else {
+                ok = ok && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
+            }
+            const size_t pix = ((size_t)b * p.H + (ok ? yy : 0)) * p.W + (ok ? xx : 0);
+            const char* a = tsrc1[i] ? x1 + pix * p.C1 * 4 + toff[i] : x2 + pix * p.C2 * 4 + toff[i];
+            ah[i] = ok ? *reinterpret_cast<const uint2*>(a) : make_uint2(0u, 0u);
+            al[i] = ok ? *reinterpret_cast<const uint2*>(a + 16) : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int co = c0 + 4 * (q + 8 * j);
+            const bool ok = mv && co < p.Cout;
+            const char* d = dyb + ((size_t)mm * p.Cout + (co >> 3) * 8) * 4 + (co & 4) * 2;
+            bh[j] = ok ? *reinterpret_cast<const uint2*>(d) : make_uint2(0u, 0u);
+            bl[j] = ok ? *reinterpret_cast<const uint2*>(d + 16) : make_uint2(0u, 0u);
+        }
+    };
+    auto put4 = [&](_Float16* plane, int row0, const uint2 v) {  // 4 consecutive rows, this pixel
+        plane[(row0 + 0) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.x & 0xffffu));
+        plane[(row0 + 1) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.x >> 16));
+        plane[(row0 + 2) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.y & 0xffffu));
+        plane[(row0 + 3) * RS + px] = __builtin_bit_cast(_Float16, (unsigned short)(v.y >> 16));
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            put4(Ah[buf], 4 * (q + 8 * i), ah[i]);
+            put4(Al[buf], 4 * (q + 8 * i), al[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            put4(Bh[buf], 4 * (q + 8 * j), bh[j]);
+            put4(Bl[buf], 4 * (q + 8 * j), bl[j]);
+        }
+    };
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
+    const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
+    if (chunk0 < chunk1) {
+        load(chunk0);
+        store(0);
+    }
+    __syncthreads();
+    for (int c = chunk0; c < chunk1; ++c) {
+        const int cur = (c - chunk0) & 1;
+        if (c + 1 < chunk1) load(c + 1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int off = 16 * s + 8 * lh;
+            const h8 fah = *reinterpret_cast<const h8*>(&Ah[cur][(wv * 32 + li) * RS + off]);
+            const h8 fal = *reinterpret_cast<const h8*>(&Al[cur][(wv * 32 + li) * RS + off]);
+            h8 fbh[NT], fbl[NT];
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                fbh[n] = *reinterpret_cast<const h8*>(&Bh[cur][(n * 32 + li) * RS + off]);
+                fbl[n] = *reinterpret_cast<const h8*>(&Bl[cur][(n * 32 + li) * RS + off]);
+            }
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbl[n], acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[n], acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbh[n], acc[n], 0, 0, 0);
+        }
+        if (c + 1 < chunk1) store(cur ^ 1);
+        __syncthreads();
+    }
+    const float sc = *p.comb;
+    float* dst = p.part + (size_t)split * p.K * p.Cout;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int co = c0 + n * 32 + li;
+        if (co >= p.Cout) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = k0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (k < p.K) dst[(size_t)k * p.Cout + co] = acc[n][r] * sc;
+        }
+    }
+}
+
 // dw[co][ci][ky][kx] = beta * dw + sum_s part[s][k][co], k = (ky*ks + kx)*Cin + ci (fixed order)
 __global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int K, int Cout, int Cin, int ks,
                                float beta, float* __restrict__ dw) {
@@ -839,7 +972,12 @@ extern "C" int tcx_conv_wgrad_h2(const void* x1, const void* x2, int Bt, int H, 
     p.part = reinterpret_cast<float*>(base);
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(p.nkblk * p.ncblk, p.nsplit);
-    if (nt == 3) hipLaunchKernelGGL((k_wgrad_h2<3>), grid, dim3(256), 0, st, p);
+    static const bool old = getenv("TCX_WG_OLD") && getenv("TCX_WG_OLD")[0] == '1';
+    if (old) {
+        if (nt == 3) hipLaunchKernelGGL((k_wgrad_h2_old<3>), grid, dim3(256), 0, st, p);
+        else if (nt == 2) hipLaunchKernelGGL((k_wgrad_h2_old<2>), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((k_wgrad_h2_old<1>), grid, dim3(256), 0, st, p);
+    } else if (nt == 3) hipLaunchKernelGGL((k_wgrad_h2<3>), grid, dim3(256), 0, st, p);
     else if (nt == 2) hipLaunchKernelGGL((k_wgrad_h2<2>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((k_wgrad_h2<1>), grid, dim3(256), 0, st, p);
     TCX_TRY(check_launch("tcx_conv_wgrad_h2"));
