@@ -407,9 +407,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_conv3g(ConvParams p) {
     }
 }
 
-template <int W>
+template <int W, int NW = g_nw(W)>
 int launch3g(const ConvParams& p, hipStream_t st) {
-    constexpr int NW = g_nw(W);
     constexpr bool ONLY_BF = W == 256;  // the 256-px rows exist only in the slim bf16 form
     if (ONLY_BF && !p.bf) {
         set_error("tcx_conv2d_h2: 256-px rows on k_conv3g need bf16");

@@ -438,134 +438,6 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
     const int kblk = tile / p.ncblk, cblk = tile - (tile / p.ncblk) * p.ncblk;
     const int k0 = kblk * GBM, c0 = cblk * BN;
     const int tid = threadIdx.x;
-    // thread = (4 consecutive pixels 4 pxq .. 4 pxq + 3 of the 32-pixel chunk, k quad q of the A tile /
-    // co quad q of the B tile): the 4 pixels' halves of one k row are ONE 8-byte ds_write_b64 (the
-    // 2-byte stores of one pixel per thread bounded the kernel: DESIGN.md §3b); needs Wo % 4 == 0 so
-    // the 4 pixels share an output row
-    const int pxq = tid & 7, q = tid >> 3;
-    const int chunk0 = split * p.cps;
-    const int nch_all = (p.M + 31) / 32;
-    const int chunk1 = min(chunk0 + p.cps, nch_all);
-    const char* x1 = reinterpret_cast<const char*>(p.x1);
-    const char* x2 = reinterpret_cast<const char*>(p.x2);
-    const char* dyb = reinterpret_cast<const char*>(p.dy);
-    // this thread's im2col quad: k = k0 + 4 q .. +3 share one tap and source (C1, C2 % 8 == 0)
-    const int kq = k0 + 4 * q;
-    const bool tkv = kq < p.K;
-    const int kk = tkv ? kq : 0;
-    const int tap = kk / p.Cin, ci = kk - (kk / p.Cin) * p.Cin;
-    const int tdy = tap / p.ks, tdx = tap - (tap / p.ks) * p.ks;
-    const bool tsrc1 = ci < p.C1;
-    const int tcc = ci < p.C1 ? ci : ci - p.C1;
-    const int toff = (tcc >> 3) * 32 + (tcc & 4) * 2;  // byte offset of the quad's hi half in the pixel record
-    const int cq = c0 + 4 * q;                       // this thread's co quad of the B tile
-    const bool bq = q < BN / 4;
-    uint2 ah[4], al[4], bh[4], bl[4];
-    auto load = [&](int c) {
-        const int m0p = c * 32 + 4 * pxq;  // first of the 4 pixels (one output row: Wo % 4 == 0)
-        const bool mv = m0p < p.M;
-        const int mm = mv ? m0p : 0;
-        const int b = mm / p.HoWo, r = mm - (mm / p.HoWo) * p.HoWo;
-        const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
-        int yy = oy * p.stride - p.pad + tdy;
-        bool oky = mv && tkv;
-        if (p.circular) yy = wrap_idx(yy, p.H);
-        else oky = oky && yy >= 0 && yy < p.H;
-        const size_t rowpix = ((size_t)b * p.H + (oky ? yy : 0)) * p.W;
-        const bool okb = mv && bq && cq < p.Cout;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            int xx = (ox + e) * p.stride - p.pad + tdx;
-            bool ok = oky;
-            if (p.circular) xx = wrap_idx(xx, p.W);
-            else ok = ok && xx >= 0 && xx < p.W;
-            const size_t pix = rowpix + (ok ? xx : 0);
-            const char* a = tsrc1 ? x1 + pix * p.C1 * 4 + toff : x2 + pix * p.C2 * 4 + toff;
-            ah[e] = ok ? *reinterpret_cast<const uint2*>(a) : make_uint2(0u, 0u);
-            al[e] = ok ? *reinterpret_cast<const uint2*>(a + 16) : make_uint2(0u, 0u);
-            const char* d = dyb + ((size_t)(mm + e) * p.Cout + (cq >> 3) * 8) * 4 + (cq & 4) * 2;
-            bh[e] = okb ? *reinterpret_cast<const uint2*>(d) : make_uint2(0u, 0u);
-            bl[e] = okb ? *reinterpret_cast<const uint2*>(d + 16) : make_uint2(0u, 0u);
-        }
-    };
-    // row r (0..3) of the quad: half r of each pixel's uint2, the 4 pixels packed into one 8-B store
-    auto half = [](const uint2 v, int r) -> unsigned { return ((r < 2 ? v.x : v.y) >> (16 * (r & 1))) & 0xffffu; };
-    auto put = [&](_Float16* plane, const uint2 (&v)[4]) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint2 w = make_uint2(half(v[0], r) | (half(v[1], r) << 16), half(v[2], r) | (half(v[3], r) << 16));
-            *reinterpret_cast<uint2*>(&plane[(4 * q + r) * RS + 4 * pxq]) = w;
-        }
-    };
-    auto store = [&](int buf) {
-        put(Ah[buf], ah);
-        put(Al[buf], al);
-        if (bq) {
-            put(Bh[buf], bh);
-            put(Bl[buf], bl);
-        }
-    };
-    f32x16 acc[NT];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
-    const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
-    if (chunk0 < chunk1) {
-        load(chunk0);
-        store(0);
-    }
-    __syncthreads();
-    for (int c = chunk0; c < chunk1; ++c) {
-        const int cur = (c - chunk0) & 1;
-        if (c + 1 < chunk1) load(c + 1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int off = 16 * s + 8 * lh;
-            const h8 fah = *reinterpret_cast<const h8*>(&Ah[cur][(wv * 32 + li) * RS + off]);
-            const h8 fal = *reinterpret_cast<const h8*>(&Al[cur][(wv * 32 + li) * RS + off]);
-            h8 fbh[NT], fbl[NT];
-#pragma unroll
-            for (int n = 0; n < NT; ++n) {
-                fbh[n] = *reinterpret_cast<const h8*>(&Bh[cur][(n * 32 + li) * RS + off]);
-                fbl[n] = *reinterpret_cast<const h8*>(&Bl[cur][(n * 32 + li) * RS + off]);
-            }
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbl[n], acc[n], 0, 0, 0);
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[n], acc[n], 0, 0, 0);
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbh[n], acc[n], 0, 0, 0);
-        }
-        if (c + 1 < chunk1) store(cur ^ 1);
-        __syncthreads();
-    }
-    const float sc = *p.comb;
-    float* dst = p.part + (size_t)split * p.K * p.Cout;
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-        const int co = c0 + n * 32 + li;
-        if (co >= p.Cout) continue;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int k = k0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (k < p.K) dst[(size_t)k * p.Cout + co] = acc[n][r] * sc;
-        }
-    }
-}
-
-// (temporary A/B: the round-2 form with 2-byte LDS stores, TCX_WG_OLD=1)
-template <int NT>
-__global__ __launch_bounds__(256, 2) void k_wgrad_h2_old(WgParams p) {
-    constexpr int BN = 32 * NT;
-    constexpr int RS = 40;  // halves per LDS row: 32 pixels + 8 pad (80 B)
-    __shared__ __attribute__((aligned(16))) _Float16 Ah[2][GBM * RS];
-    __shared__ __attribute__((aligned(16))) _Float16 Al[2][GBM * RS];
-    __shared__ __attribute__((aligned(16))) _Float16 Bh[2][BN * RS];
-    __shared__ __attribute__((aligned(16))) _Float16 Bl[2][BN * RS];
-    const int split = blockIdx.y;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int kblk = tile / p.ncblk, cblk = tile - (tile / p.ncblk) * p.ncblk;
-    const int k0 = kblk * GBM, c0 = cblk * BN;
-    const int tid = threadIdx.x;
     const int px = tid & 31, q = tid >> 5;
     const int chunk0 = split * p.cps;
     const int nch_all = (p.M + 31) / 32;
@@ -959,7 +831,6 @@ extern "C" int tcx_conv_wgrad_h2(const void* x1, const void* x2, int Bt, int H, 
     p.Ho = (H + 2 * pad - ks) / stride + 1;
     p.Wo = (W + 2 * pad - ks) / stride + 1;
     TCX_REQUIRE(p.Ho > 0 && p.Wo > 0, "tcx_conv_wgrad_h2: empty output");
-    TCX_REQUIRE(p.Wo % 4 == 0, "tcx_conv_wgrad_h2: needs Wo %% 4 == 0 (4 pixels of a row per thread)");
     p.HoWo = p.Ho * p.Wo; p.M = Bt * p.HoWo;
     p.ks = ks; p.stride = stride; p.pad = pad; p.circular = circular;
     p.dy = (const float*)dy; p.Cout = Cout; p.K = ks * ks * p.Cin; p.comb = comb;
@@ -972,12 +843,7 @@ extern "C" int tcx_conv_wgrad_h2(const void* x1, const void* x2, int Bt, int H, 
     p.part = reinterpret_cast<float*>(base);
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(p.nkblk * p.ncblk, p.nsplit);
-    static const bool old = getenv("TCX_WG_OLD") && getenv("TCX_WG_OLD")[0] == '1';
-    if (old) {
-        if (nt == 3) hipLaunchKernelGGL((k_wgrad_h2_old<3>), grid, dim3(256), 0, st, p);
-        else if (nt == 2) hipLaunchKernelGGL((k_wgrad_h2_old<2>), grid, dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((k_wgrad_h2_old<1>), grid, dim3(256), 0, st, p);
-    } else if (nt == 3) hipLaunchKernelGGL((k_wgrad_h2<3>), grid, dim3(256), 0, st, p);
+    if (nt == 3) hipLaunchKernelGGL((k_wgrad_h2<3>), grid, dim3(256), 0, st, p);
     else if (nt == 2) hipLaunchKernelGGL((k_wgrad_h2<2>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((k_wgrad_h2<1>), grid, dim3(256), 0, st, p);
     TCX_TRY(check_launch("tcx_conv_wgrad_h2"));

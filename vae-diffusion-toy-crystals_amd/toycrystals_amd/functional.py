@@ -216,7 +216,7 @@ def _conv_wgrad(x1, x2, dy, Cout, ks, stride, pad, circular, xrec=None, dyrec=No
     dw = _empty((Cout, C1 + C2, ks, ks), dy)
     nb = int(L.tcx_conv_wgrad_workspace(B, Ho, Wo, C1 + C2, Cout, ks))
     ws = _ws(dy.device, nb)
-    if _WGRAD_SPLIT and xrec is not None and Cout % 8 == 0 and Wo % 4 == 0 and dy.numel() * 4 < (1 << 31):
+    if _WGRAD_SPLIT and xrec is not None and Cout % 8 == 0 and dy.numel() * 4 < (1 << 31):
         if dyrec is None:
             (dyh,), dyinv = _h2_scaled([dy])
         else:
