@@ -396,7 +396,7 @@ __global__ __launch_bounds__(256) void k_head8(const float* __restrict__ h, int 
                                                float* __restrict__ r) {
     constexpr int C = 32 * Q;
     constexpr int CL = 4 * Q;  // channels per lane
-    __shared__ __attribute__((aligned(16))) float ws[C * 9];
+    __shared__ __attribute__((aligned(16))) float ws[C * 12];  // [c][12]: taps 0-8 + pad: 3 ds_read_b128 per channel
     __shared__ __attribute__((aligned(16))) float ssc[C], ssh[C];
     const int p0 = blockIdx.x * HP8;  // first pixel (flat over b, p)
     const int b = p0 / HW;
@@ -410,7 +410,10 @@ __global__ __launch_bounds__(256) void k_head8(const float* __restrict__ h, int 
 #pragma unroll
         for (int q = 0; q < Q; ++q) v[q] = *reinterpret_cast<const float4*>(src + 4 * q);
     }
-    for (int i = tid; i < C * 9; i += 256) ws[i] = w_out[i];
+    for (int i = tid; i < C * 12; i += 256) {
+        const int c = i / 12, t = i - (i / 12) * 12;
+        ws[i] = t < 9 ? w_out[c * 9 + t] : 0.f;
+    }
     for (int i = tid; i < C; i += 256) {
         ssc[i] = tsc[(size_t)b * C + i];
         ssh[i] = tsh[(size_t)b * C + i];
@@ -437,9 +440,18 @@ __global__ __launch_bounds__(256) void k_head8(const float* __restrict__ h, int 
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int c = c0 + 4 * q + e;
-                const float x = silu_f(fmaf(xs[e], ssc[c], ssh[c]));
-#pragma unroll
-                for (int t = 0; t < 9; ++t) acc[t] = fmaf(x, ws[c * 9 + t], acc[t]);
+                // SiLU as y rcp(1 + exp2(-y log2 e)) (hardware exp2 / rcp, as the conv prologues): the
+                // IEEE expf + division form made this kernel VALU-bound (~25 instructions per element)
+                const float yv = fmaf(xs[e], ssc[c], ssh[c]);
+                const float x = yv * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * yv));
+                const float4 w0 = *reinterpret_cast<const float4*>(&ws[c * 12]);
+                const float4 w1 = *reinterpret_cast<const float4*>(&ws[c * 12 + 4]);
+                const float w8 = ws[c * 12 + 8];
+                acc[0] = fmaf(x, w0.x, acc[0]); acc[1] = fmaf(x, w0.y, acc[1]);
+                acc[2] = fmaf(x, w0.z, acc[2]); acc[3] = fmaf(x, w0.w, acc[3]);
+                acc[4] = fmaf(x, w1.x, acc[4]); acc[5] = fmaf(x, w1.y, acc[5]);
+                acc[6] = fmaf(x, w1.z, acc[6]); acc[7] = fmaf(x, w1.w, acc[7]);
+                acc[8] = fmaf(x, w8, acc[8]);
             }
         }
 #pragma unroll
