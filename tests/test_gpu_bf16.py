@@ -105,11 +105,14 @@ def conv_ref(x, w, b, stride, pad):
 
 
 @pytest.mark.parametrize("B,C1,C2,H,co,ks,stride,frag", [
-    (2, 96, 0, 64, 96, 3, 1, True),      # k_conv3g, 64-px rows
+    (2, 96, 0, 64, 96, 3, 1, True),      # k_conv3lb (LDS-DMA bf16), 64-px rows
     (2, 96, 96, 32, 96, 3, 1, True),     # k_conv3g, two sources, 32-px rows
-    (1, 96, 0, 128, 96, 3, 1, True),     # k_conv3g, 128-px rows
-    (1, 96, 0, 256, 96, 3, 1, True),     # k_conv3g slim halo (hi pieces only), 256-px rows
-    (1, 96, 96, 256, 96, 3, 1, True),    # slim, two sources (up1_0 at 256^2)
+    (1, 96, 0, 128, 96, 3, 1, True),     # k_conv3lb, 128-px rows
+    (1, 96, 0, 256, 96, 3, 1, True),     # k_conv3lb, 256-px rows (one row per tile)
+    (1, 96, 96, 256, 96, 3, 1, True),    # k_conv3lb, two sources (up1_0 at 256^2)
+    (2, 192, 0, 64, 192, 3, 1, True),    # k_conv3lb, two n blocks (mid block at 256^2)
+    (1, 192, 192, 128, 96, 3, 1, True),  # k_conv3lb, Cin = 384 over two sources (up2_0 at 256^2)
+    (3, 96, 0, 128, 192, 3, 1, True),    # k_conv3lb, 96 -> 192, odd batch (down2_0 at 256^2)
     (2, 64, 0, 16, 96, 3, 1, True),      # k_conv3g, 16-px rows (mid block)
     (2, 64, 0, 16, 64, 3, 1, False),     # no fragment copy: the im2col kernel (no bf16 k_conv3p)
     (2, 96, 0, 64, 96, 4, 2, False),     # k_conv4s2h (ds1 at 64 -> 32)
