@@ -352,10 +352,12 @@ def test_gn_apply_h2(inplace):
     assert int(ovf.item()) == 0
 
 
-@pytest.mark.parametrize("B,H,W,C", [(2, 8, 8, 96), (2, 16, 16, 192), (2, 32, 32, 96), (1, 12, 20, 32), (1, 6, 64, 64)])
+@pytest.mark.parametrize("B,H,W,C", [(2, 8, 8, 96), (2, 16, 16, 192), (2, 32, 32, 96), (1, 12, 20, 32), (1, 6, 64, 64),
+                                     (2, 16, 128, 96), (1, 8, 64, 192), (1, 6, 48, 96), (1, 5, 7, 8)])
 def test_upsample_h2(B, H, W, C):
-    """h2 upsample (the banded LDS kernel where H % 4 == 0 and W C <= 3072 — us1 / us2 of the 64^2
-    U-Net —, else k_upsample2x_g8) against the fp32 upsample: the h2 decode bound."""
+    """h2 upsample (the banded LDS kernel where H % 2 == 0 and W C <= 3072 — us1 / us2 of the 64^2
+    U-Net —; the column-segmented band for wider rows — config 5's us1 / us2 at 256^2, 16 / 8 source
+    columns per segment —; else k_upsample2x_g8) against the fp32 upsample: the h2 decode bound."""
     x = dev(rng.standard_normal((B, H, W, C)))
     y = torch.empty((B, 2 * H, 2 * W, C), device="cuda")
     y32 = torch.empty_like(y)
@@ -364,7 +366,8 @@ def test_upsample_h2(B, H, W, C):
     dec_ok(from_h2(y).cpu().numpy(), y32.cpu().numpy())
 
 
-@pytest.mark.parametrize("B,H,W,C", [(2, 32, 32, 96), (2, 16, 16, 192), (1, 6, 64, 64)])
+@pytest.mark.parametrize("B,H,W,C", [(2, 32, 32, 96), (2, 16, 16, 192), (1, 6, 64, 64), (2, 16, 128, 96),
+                                     (1, 8, 64, 192)])
 def test_upsample_h2_fused_gn_silu(B, H, W, C):
     """The evaluator's us1 input: GroupNorm+SiLU tables applied by the upsample while it stages its
     source (no apply pass), against the in-place fp32 apply pass (IEEE-division SiLU) followed by the

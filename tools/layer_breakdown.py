@@ -7,6 +7,8 @@ seq, cur = [], []
 # an evaluation starts at k_cond (per-evaluation conditioning) or, when the sampler hoisted it
 # (k_cond_maps once per call), at the first conv
 starts = 'k_cond(' if any('k_cond(' in r['Kernel_Name'] for r in rows) else 'k_conv_first'
+if starts == 'k_conv_first':  # round 3: statistics pass <1> then record pass <2>; the fp32 form <0>
+    starts = next((s for s in ('k_conv_first<1>', 'k_conv_first<0>') if any(s in r['Kernel_Name'] for r in rows)), starts)
 for r in rows:
     if starts in r['Kernel_Name']:
         if cur:

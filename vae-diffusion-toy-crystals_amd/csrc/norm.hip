@@ -413,6 +413,100 @@ __global__ __launch_bounds__(256, 2) void k_upsample2x_band(const float* __restr
     h2_flag(ovf, bad && !bf);
 }
 
+// Column-segmented form of k_upsample2x_band for source rows wider than the LDS holds (config 5's us1 /
+// us2 at 256^2: 128 x 96 and 64 x 192 floats per source row): one workgroup per (image, band of ROWS
+// output rows, segment of SW source columns).  The segment's SW columns and one clamped halo column
+// either side (the bilinear taps of its 2 SW output columns) are staged; the arithmetic per output is
+// that of k_upsample2x_band / k_upsample2x_g8 (same clamped coordinates, same fmaf order).
+template <int ROWS>
+__global__ __launch_bounds__(256, 2) void k_upsample2x_bandseg(const float* __restrict__ x, char* __restrict__ y,
+                                                              int H, int W, int C, int SW,
+                                                              const float* __restrict__ tsc,
+                                                              const float* __restrict__ tsh, unsigned* ovf, int bf) {
+    constexpr int SRC = ROWS / 2 + 2;
+    extern __shared__ __attribute__((aligned(16))) float ub[];  // [SRC][SW + 2][C]
+    const int nband = 2 * H / ROWS, nseg = W / SW;
+    const int seg = blockIdx.x % nseg;
+    const int rest = blockIdx.x / nseg;
+    const int b = rest / nband, band = rest - (rest / nband) * nband;
+    const int ys0 = band * (ROWS / 2) - 1;  // source row of LDS row 0 (before clamping)
+    const int xs0 = seg * SW - 1;           // source column of LDS column 0 (before clamping)
+    const int SC2 = SW + 2;
+    const int RC4 = SC2 * C / 4, C4 = C / 4;
+    constexpr int NL = (SRC * UB_MAXWC / 4 + 255) / 256;
+    f4v v[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < SRC * RC4) {
+            const int r = i / RC4, e = i - (i / RC4) * RC4;
+            const int col = e / C4, c4 = e - (e / C4) * C4;
+            const int ysrc = min(max(ys0 + r, 0), H - 1);
+            const int xsrc = min(max(xs0 + col, 0), W - 1);
+            v[k] = *reinterpret_cast<const f4v*>(x + (((size_t)b * H + ysrc) * W + xsrc) * C + 4 * c4);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < SRC * RC4) {
+            if (tsc) {
+                const int c4 = (i - (i / C4) * C4) * 4;
+                const f4v s4 = *reinterpret_cast<const f4v*>(tsc + (size_t)b * C + c4);
+                const f4v h4 = *reinterpret_cast<const f4v*>(tsh + (size_t)b * C + c4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float yv = fmaf(v[k][e], s4[e], h4[e]);
+                    v[k][e] = yv * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * yv));
+                }
+            }
+            *reinterpret_cast<f4v*>(ub + 4 * i) = v[k];
+        }
+    }
+    __syncthreads();
+    bool bad = false;
+    const int CI = C / 8;
+    const int nq = ROWS * 2 * SW * CI;
+    for (int i = threadIdx.x; i < nq; i += 256) {
+        const int q = i % CI, r2 = i / CI;
+        const int oxl = r2 % (2 * SW), ry = r2 / (2 * SW);
+        const int ox = 2 * seg * SW + oxl;
+        const int oy = band * ROWS + ry;
+        float sy = 0.5f * ((float)oy + 0.5f) - 0.5f;
+        sy = sy < 0.f ? 0.f : sy;
+        const int y0 = (int)sy;
+        const int y1 = y0 + (y0 < H - 1 ? 1 : 0);
+        const float ly1 = sy - (float)y0, ly0 = 1.f - ly1;
+        float sx = 0.5f * ((float)ox + 0.5f) - 0.5f;
+        sx = sx < 0.f ? 0.f : sx;
+        const int x0 = (int)sx, x1 = x0 + (x0 < W - 1 ? 1 : 0);
+        const float lx1 = sx - (float)x0, lx0 = 1.f - lx1;
+        const float* r0 = ub + (y0 - ys0) * SC2 * C + 8 * q;
+        const float* r1 = ub + (y1 - ys0) * SC2 * C + 8 * q;
+        const int c0 = (x0 - xs0) * C, c1 = (x1 - xs0) * C;
+        const size_t pix = ((size_t)b * 2 * H + oy) * 2 * W + ox;
+        uint2 hi[2], lo[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f4v va = *reinterpret_cast<const f4v*>(r0 + c0 + 4 * h);
+            const f4v vb = *reinterpret_cast<const f4v*>(r0 + c1 + 4 * h);
+            const f4v vc = *reinterpret_cast<const f4v*>(r1 + c0 + 4 * h);
+            const f4v vd = *reinterpret_cast<const f4v*>(r1 + c1 + 4 * h);
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o[e] = fmaf(ly1, fmaf(lx1, vd[e], lx0 * vc[e]), ly0 * fmaf(lx1, vb[e], lx0 * va[e]));
+                bad = bad || h2_bad(o[e]);
+            }
+            split4x(make_float4(o[0], o[1], o[2], o[3]), hi[h], lo[h], bf != 0);
+        }
+        char* gp = y + pix * C * 4 + 32 * (size_t)q;
+        *reinterpret_cast<uint4*>(gp) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
+        *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo[0].x, lo[0].y, lo[1].x, lo[1].y);
+    }
+    h2_flag(ovf, bad && !bf);
+}
+
 // LayerNorm over rows of width Wd (+ optional FiLM h*(1+gamma)+beta), one wave per row.
 // gamma = gb[row][i] (+ gt[i]), beta = gb[row][Wd + i] (+ gt[Wd + i]): gt is one row broadcast over
 // all rows (the prior DDIM's per-step time half of the FiLM projection, prior.hip).
@@ -710,6 +804,16 @@ extern "C" int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, in
 namespace tcx {
 // the banded upsample covers this source shape (its band of source rows fits the LDS)
 bool upsample_band_ok(int H, int W, int C) { return H % 2 == 0 && W * C <= UB_MAXWC && C % 8 == 0; }
+// source columns per segment of the column-segmented band (0: none fits): the widest power of two
+// dividing W whose segment + 2 halo columns fit the LDS band
+int upsample_seg_width(int H, int W, int C) {
+    if (H % 2 != 0 || C % 8 != 0) return 0;
+    for (int sw = 64; sw >= 8; sw /= 2)
+        if (W % sw == 0 && sw < W && (sw + 2) * C <= UB_MAXWC) return sw;
+    return 0;
+}
+// the upsample can take the GroupNorm+SiLU tables of its source (band or segmented band)
+bool upsample_fused_ok(int H, int W, int C) { return upsample_band_ok(H, W, C) || upsample_seg_width(H, W, C) > 0; }
 
 // h2 (f16x3) or bf16 (bf != 0) records out of the upsample / GroupNorm apply (unet.hip, and the C ABI below)
 int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
@@ -733,6 +837,27 @@ int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const fl
         }
         hipLaunchKernelGGL(k, dim3(Bt * (2 * H / rows)), dim3(256), shm, st, x, (char*)y, H, W, C, scale, shift, ovf, bf);
         return check_launch("tcx_upsample2x_h2(band)");
+    }
+    static const bool seg_on = [] {  // TCX_UPSEG=0: the g8 form at wide rows (A/B)
+        const char* e = getenv("TCX_UPSEG");
+        return !(e && e[0] == '0');
+    }();
+    if (const int sw = seg_on ? upsample_seg_width(H, W, C) : 0) {  // config 5's wide rows
+        constexpr int rows = 4;
+        const size_t shm = (size_t)(rows / 2 + 2) * (sw + 2) * C * sizeof(float);
+        const auto k = &k_upsample2x_bandseg<4>;
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(4 * UB_MAXWC * sizeof(float))) != hipSuccess) {
+                set_error("tcx_upsample2x_h2: cannot enable %zu B of dynamic LDS", 4 * UB_MAXWC * sizeof(float));
+                return TCX_EHIP;
+            }
+            attr = true;
+        }
+        hipLaunchKernelGGL(k, dim3(Bt * (2 * H / rows) * (W / sw)), dim3(256), shm, st, x, (char*)y, H, W, C, sw, scale,
+                           shift, ovf, bf);
+        return check_launch("tcx_upsample2x_h2(segmented band)");
     }
     const dim3 grid(Bt * 2 * H, cdiv(2 * W * (C / 8), UPG * 256));
     hipLaunchKernelGGL(k_upsample2x_g8, grid, dim3(256), 0, st, x, (char*)y, H, W, C, scale, shift, ovf, bf);

@@ -13,11 +13,12 @@
 //              and the sampler update (EM / Heun stage / final x0 projection) in one pass;
 //              noise either host-injected or Philox4x32-10 in-kernel.
 #include "common.hpp"
+#include "h2.hpp"
 
 namespace tcx {
 bool conv3g_covers(int H, int W, int Cin, int cout_pad, bool bf);  // conv3g.hip
 // h2 / bf16 record writers (norm.hip, attention_split.hip): bf != 0 writes bf16 halves
-bool upsample_band_ok(int H, int W, int C);
+bool upsample_fused_ok(int H, int W, int C);  // norm.hip: band / segmented band
 int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
                   unsigned* ovf, int bf, hipStream_t st);
 int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
@@ -212,11 +213,19 @@ __global__ __launch_bounds__(256) void k_fold_bias(CondTab ct, int C0, int B, in
 // several blocks per CU overlap their load/compute/store phases) and written as one contiguous
 // block; per-channel {sum, sumsq} (fp64) of the tile feed the following GroupNorm.
 // grid (HW/64, Bt); block 256 = 64 pixels x 4 channel quarters; needs HW % 128 == 0, C0 % 16 == 0.
+// MODE 0: fp32 output + GroupNorm partials per 64-pixel tile (the fp32 path / the f16x3 prologue form).
+// MODE 2 (split path, round 3): silu(GroupNorm_0(conv)) written as the h2 / bf16 record of
+//   down1.net.3's input (scale/shift tables of tcx_gn_finalize over the statistics of k_first_acf /
+//   k_first_gnsum below; SiLU as the conv prologues: y rcp(1 + exp2(-y log2 e))), so that conv runs
+//   without a prologue and the fp32 tensor is never written or re-read.
 constexpr int FIRST_PX = 64;
+template <int MODE>
 __global__ __launch_bounds__(256) void k_conv_first(const float* __restrict__ x, int bmod, int H, int W, int C0,
                                                     const float* __restrict__ w0, int kpad,
                                                     const float* __restrict__ bias_b, float* __restrict__ y,
-                                                    double* __restrict__ gn, CondTab ct, int Bimg, int cfg) {
+                                                    double* __restrict__ gn, CondTab ct, int Bimg, int cfg,
+                                                    const float* __restrict__ tsc, const float* __restrict__ tsh,
+                                                    unsigned* ovf, int bf) {
     extern __shared__ __attribute__((aligned(16))) float fs[];  // tile[64][C0+4] | w[9][C0] | red[4][C0][2] (dbl)
     const int LD = C0 + 4;
     float* tile = fs;
@@ -224,69 +233,213 @@ __global__ __launch_bounds__(256) void k_conv_first(const float* __restrict__ x,
     double* red = reinterpret_cast<double*>(w + 9 * C0);
     const int HW = H * W;
     const int b = blockIdx.y;
-    const int p0 = blockIdx.x * FIRST_PX;
     const int tid = threadIdx.x;
     for (int i = tid; i < 9 * C0; i += 256) {
         const int co = i / 9, k = i - (i / 9) * 9;  // w0 packed [co][kpad] with k = tap (Cin = 1)
         w[k * C0 + co] = w0[(size_t)co * kpad + k];
     }
-    __syncthreads();
+    float* const tab = reinterpret_cast<float*>(red);  // MODE 2: this image's scale | shift (LDS)
+    if constexpr (MODE == 2) {
+        for (int c = tid; c < C0; c += 256) {
+            tab[c] = tsc[(size_t)b * C0 + c];
+            tab[C0 + c] = tsh[(size_t)b * C0 + c];
+        }
+    }
     const int px = tid & (FIRST_PX - 1), qtr = tid >> 6;
-    const int p = p0 + px;
-    const int yy = p / W, xx = p - (p / W) * W;
     const float* xb = x + (size_t)(b % bmod) * HW;
-    float xv[9];
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) xv[dy * 3 + dx] = xb[wrap_idx(yy + dy - 1, H) * W + wrap_idx(xx + dx - 1, W)];
     const int cq = C0 / 4;
     const float* bb = ct.bias_img ? cond_bias_row(ct, b, Bimg, cfg, C0) : bias_b + (size_t)b * C0;
-    for (int c = qtr * cq; c < (qtr + 1) * cq; c += 4) {
-        float4 a = *reinterpret_cast<const float4*>(bb + c);
+    constexpr int NT = 1;
+    double as[2] = {0.0, 0.0}, aq[2] = {0.0, 0.0};  // this thread's (quarter, c) sums
+    for (int tt = 0; tt < NT; ++tt) {
+        const int p0 = (blockIdx.x * NT + tt) * FIRST_PX;
+        __syncthreads();  // w staged / the previous tile consumed
+        const int p = p0 + px;
+        const int yy = p / W, xx = p - (p / W) * W;
+        float xv[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const float4 wk = *reinterpret_cast<const float4*>(&w[k * C0 + c]);  // broadcast read
-            a.x = fmaf(wk.x, xv[k], a.x);
-            a.y = fmaf(wk.y, xv[k], a.y);
-            a.z = fmaf(wk.z, xv[k], a.z);
-            a.w = fmaf(wk.w, xv[k], a.w);
-        }
-        *reinterpret_cast<float4*>(&tile[px * LD + c]) = a;
-    }
-    __syncthreads();
-    float* dst = y + ((size_t)b * HW + p0) * C0;
-    const int C4 = C0 / 4;
-    for (int i = tid; i < FIRST_PX * C4; i += 256) {
-        const int r = i / C4, c = (i - (i / C4) * C4) * 4;
-        *reinterpret_cast<float4*>(dst + (size_t)i * 4) = *reinterpret_cast<const float4*>(&tile[r * LD + c]);
-    }
-    if (gn) {  // 128-pixel GN split = 2 tiles: tile t contributes to split blockIdx.x / 2 (atomic-free:
-               // each half-split is written to its own slot and summed by the consumer's fold)
-        const int nsplit = HW / FIRST_PX;
-        for (int i = tid; i < 4 * C0; i += 256) {
-            const int c = i % C0, part = i / C0;  // 4 row quarters of 16 pixels
-            double s = 0.0, q = 0.0;
-            for (int r = part * 16; r < part * 16 + 16; ++r) {
-                const double v = tile[r * LD + c];
-                s += v;
-                q += v * v;
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) xv[dy * 3 + dx] = xb[wrap_idx(yy + dy - 1, H) * W + wrap_idx(xx + dx - 1, W)];
+        for (int c = qtr * cq; c < (qtr + 1) * cq; c += 4) {
+            float4 a = *reinterpret_cast<const float4*>(bb + c);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const float4 wk = *reinterpret_cast<const float4*>(&w[k * C0 + c]);  // broadcast read
+                a.x = fmaf(wk.x, xv[k], a.x);
+                a.y = fmaf(wk.y, xv[k], a.y);
+                a.z = fmaf(wk.z, xv[k], a.z);
+                a.w = fmaf(wk.w, xv[k], a.w);
             }
-            red[(part * C0 + c) * 2] = s;
-            red[(part * C0 + c) * 2 + 1] = q;
+            *reinterpret_cast<float4*>(&tile[px * LD + c]) = a;
         }
         __syncthreads();
-        for (int c = tid; c < C0; c += 256) {
-            double s = 0.0, q = 0.0;
-#pragma unroll
-            for (int part = 0; part < 4; ++part) {
-                s += red[(part * C0 + c) * 2];
-                q += red[(part * C0 + c) * 2 + 1];
+        if constexpr (MODE == 0) {
+            float* dst = y + ((size_t)b * HW + p0) * C0;
+            const int C4 = C0 / 4;
+            for (int i = tid; i < FIRST_PX * C4; i += 256) {
+                const int r = i / C4, c = (i - (i / C4) * C4) * 4;
+                *reinterpret_cast<float4*>(dst + (size_t)i * 4) = *reinterpret_cast<const float4*>(&tile[r * LD + c]);
             }
-            double* g = gn + (((size_t)b * nsplit + blockIdx.x) * C0 + c) * 2;
-            g[0] = s;
-            g[1] = q;
+        } else if constexpr (MODE == 2) {
+            // 8-channel groups, channel fastest: consecutive threads write consecutive 32-B records
+            char* dst = reinterpret_cast<char*>(y) + ((size_t)b * HW + p0) * C0 * 4;
+            const int C8 = C0 / 8;
+            const float* s8 = tab;
+            const float* h8p = tab + C0;
+            bool bad = false;
+            for (int i = tid; i < FIRST_PX * C8; i += 256) {
+                const int r = i / C8, g = i - (i / C8) * C8;
+                const float4 v0 = *reinterpret_cast<const float4*>(&tile[r * LD + 8 * g]);
+                const float4 v1 = *reinterpret_cast<const float4*>(&tile[r * LD + 8 * g + 4]);
+                const float4 s0 = *reinterpret_cast<const float4*>(s8 + 8 * g);
+                const float4 s1 = *reinterpret_cast<const float4*>(s8 + 8 * g + 4);
+                const float4 t0 = *reinterpret_cast<const float4*>(h8p + 8 * g);
+                const float4 t1 = *reinterpret_cast<const float4*>(h8p + 8 * g + 4);
+                auto sl = [](float v, float sc, float sh) {
+                    const float q = fmaf(v, sc, sh);
+                    return q * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * q));
+                };
+                const float4 a0 = make_float4(sl(v0.x, s0.x, t0.x), sl(v0.y, s0.y, t0.y), sl(v0.z, s0.z, t0.z),
+                                              sl(v0.w, s0.w, t0.w));
+                const float4 a1 = make_float4(sl(v1.x, s1.x, t1.x), sl(v1.y, s1.y, t1.y), sl(v1.z, s1.z, t1.z),
+                                              sl(v1.w, s1.w, t1.w));
+                uint2 hi0, lo0, hi1, lo1;
+                split4x(a0, hi0, lo0, bf != 0);
+                split4x(a1, hi1, lo1, bf != 0);
+                if (!bf)
+                    bad = bad || h2_bad(a0.x) || h2_bad(a0.y) || h2_bad(a0.z) || h2_bad(a0.w) || h2_bad(a1.x) ||
+                          h2_bad(a1.y) || h2_bad(a1.z) || h2_bad(a1.w);
+                char* gp = dst + (size_t)r * C0 * 4 + 32 * g;
+                *reinterpret_cast<uint4*>(gp) = make_uint4(hi0.x, hi0.y, hi1.x, hi1.y);
+                *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo0.x, lo0.y, lo1.x, lo1.y);
+            }
+            h2_flag(ovf, bad);
         }
+        if constexpr (MODE != 2) {
+            if (gn) {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int i = tid + 256 * e;
+                    if (i < 4 * C0) {
+                        const int c = i % C0, part = i / C0;  // 4 row quarters of 16 pixels
+                        double s = 0.0, q = 0.0;
+                        for (int r = part * 16; r < part * 16 + 16; ++r) {
+                            const double v = tile[r * LD + c];
+                            s += v;
+                            q += v * v;
+                        }
+                        as[e] += s;
+                        aq[e] += q;
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (MODE != 2) {
+        if (gn) {  // 128-pixel GN split = 2 tiles (each half-split in its own slot, summed by the
+                   // consumer's fold)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int i = tid + 256 * e;
+                if (i < 4 * C0) {
+                    red[i * 2] = as[e];
+                    red[i * 2 + 1] = aq[e];
+                }
+            }
+            __syncthreads();
+            const int nsplit = HW / (FIRST_PX * NT);
+            for (int c = tid; c < C0; c += 256) {
+                double s = 0.0, q = 0.0;
+#pragma unroll
+                for (int part = 0; part < 4; ++part) {
+                    s += red[(part * C0 + c) * 2];
+                    q += red[(part * C0 + c) * 2 + 1];
+                }
+                double* g = gn + (((size_t)b * nsplit + blockIdx.x) * C0 + c) * 2;
+                g[0] = s;
+                g[1] = q;
+            }
+        }
+    }
+}
+
+// GroupNorm statistics of the first conv without evaluating it (split path, round 3).  The conv is
+// out[p][c] = bias[c] + sum_k w[c][k] x[p + o_k] over the 9 circular taps o_k of ONE input channel, so
+//   sum_p out   = HW bias + (sum_k w_k) S,                         S = sum_q x[q]
+//   sum_p out^2 = HW bias^2 + 2 bias (sum_k w_k) S + sum_{k,l} w_k w_l R(o_l - o_k),  R(d) = sum_q x[q] x[q + d]
+// (circular shifts preserve both sums): per image, S and the 25 circular autocorrelations R(d),
+// d in [-2, 2]^2, then 96 channel sums from them.  Everything in fp64 from the fp32 inputs.
+// k_first_acf: grid (HW / chunk, Bt) -> part[b][chunk][26] (chunk = 4096 pixels where HW allows: the
+// 26 block reductions cost more than the sums at 1024); k_first_gnsum: grid Bt -> the [Bt][1][C0][2]
+// GroupNorm partials tcx_gn_finalize reads (one split).
+constexpr int FIRST_ACF_PX = 1024;  // smallest chunk (HW % 1024 == 0)
+__global__ __launch_bounds__(256) void k_first_acf(const float* __restrict__ x, int bmod, int H, int W, int chunk,
+                                                   double* __restrict__ part) {
+    __shared__ double wred[4][26];
+    const int b = blockIdx.y, HW = H * W;
+    const float* xb = x + (size_t)(b % bmod) * HW;
+    double acc[26];
+#pragma unroll
+    for (int k = 0; k < 26; ++k) acc[k] = 0.0;
+    for (int p = blockIdx.x * chunk + threadIdx.x; p < (blockIdx.x + 1) * chunk; p += 256) {
+        const int yy = p / W, xx = p - (p / W) * W;
+        const double v = xb[p];
+        acc[25] += v;
+#pragma unroll
+        for (int dy = -2; dy <= 2; ++dy) {
+            const float* row = xb + wrap_idx(yy + dy, H) * W;
+#pragma unroll
+            for (int dx = -2; dx <= 2; ++dx) acc[(dy + 2) * 5 + dx + 2] = fma(v, (double)row[wrap_idx(xx + dx, W)], acc[(dy + 2) * 5 + dx + 2]);
+        }
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 26; ++k) {
+        double t = acc[k];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+        if (lane == 0) wred[wv][k] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 26) {
+        const int k = threadIdx.x;
+        part[((size_t)b * gridDim.x + blockIdx.x) * 26 + k] = ((wred[0][k] + wred[1][k]) + wred[2][k]) + wred[3][k];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_first_gnsum(const double* __restrict__ part, int nchunk, int HW, int C0,
+                                                     const float* __restrict__ w0, int kpad,
+                                                     const float* __restrict__ bias_b, CondTab ct, int Bimg, int cfg,
+                                                     double* __restrict__ gn) {
+    __shared__ double a[26];
+    const int b = blockIdx.x;
+    if (threadIdx.x < 26) {
+        double t = 0.0;
+        for (int j = 0; j < nchunk; ++j) t += part[((size_t)b * nchunk + j) * 26 + threadIdx.x];
+        a[threadIdx.x] = t;
+    }
+    __syncthreads();
+    const float* bb = ct.bias_img ? cond_bias_row(ct, b, Bimg, cfg, C0) : bias_b + (size_t)b * C0;
+    for (int c = threadIdx.x; c < C0; c += 256) {
+        double w[9], ws = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            w[k] = w0[(size_t)c * kpad + k];
+            ws += w[k];
+        }
+        const double bi = bb[c], S = a[25];
+        double q = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+#pragma unroll
+            for (int l = 0; l < 9; ++l) {
+                const int dy = l / 3 - k / 3, dx = l % 3 - k % 3;
+                q = fma(w[k] * w[l], a[(dy + 2) * 5 + dx + 2], q);
+            }
+        double* g = gn + ((size_t)b * C0 + c) * 2;
+        g[0] = (double)HW * bi + ws * S;
+        g[1] = (double)HW * bi * bi + 2.0 * bi * ws * S + q;
     }
 }
 
@@ -744,12 +897,25 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         const char* e = getenv("TCX_GN_PRO");
         return !(e && e[0] == '0');
     }();
+    // bf16 at rows of 64/128/256 pixels: the h2-source conv there is the LDS-DMA k_conv3lb, which has no
+    // prologue form; an apply pass + k_conv3lb beats k_conv3g's register-staged prologue form, whose
+    // transform (7 halo units per thread at 256-px rows, 3x redundant over the tiles of a row) is not
+    // hidden behind a bf16 tap's 6 MFMAs (TCX_BF_PRO=1 keeps the prologue: A/B)
+    static const bool bf_pro = [] {
+        const char* e = getenv("TCX_BF_PRO");
+        return e && e[0] == '1';
+    }();
+    auto pro_ok = [&](const tcx_conv& cv, int h, int w, int cin) {
+        const bool bf = net->precision == 2;
+        if (!cv.whf || !conv3g_covers(h, w, cin, cv.cout_pad, bf)) return false;
+        return !(bf && !bf_pro && (w == 64 || w == 128 || w == 256));
+    };
     if (net->precision >= 1 && gn_pro) {
-        pro[0] = net->down1_1.whf && conv3g_covers(H, W, C, net->down1_1.cout_pad, net->precision == 2);
-        pro[2] = net->down2_1.whf && conv3g_covers(H1, W1, C2, net->down2_1.cout_pad, net->precision == 2);
-        pro[7] = net->up2_1.whf && conv3g_covers(H1, W1, C, net->up2_1.cout_pad, net->precision == 2);
-        pro[9] = net->up1_1.whf && conv3g_covers(H, W, C, net->up1_1.cout_pad, net->precision == 2);
-        pro[4] = net->mid_1.whf && conv3g_covers(H2, W2, C2, net->mid_1.cout_pad, net->precision == 2);  // mid.net.1 -> mid.net.3
+        pro[0] = pro_ok(net->down1_1, H, W, C);
+        pro[2] = pro_ok(net->down2_1, H1, W1, C2);
+        pro[7] = pro_ok(net->up2_1, H1, W1, C);
+        pro[9] = pro_ok(net->up1_1, H, W, C);
+        pro[4] = pro_ok(net->mid_1, H2, W2, C2);  // mid.net.1 -> mid.net.3
     }
     auto SC = [&](int i) -> const float* { return pro[i] ? P.sc(i) : nullptr; };
     auto SH = [&](int i) -> const float* { return pro[i] ? P.sh(i) : nullptr; };
@@ -764,15 +930,42 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         return tcx_gn_apply_tab(y, y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, st);
     };
     // down1 (first conv: x_t channel only, maps folded into bias0; the conv bias is inside bias0)
+    // Split path (round 3): statistics pass + a second pass that recomputes the conv and writes
+    // silu(GroupNorm_0(.)) as down1.net.3's h2 / bf16 record (k_first_acf + k_first_gnsum, k_conv_first MODE 2), so norm 0 needs
+    // neither a prologue nor an apply pass and the fp32 tensor is never written (TCX_FIRST_FUSE=0: A/B)
+    static const bool first_fuse = [] {
+        const char* e = getenv("TCX_FIRST_FUSE");
+        return !(e && e[0] == '0');
+    }();
+    bool first_fused = false;
     {
         const tcx_conv& c0 = net->down1_0;
-        if ((H * W) % FIRST_PX == 0 && C % 16 == 0 && c0.kpad == 32) {
+        if ((H * W) % FIRST_PX == 0 && C % 16 == 0 && C <= 128 && c0.kpad == 32) {
             const size_t shm = ((size_t)FIRST_PX * (C + 4) + 9 * (size_t)C) * sizeof(float) +
                                8 * (size_t)C * sizeof(double);
-            hipLaunchKernelGGL(k_conv_first, dim3(H * W / FIRST_PX, Bt), dim3(256), shm, st, x, B, H, W, C, c0.w,
-                               c0.kpad, P.bias0, P.a64, gn, ct, B, cfg);
-            TCX_TRY(check_launch("k_conv_first"));
-            ns = H * W / FIRST_PX;
+            if (h2.on && first_fuse && (H * W) % FIRST_ACF_PX == 0 && C % 8 == 0) {
+                const int chunk = (H * W) % 4096 == 0 ? 4096 : FIRST_ACF_PX;
+                const int nchunk = H * W / chunk;
+                double* acf = gn + (size_t)Bt * C * 2;  // the autocorrelation partials, past the [Bt][1][C][2] sums
+                hipLaunchKernelGGL(k_first_acf, dim3(nchunk, Bt), dim3(256), 0, st, x, B, H, W, chunk, acf);
+                TCX_TRY(check_launch("k_first_acf"));
+                hipLaunchKernelGGL(k_first_gnsum, dim3(Bt), dim3(256), 0, st, acf, nchunk, H * W, C, c0.w, c0.kpad,
+                                   P.bias0, ct, B, cfg, gn);
+                TCX_TRY(check_launch("k_first_gnsum"));
+                ns = 1;
+                TCX_TRY(gn_tab(net, P, 0, P.P0, C, gn, ns, st));
+                hipLaunchKernelGGL(k_conv_first<2>, dim3(H * W / FIRST_PX, Bt), dim3(256), shm, st, x, B, H, W, C,
+                                   c0.w, c0.kpad, P.bias0, P.a64, nullptr, ct, B, cfg, P.sc(0), P.sh(0), h2.ovf,
+                                   h2.bf ? 1 : 0);
+                TCX_TRY(check_launch("k_conv_first (GroupNorm+SiLU records)"));
+                first_fused = true;
+                pro[0] = false;
+            } else {
+                hipLaunchKernelGGL(k_conv_first<0>, dim3(H * W / FIRST_PX, Bt), dim3(256), shm, st, x, B, H, W, C,
+                                   c0.w, c0.kpad, P.bias0, P.a64, gn, ct, B, cfg, nullptr, nullptr, nullptr, 0);
+                TCX_TRY(check_launch("k_conv_first"));
+                ns = H * W / FIRST_PX;
+            }
         } else {
             if (ct.bias_img) {
                 hipLaunchKernelGGL(k_fold_bias, dim3(cdiv(Bt * C, 256)), dim3(256), 0, st, ct, C, B, cfg, Bt, P.bias0);
@@ -784,7 +977,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
             TCX_TRY(tcx_gn_partials(P.a64, Bt, H * W, C, ns, gn, st));
         }
     }
-    TCX_TRY(norm(0, P.a64, P.P0, C));
+    if (!first_fused) TCX_TRY(norm(0, P.a64, P.P0, C));
     TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.h1, gn, &ns, st,
                     SC(0), SH(0), nullptr, nullptr, h2));
     TCX_TRY(norm(1, P.h1, P.P0, C));  // h1 stays raw; its two consumers apply table 1
@@ -851,7 +1044,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // upsample applies the GroupNorm+SiLU once per source element while staging (no apply pass);
     // fp32 path: the apply pass in place, then the plain upsample
     // (r03_o, one lane, alternating: 72.7 vs 72.3 images/s against the separate apply pass)
-    if (h2.on && upsample_band_ok(H1, W1, C)) {
+    if (h2.on && upsample_fused_ok(H1, W1, C)) {
         TCX_TRY(gn_tab(net, P, 8, P.P1, C, gn, ns, st));
         TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, P.sc(8), P.sh(8), h2.ovf, h2.bf, st));
     } else {
