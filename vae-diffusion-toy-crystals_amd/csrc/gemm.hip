@@ -279,6 +279,7 @@ struct WgParams {
     int nsplit, cps;  // splits, 32-pixel chunks per split
     int nkblk, ncblk;
     const float* comb;  // k_wgrad_h2: 1 / (s_x s_dy), the operands' power-of-two scales
+    unsigned bx1, bx2, bdy;  // k_wgrad_h2: byte extents of x1, x2, dy (raw-buffer loads, zero past the end)
 };
 
 // ASC: scalar im2col gather (Cin % 4 != 0); BSC: scalar dY loads (Cout % 4 != 0)
@@ -426,7 +427,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgParams p) {
 // (hi*lo, lo*hi, hi*hi) instead of eight fp32 ones.  Same tiling, split plan and fixed-order reduce as
 // k_wgrad; the partials are acc * comb.  Needs C1, C2, Cout % 8 == 0 (whole 4-channel quads of a record).
 template <int NT>
-__global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
+__global__ __launch_bounds__(256, 2) void k_wgrad_h2_r2(WgParams p) {
     constexpr int BN = 32 * NT;
     constexpr int RS = 40;  // halves per LDS row: 32 pixels + 8 pad (80 B)
     __shared__ __attribute__((aligned(16))) _Float16 Ah[2][GBM * RS];
@@ -556,6 +557,169 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
         }
     }
 }
+
+// f16x3 weight gradient, round 3: same tiles, split plan, partials and fixed-order reduce as
+// k_wgrad_h2_r2 above, with the operands staged as whole 16-B record pieces and transposed by the LDS
+// read instead of the store.  PMC of the round-2 kernel on the score step (profiles/r03_aa_*): TD
+// (vector-memory return path) busy 88 %, MFMA busy 14 %, 315 M L1 accesses per launch — its 8-byte
+// quad loads touch one cache line per lane — and 56 2-byte LDS stores per thread per chunk.
+// Here a thread loads 16-B pieces (the hi or lo half of one 8-channel group of one pixel's record:
+// 32 consecutive lanes read 512 contiguous bytes), stores each with ONE ds_write_b128 into a
+// [pixel][hi plane 16 pieces | lo plane 16 pieces] image (512-B rows, piece o of row r at o ^ 4 (r & 3)),
+// and the MFMA operands (k or co on the lane, 8 consecutive pixels) come from ds_read_b64_tr_b16:
+// lane 4q + p of a 16-lane group addresses pixel row q, columns 4p .. 4p + 3 and receives one column
+// of the 4 rows.  A 32-lane half reads 4 rows x 4 pieces of one plane; the swizzle puts those 16
+// pieces on 16 distinct 16-B bank groups (row stride 512 B = 0 mod 256).
+template <int NT>
+__global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
+    constexpr int BN = 32 * NT;
+    constexpr int ROWB = 512;                 // bytes per pixel row of either image
+    constexpr int AB = 32 * ROWB;             // A image: 32 pixels x 128 k (hi | lo planes)
+    constexpr int BB = 32 * ROWB;             // B image: 32 pixels x BN co (4 NT of 16 pieces used)
+    constexpr int STG = AB + BB;
+    constexpr int OB = 4 * NT;                // co octets per plane
+    extern __shared__ __attribute__((aligned(16))) char wsm[];
+    const int split = blockIdx.y;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kblk = tile / p.ncblk, cblk = tile - (tile / p.ncblk) * p.ncblk;
+    const int k0 = kblk * GBM, c0 = cblk * BN;
+    const int tid = threadIdx.x;
+    const int chunk0 = split * p.cps;
+    const int nch_all = (p.M + 31) / 32;
+    const int chunk1 = min(chunk0 + p.cps, nch_all);
+    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x1), 0, (int)p.bx1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r2 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x2 ? p.x2 : p.x1), 0, (int)(p.x2 ? p.bx2 : p.bx1), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.dy), 0, (int)p.bdy, 0x00020000);
+    constexpr int OOB = (int)0x80000000u;
+
+    // A pieces of this thread: idx = tid + 256 i -> pixel row tid / 32 + 8 i, logical piece lp = tid % 32
+    // (plane lp / 16, octet lp % 16: k = k0 + 8 octet, one tap and one source per octet)
+    const int lp = tid & 31, apl = lp >> 4, aoc = lp & 15;
+    const int ak = k0 + 8 * aoc;
+    const bool akv = ak < p.K;
+    const int akk = akv ? ak : 0;
+    const int atap = akk / p.Cin, aci = akk - (akk / p.Cin) * p.Cin;
+    const int ady = atap / p.ks, adx = atap - (atap / p.ks) * p.ks;
+    const bool asrc1 = aci < p.C1;
+    const int aC = asrc1 ? p.C1 : p.C2;
+    const int aoff = (asrc1 ? aci : aci - p.C1) * 4 + 16 * apl;  // byte offset within the pixel record
+    float4 ra[4], rb[NT];
+    auto load = [&](int c) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = (tid >> 5) + 8 * i;
+            const int m = c * 32 + row;
+            const bool mv = m < p.M;
+            const int mm = mv ? m : 0;
+            const int b = mm / p.HoWo, r = mm - (mm / p.HoWo) * p.HoWo;
+            const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+            int yy = oy * p.stride - p.pad + ady, xx = ox * p.stride - p.pad + adx;
+            bool ok = mv && akv;
+            if (p.circular) {
+                yy = wrap_idx(yy, p.H);
+                xx = wrap_idx(xx, p.W);
+            } else {
+                ok = ok && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
+            }
+            const int off = ok ? ((b * p.H + yy) * p.W + xx) * aC * 4 + aoff : OOB;
+            ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc1 ? r1 : r2, off, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {  // B pieces: idx = tid + 256 i -> row idx / (2 OB), piece idx % (2 OB)
+            const int idx = tid + 256 * i;
+            const int row = idx / (2 * OB), q = idx - row * (2 * OB);
+            const int pl = q / OB, oc = q - pl * OB;
+            const int m = c * 32 + row;
+            const int co = c0 + 8 * oc;
+            const bool ok = m < p.M && co < p.Cout;
+            const int off = ok ? (m * p.Cout + co) * 4 + 16 * pl : OOB;
+            rb[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0));
+        }
+    };
+    auto store = [&](int buf) {
+        char* A = wsm + buf * STG;
+        char* B = A + AB;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = (tid >> 5) + 8 * i;
+            *reinterpret_cast<float4*>(A + row * ROWB + 16 * (16 * apl + (aoc ^ (4 * (row & 3))))) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            const int idx = tid + 256 * i;
+            const int row = idx / (2 * OB), q = idx - row * (2 * OB);
+            const int pl = q / OB, oc = q - pl * OB;
+            *reinterpret_cast<float4*>(B + row * ROWB + 16 * (16 * pl + (oc ^ (4 * (row & 3))))) = rb[i];
+        }
+    };
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
+    const int lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
+    // tr-read address of this lane: group g = lane / 16, q = (lane / 4) % 4, pp = lane % 4; operand
+    // rows (pixels) 16 s + 8 (g >> 1) + 4 r + q, columns 16 (g & 1) + 4 pp of the 32-column tile
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int trow = 8 * (g >> 1) + q;                // + 16 s + 4 r (both keep row & 3 == q)
+    const int tpc = 2 * (g & 1) + (pp >> 1);           // piece within the tile's 4-piece group
+    const int tb = trow * ROWB + 8 * (pp & 1);
+    const int apc = 16 * ((4 * wv + tpc) ^ (4 * q));   // A: octet 4 wv + tpc of the hi plane
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    auto tr = [&](const char* base) {
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(base));
+    };
+    auto frag8 = [&](const char* img, int pc, int s, int plane) -> h8 {
+        const char* b0 = img + tb + 16 * s * ROWB + pc + 256 * plane;
+        const v4s u0 = tr(b0), u1 = tr(b0 + 4 * ROWB);
+        typedef short v8s __attribute__((ext_vector_type(8)));
+        const v8s u = __builtin_shufflevector(u0, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+        return __builtin_bit_cast(h8, u);
+    };
+    if (chunk0 < chunk1) {
+        load(chunk0);
+        store(0);
+    }
+    __syncthreads();
+    for (int c = chunk0; c < chunk1; ++c) {
+        const int cur = (c - chunk0) & 1;
+        if (c + 1 < chunk1) load(c + 1);
+        const char* A = wsm + cur * STG;
+        const char* B = A + AB;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const h8 fah = frag8(A, apc, s, 0);
+            const h8 fal = frag8(A, apc, s, 1);
+            h8 fbh[NT], fbl[NT];
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int bpc = 16 * ((4 * n + tpc) ^ (4 * q));
+                fbh[n] = frag8(B, bpc, s, 0);
+                fbl[n] = frag8(B, bpc, s, 1);
+            }
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbl[n], acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal, fbh[n], acc[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbh[n], acc[n], 0, 0, 0);
+        }
+        if (c + 1 < chunk1) store(cur ^ 1);
+        __syncthreads();
+    }
+    const float sc = *p.comb;
+    float* dst = p.part + (size_t)split * p.K * p.Cout;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int co = c0 + n * 32 + li;
+        if (co >= p.Cout) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = k0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (k < p.K) dst[(size_t)k * p.Cout + co] = acc[n][r] * sc;
+        }
+    }
+}
+constexpr size_t wgrad_h2_lds_bytes() { return 2 * (size_t)(32 * 512 + 32 * 512); }
 
 // dw[co][ci][ky][kx] = beta * dw + sum_s part[s][k][co], k = (ky*ks + kx)*Cin + ci (fixed order)
 __global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int K, int Cout, int Cin, int ks,
@@ -843,9 +1007,28 @@ extern "C" int tcx_conv_wgrad_h2(const void* x1, const void* x2, int Bt, int H, 
     p.part = reinterpret_cast<float*>(base);
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(p.nkblk * p.ncblk, p.nsplit);
-    if (nt == 3) hipLaunchKernelGGL((k_wgrad_h2<3>), grid, dim3(256), 0, st, p);
-    else if (nt == 2) hipLaunchKernelGGL((k_wgrad_h2<2>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_wgrad_h2<1>), grid, dim3(256), 0, st, p);
+    static const bool r2 = [] {  // TCX_WG_R2=1: the round-2 quad-staged kernel (A/B)
+        const char* e = getenv("TCX_WG_R2");
+        return e && e[0] == '1';
+    }();
+    const size_t in1 = (size_t)Bt * H * W * C1 * 4, in2 = (size_t)Bt * H * W * C2 * 4, ind = (size_t)p.M * Cout * 4;
+    if (!r2 && in1 < (1u << 31) && in2 < (1u << 31) && ind < (1u << 31)) {
+        p.bx1 = (unsigned)in1; p.bx2 = (unsigned)in2; p.bdy = (unsigned)ind;
+        using K = void (*)(WgParams);
+        const K k = nt == 3 ? &k_wgrad_h2<3> : (nt == 2 ? &k_wgrad_h2<2> : &k_wgrad_h2<1>);
+        static bool attr[3] = {};
+        if (!attr[nt - 1]) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)wgrad_h2_lds_bytes()) != hipSuccess) {
+                set_error("tcx_conv_wgrad_h2: cannot enable %zu B of dynamic LDS", wgrad_h2_lds_bytes());
+                return TCX_EHIP;
+            }
+            attr[nt - 1] = true;
+        }
+        hipLaunchKernelGGL(k, grid, dim3(256), wgrad_h2_lds_bytes(), st, p);
+    } else if (nt == 3) hipLaunchKernelGGL((k_wgrad_h2_r2<3>), grid, dim3(256), 0, st, p);
+    else if (nt == 2) hipLaunchKernelGGL((k_wgrad_h2_r2<2>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_wgrad_h2_r2<1>), grid, dim3(256), 0, st, p);
     TCX_TRY(check_launch("tcx_conv_wgrad_h2"));
     const size_t n = (size_t)p.K * Cout;
     const int blocks = (int)std::min<size_t>((n + 255) / 256, 4096);
