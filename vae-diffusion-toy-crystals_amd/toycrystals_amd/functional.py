@@ -109,6 +109,7 @@ _TRAIN_SPLIT = os.environ.get("TCX_TRAIN_SPLIT", "1") != "0"
 
 _SPLIT_MIN_MACS = 4e9  # below this the scaling / conversion launches cost more than the MFMA saves
 _WGRAD_SPLIT = os.environ.get("TCX_WGRAD_FP32", "0") == "0"  # TCX_WGRAD_FP32=1: weight gradients on fp32 MFMA
+_FRAG_TRAIN = os.environ.get("TCX_TRAIN_FRAG", "1") != "0"  # TCX_TRAIN_FRAG=0: training convs without the fragment copy (A/B)
 
 
 def _split_ok(x1, x2, C1, C2, ks, kpad, macs) -> bool:
@@ -150,9 +151,20 @@ def _conv_fwd_split(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride,
     x1h, x2h, xinv = xh
     (wh,), winv = _h2_scaled([wpk])  # h2 of the packed weight (the layout of tcx_pack_conv_weight_h2)
     comb = winv * xinv  # 1 / (s_w s_x), applied by the conv epilogue
-    check(L.tcx_conv2d_h2(ptr(x1h), ptr(x2h), B, 0, H, W, C1, C2, ptr(wh), ptr(comb), ptr(b), ptr(bias_b),
-                          ptr(resid), ptr(y), 0, Cout, cpad, kpad, ks, stride, pad, circular, 0, None, None, st),
-          "tcx_conv2d_h2")
+    # fragment-ordered copy of the weight (round 3): the 3x3 convs then run on the LDS-DMA kernels of
+    # the sampler (k_conv3lg / k_conv3g) and the 4x4/s2 ones on k_conv4s2g instead of the register-
+    # staged k_conv3p / k_conv4s2h (the library picks; a shape they do not cover ignores the copy)
+    wf = None
+    if _FRAG_TRAIN and stride in (1, 2) and ks in (3, 4) and (ks == 3) == (stride == 1):
+        Cin = C1 + C2
+        nb = int(L.tcx_conv_weight_h2_frag_bytes(cpad, Cin) if ks == 3 else L.tcx_conv_weight_h2_frag4_bytes(cpad, Cin))
+        if nb and kpad == ks * ks * Cin:
+            wf = torch.empty(nb // 4, dtype=torch.float32, device=x1.device)
+            pk = L.tcx_pack_conv_weight_h2_frag if ks == 3 else L.tcx_pack_conv_weight_h2_frag4
+            check(pk(ptr(wh), ptr(wf), cpad, kpad, Cin, st), "pack frag")
+    check(L.tcx_conv2d_h2_pro(ptr(x1h), ptr(x2h), B, 0, H, W, C1, C2, ptr(wh), ptr(wf), ptr(comb), ptr(b), ptr(bias_b),
+                              ptr(resid), ptr(y), 0, Cout, cpad, kpad, ks, stride, pad, circular, 0, None, None, None,
+                              None, None, 0, None, st), "tcx_conv2d_h2")
     return y, xh
 
 
