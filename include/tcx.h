@@ -103,6 +103,10 @@ int tcx_gn_finalize(const double* part, int Bt, int HW, int C, int groups, int n
 /* GroupNorm apply from finalize tables: y = x*scale[b][c] + shift[b][c] (+ SiLU); in place OK. */
 int tcx_gn_apply_tab(const float* x, float* y, int Bt, int HW, int C, const float* scale,
                      const float* shift, int silu, void* stream);
+/* The same, also raising *amax (the bit pattern of max |y| as a non-negative float; the caller zeroes
+ * it) so that the split training conv consuming y skips its tcx_absmax pass (functional.py). */
+int tcx_gn_apply_tab_absmax(const float* x, float* y, int Bt, int HW, int C, const float* scale,
+                            const float* shift, int silu, unsigned* amax, void* stream);
 
 /* Bilinear x2 upsample, align_corners=False (nn.Upsample, sde_score_model.py:217,221); optional
  * fused GN+SiLU of the source (scale/shift tables as above, or NULL). */
@@ -473,6 +477,12 @@ size_t tcx_gn_bwd_workspace(int Bt, int HW, int C);
 int tcx_gn_bwd(const float* x, const float* dy, const float* scale, const float* shift, const float* mean,
                const float* rstd, const float* gamma, int Bt, int HW, int C, int groups, int silu, float* dx,
                float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
+/* The same, also raising *amax with max |dx| (as tcx_gn_apply_tab_absmax): dx is the dY operand of the
+ * split data-gradient conv that follows in backward. */
+int tcx_gn_bwd_absmax(const float* x, const float* dy, const float* scale, const float* shift,
+                      const float* mean, const float* rstd, const float* gamma, int Bt, int HW, int C,
+                      int groups, int silu, float* dx, float* dgamma, float* dbeta, unsigned* amax, void* ws,
+                      size_t ws_bytes, void* stream);
 
 /* Adjoint of tcx_upsample2x (nn.Upsample(2, bilinear, align_corners=False), :217-222). */
 int tcx_upsample2x_bwd(const float* dy, float* dx, int Bt, int H, int W, int C, void* stream);

@@ -58,6 +58,21 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 }
 
 __device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
+
+__device__ __forceinline__ float absmax4(const float4 v) {
+    return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+// Block-reduce a per-thread max |value| (>= 0; 256-thread blocks) and raise *amax (the bit pattern of
+// a non-negative float, ordered like the value) with ONE vector-memory atomic per workgroup: same-address
+// atomics serialise in one L2 channel, so a launch must keep them to a few thousand (one per wave of a
+// 16k-workgroup grid cost milliseconds).  Every thread of the block must call it.
+__device__ __forceinline__ void block_amax_publish(float m, unsigned* amax) {
+    __shared__ float red[4];
+    for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
 // SiLU with the hardware exp2 / reciprocal (a few ulp; used in staged prologues)
 
 __device__ __forceinline__ int wrap_idx(int i, int n) {
@@ -65,6 +80,9 @@ __device__ __forceinline__ int wrap_idx(int i, int n) {
     return i >= n ? i - n : i;
 }
 
+__device__ inline void gn_tables_from_csum(int C, int groups, int HW, const float* __restrict__ gamma,
+                                           const float* __restrict__ beta, float eps, float* sc, float* sh,
+                                           double* gstat, const double* csum);
 // Per-channel scale/shift of batch b into LDS from the partials [b][nsplit][C][2].
 // Stage 1: one thread per channel sums its nsplit partials (independent, coalesced loads);
 // stage 2: one thread per group sums its cpg channel totals.  (A group-per-thread loop over
@@ -72,7 +90,6 @@ __device__ __forceinline__ int wrap_idx(int i, int n) {
 __device__ inline void gn_scale_shift(const double* __restrict__ part, int b, int nsplit, int C, int groups, int HW,
                                const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
                                float* sc, float* sh, double* gstat, double* csum) {
-    const int cpg = C / groups;
     const int tid = threadIdx.x;
     const double* pb = part + (size_t)b * nsplit * C * 2;
     for (int c = tid; c < C; c += blockDim.x) {
@@ -87,6 +104,15 @@ __device__ inline void gn_scale_shift(const double* __restrict__ part, int b, in
         csum[2 * c + 1] = q;
     }
     __syncthreads();
+    gn_tables_from_csum(C, groups, HW, gamma, beta, eps, sc, sh, gstat, csum);
+}
+
+// Stages 2-3 of gn_scale_shift: per-channel totals csum[C][2] (LDS) -> group mean / rstd -> tables.
+__device__ inline void gn_tables_from_csum(int C, int groups, int HW, const float* __restrict__ gamma,
+                                           const float* __restrict__ beta, float eps, float* sc, float* sh,
+                                           double* gstat, const double* csum) {
+    const int cpg = C / groups;
+    const int tid = threadIdx.x;
     for (int g = tid; g < groups; g += blockDim.x) {
         double a = 0, q = 0;
         for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
@@ -112,6 +138,14 @@ __device__ inline void gn_scale_shift(const double* __restrict__ part, int b, in
         sh[c] = bt - mean * scl;
     }
     __syncthreads();
+}
+
+// LDS of k_gn_finalize's 1024-thread form: the tables, group stats, channel totals and the per-lane
+// channel sums [lanes][C][2] (lanes = 1024 / C)
+inline size_t gn_finalize_wide_lds_bytes(int C, int groups) {
+    const int lanes = C <= 1024 ? 1024 / C : 1;
+    return (size_t)2 * ((C + 3) & ~3) * sizeof(float) + (size_t)2 * groups * sizeof(double) +
+           (size_t)2 * C * sizeof(double) * (1 + lanes) + 64;
 }
 
 inline size_t gn_fold_lds_bytes(int C, int groups) {

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void k_gn_apply(const float* __restrict__ x, f
 // Streaming GroupNorm apply from per-(b, c) tables: y = act(x * scale + shift).  grid (chunks, Bt).
 __global__ __launch_bounds__(256) void k_gn_apply_tab(const float* __restrict__ x, float* __restrict__ y, int HW, int C,
                                                       const float* __restrict__ tsc, const float* __restrict__ tsh,
-                                                      int silu, int ppb) {
+                                                      int silu, int ppb, unsigned* __restrict__ amax) {
     extern __shared__ __attribute__((aligned(16))) float lsm[];
     float* sc = lsm;
     float* sh = lsm + ((C + 3) & ~3);
@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab(const float* __restrict__ 
     const int n4 = (p1 - p0) * C / 4;
     const int C4 = C / 4;
     int i = threadIdx.x;
+    float m = 0.f;  // max |y| of this thread's elements (only reported when amax is given)
     for (; i + 256 < n4; i += 512) {  // two float4 in flight per thread
         const int c0 = (i % C4) * 4, c1 = ((i + 256) % C4) * 4;
         float4 v0 = *reinterpret_cast<const float4*>(x + base + (size_t)i * 4);
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab(const float* __restrict__ 
         }
         *reinterpret_cast<float4*>(y + base + (size_t)i * 4) = v0;
         *reinterpret_cast<float4*>(y + base + (size_t)(i + 256) * 4) = v1;
+        m = fmaxf(m, fmaxf(absmax4(v0), absmax4(v1)));
     }
     for (; i < n4; i += 256) {
         const int c = (i % C4) * 4;
@@ -138,11 +140,13 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab(const float* __restrict__ 
             v.x = silu_f(v.x); v.y = silu_f(v.y); v.z = silu_f(v.z); v.w = silu_f(v.w);
         }
         *reinterpret_cast<float4*>(y + base + (size_t)i * 4) = v;
+        m = fmaxf(m, absmax4(v));
     }
+    if (amax) block_amax_publish(m, amax);
 }
 
 // One block per image: partials -> per-(b, c) scale/shift tables for a fused GN(+SiLU) prologue.
-__global__ __launch_bounds__(256) void k_gn_finalize(const double* __restrict__ part, int HW, int C, int groups,
+__global__ __launch_bounds__(1024) void k_gn_finalize(const double* __restrict__ part, int HW, int C, int groups,
                                                      int nsplit, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
                                                      float* __restrict__ scale, float* __restrict__ shift) {
@@ -151,8 +155,37 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const double* __restrict__ 
     float* sh = lsm + ((C + 3) & ~3);
     double* gstat = reinterpret_cast<double*>(lsm + 2 * ((C + 3) & ~3));
     double* csum = gstat + 2 * groups;
+    double* lsum = csum + 2 * C;  // [lanes][C][2]
     const int b = blockIdx.x;
-    gn_scale_shift(part, b, nsplit, C, groups, HW, gamma, beta, eps, sc, sh, gstat, csum);
+    // 1024 threads: `lanes` threads per channel each sum a strided subset of the nsplit partials (the
+    // one-thread-per-channel loop left 3/4 of a 256-thread block idle and was ~45 us at 256^2, where
+    // nsplit is 512), then one thread per channel adds its lanes in lane order (deterministic)
+    const int lanes = max(1, (int)blockDim.x / C);
+    const double* pb = part + (size_t)b * nsplit * C * 2;
+    for (int t = threadIdx.x; t < lanes * C; t += blockDim.x) {
+        const int l = t / C, c = t - (t / C) * C;
+        double a = 0, q = 0;
+#pragma unroll 4
+        for (int sp = l; sp < nsplit; sp += lanes) {
+            const double2 v = *reinterpret_cast<const double2*>(pb + ((size_t)sp * C + c) * 2);
+            a += v.x;
+            q += v.y;
+        }
+        lsum[2 * t] = a;
+        lsum[2 * t + 1] = q;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        double a = 0, q = 0;
+        for (int l = 0; l < lanes; ++l) {
+            a += lsum[2 * (l * C + c)];
+            q += lsum[2 * (l * C + c) + 1];
+        }
+        csum[2 * c] = a;
+        csum[2 * c + 1] = q;
+    }
+    __syncthreads();
+    gn_tables_from_csum(C, groups, HW, gamma, beta, eps, sc, sh, gstat, csum);
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
         scale[(size_t)b * C + c] = sc[c];
         shift[(size_t)b * C + c] = sh[c];
@@ -773,21 +806,27 @@ extern "C" int tcx_gn_finalize(const double* part, int Bt, int HW, int C, int gr
                                const float* beta, float eps, float* scale, float* shift, void* stream) {
     TCX_REQUIRE(part && scale && shift && groups > 0 && C % groups == 0 && nsplit >= 1, "tcx_gn_finalize: bad args");
     if (Bt == 0) return TCX_OK;
-    const size_t shm = gn_fold_lds_bytes(C, groups);
-    hipLaunchKernelGGL(k_gn_finalize, dim3(Bt), dim3(256), shm, (hipStream_t)stream, part, HW, C, groups, nsplit, gamma,
+    const size_t shm = gn_finalize_wide_lds_bytes(C, groups);
+    hipLaunchKernelGGL(k_gn_finalize, dim3(Bt), dim3(1024), shm, (hipStream_t)stream, part, HW, C, groups, nsplit, gamma,
                        beta, eps, scale, shift);
     return check_launch("tcx_gn_finalize");
 }
 
-extern "C" int tcx_gn_apply_tab(const float* x, float* y, int Bt, int HW, int C, const float* scale, const float* shift,
-                                int silu, void* stream) {
+extern "C" int tcx_gn_apply_tab_absmax(const float* x, float* y, int Bt, int HW, int C, const float* scale,
+                                       const float* shift, int silu, unsigned* amax, void* stream) {
     TCX_REQUIRE(x && y && scale && shift && C % 4 == 0 && aligned16(x) && aligned16(y), "tcx_gn_apply_tab: bad args");
     if (Bt == 0) return TCX_OK;
     const int ppb = std::max(1, 32768 / C);  // 128 KB of activations per block
     const dim3 grid(cdiv(HW, ppb), Bt);
     const size_t shm = (size_t)2 * ((C + 3) & ~3) * sizeof(float);
-    hipLaunchKernelGGL(k_gn_apply_tab, grid, dim3(256), shm, (hipStream_t)stream, x, y, HW, C, scale, shift, silu, ppb);
+    hipLaunchKernelGGL(k_gn_apply_tab, grid, dim3(256), shm, (hipStream_t)stream, x, y, HW, C, scale, shift, silu, ppb,
+                       amax);
     return check_launch("tcx_gn_apply_tab");
+}
+
+extern "C" int tcx_gn_apply_tab(const float* x, float* y, int Bt, int HW, int C, const float* scale, const float* shift,
+                                int silu, void* stream) {
+    return tcx_gn_apply_tab_absmax(x, y, Bt, HW, C, scale, shift, silu, nullptr, stream);
 }
 
 extern "C" int tcx_upsample2x(const float* x, float* y, int Bt, int H, int W, int C, const float* scale,

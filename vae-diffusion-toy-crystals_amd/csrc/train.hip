@@ -162,9 +162,10 @@ __global__ __launch_bounds__(256) void k_gn_bwd_apply(const float* __restrict__ 
                                                       const float* __restrict__ sc, const float* __restrict__ sh,
                                                       const float* __restrict__ k1, const float* __restrict__ k2,
                                                       const float* __restrict__ k3, int Bt, int HW, int C, int silu,
-                                                      float* __restrict__ dx) {
+                                                      float* __restrict__ dx, unsigned* __restrict__ amax) {
     const size_t n4 = (size_t)Bt * HW * C / 4;
     const int C4 = C / 4;
+    float m = 0.f;  // max |dx| of this thread's elements (reported when amax is given)
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
         const size_t pix = i / C4;
         const int c = (int)(i - pix * C4) * 4;
@@ -181,7 +182,9 @@ __global__ __launch_bounds__(256) void k_gn_bwd_apply(const float* __restrict__ 
             o[e] = fmaf(k1[t + e], dz, fmaf(k2[t + e], xs[e], k3[t + e]));
         }
         reinterpret_cast<float4*>(dx)[i] = make_float4(o[0], o[1], o[2], o[3]);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
     }
+    if (amax) block_amax_publish(m, amax);
 }
 
 // d gamma[c] = sum_b S2[b][c], d beta[c] = sum_b S1[b][c]  (32-lane group per channel, fixed tree)
@@ -941,9 +944,10 @@ extern "C" size_t tcx_gn_bwd_workspace(int Bt, int HW, int C) {
     return ((size_t)Bt * nsplit * C * 2 + (size_t)Bt * C * 2) * sizeof(double) + (size_t)3 * Bt * C * sizeof(float) + 1024;
 }
 
-extern "C" int tcx_gn_bwd(const float* x, const float* dy, const float* scale, const float* shift, const float* mean,
-                          const float* rstd, const float* gamma, int Bt, int HW, int C, int groups, int silu, float* dx,
-                          float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+extern "C" int tcx_gn_bwd_absmax(const float* x, const float* dy, const float* scale, const float* shift,
+                                 const float* mean, const float* rstd, const float* gamma, int Bt, int HW, int C,
+                                 int groups, int silu, float* dx, float* dgamma, float* dbeta, unsigned* amax, void* ws,
+                                 size_t ws_bytes, void* stream) {
     TCX_REQUIRE(x && dy && scale && shift && mean && rstd && dx && ws, "tcx_gn_bwd: null pointer");
     TCX_REQUIRE(C % 4 == 0 && groups > 0 && C % groups == 0 && Bt >= 0 && HW > 0, "tcx_gn_bwd: need C %% 4 == 0");
     TCX_REQUIRE(ws_bytes >= tcx_gn_bwd_workspace(Bt, HW, C), "tcx_gn_bwd: workspace too small");
@@ -966,14 +970,22 @@ extern "C" int tcx_gn_bwd(const float* x, const float* dy, const float* scale, c
                        nsplit, HW, C, groups, mean, rstd, gamma, k1, k2, k3, s12);
     TCX_TRY(check_launch("tcx_gn_bwd finalize"));
     const size_t n4 = (size_t)Bt * HW * C / 4;
-    hipLaunchKernelGGL(k_gn_bwd_apply, dim3(grid1d(n4, 16384)), dim3(256), 0, st, x, dy, scale, shift, k1, k2, k3, Bt,
-                       HW, C, silu, dx);
+    // with amax: at most 2048 workgroups (grid-stride), one atomic each
+    hipLaunchKernelGGL(k_gn_bwd_apply, dim3(grid1d(n4, amax ? 2048 : 16384)), dim3(256), 0, st, x, dy, scale, shift, k1, k2, k3, Bt,
+                       HW, C, silu, dx, amax);
     TCX_TRY(check_launch("tcx_gn_bwd apply"));
     if (dgamma || dbeta) {
         hipLaunchKernelGGL(k_gn_bwd_affine, dim3(cdiv(C, 8)), dim3(256), 0, st, s12, Bt, C, dgamma, dbeta);
         TCX_TRY(check_launch("tcx_gn_bwd affine"));
     }
     return TCX_OK;
+}
+
+extern "C" int tcx_gn_bwd(const float* x, const float* dy, const float* scale, const float* shift, const float* mean,
+                          const float* rstd, const float* gamma, int Bt, int HW, int C, int groups, int silu, float* dx,
+                          float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+    return tcx_gn_bwd_absmax(x, dy, scale, shift, mean, rstd, gamma, Bt, HW, C, groups, silu, dx, dgamma, dbeta, nullptr,
+                             ws, ws_bytes, stream);
 }
 
 extern "C" int tcx_upsample2x_bwd(const float* dy, float* dx, int Bt, int H, int W, int C, void* stream) {

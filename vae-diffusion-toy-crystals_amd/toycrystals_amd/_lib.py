@@ -82,6 +82,7 @@ _SIGS = {
     "tcx_gn_partials": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),
     "tcx_gn_apply": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_int, c_fp, c_fp, c_float, c_int, c_fp]),
     "tcx_gn_apply_tab": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp]),
+    "tcx_gn_apply_tab_absmax": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp, c_fp]),
     "tcx_gn_finalize": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_float, c_fp, c_fp, c_fp]),
     "tcx_upsample2x": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
     "tcx_attention": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
@@ -156,6 +157,8 @@ _SIGS = {
     "tcx_gn_bwd_workspace": (c_size, [c_int, c_int, c_int]),
     "tcx_gn_bwd": (c_int, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp,
                            c_fp, c_fp, c_size, c_fp]),
+    "tcx_gn_bwd_absmax": (c_int, [c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp,
+                                  c_fp, c_fp, c_fp, c_fp, c_size, c_fp]),
     "tcx_upsample2x_bwd": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_colsum_workspace": (c_size, [c_int, c_int, c_int]),
     "tcx_colsum": (c_int, [c_fp, c_int, c_int, c_int, c_fp, c_fp, c_float, c_fp, c_size, c_fp]),

@@ -119,15 +119,56 @@ def _split_ok(x1, x2, C1, C2, ks, kpad, macs) -> bool:
             and max(x1.numel(), 0 if x2 is None else x2.numel()) * 4 < (1 << 31))
 
 
+_SLOT_INIT = {}
+_PRODUCER_AMAX = os.environ.get("TCX_TRAIN_AMAX", "1") != "0"  # 0: every split operand gets its own absmax pass (A/B)
+
+
+def _scale_slot(device) -> torch.Tensor:
+    """A fresh [bits = 0][1.0][1/s] slot (int32 x 12, fields 16 B apart): one copy launch."""
+    t = _SLOT_INIT.get(device)
+    if t is None:
+        h = torch.zeros(12, dtype=torch.int32)
+        h[4:5].view(torch.float32).fill_(1.0)
+        t = _SLOT_INIT[device] = h.to(device)
+    return t.clone()
+
+
+def _absmax_slot_for(x: torch.Tensor, C: int) -> torch.Tensor | None:
+    """A slot for a producer kernel to raise with max |x| (tcx_gn_apply_tab_absmax / tcx_gn_bwd_absmax)
+    when a split training conv may consume x (f16x3, channels % 32, a conv above the split threshold)."""
+    from ._lib import conv_precision
+    if not (_PRODUCER_AMAX and _TRAIN_SPLIT and C % 32 == 0 and 9.0 * x.numel() * C >= _SPLIT_MIN_MACS
+            and conv_precision() == "f16x3"):
+        return None
+    return _scale_slot(x.device)
+
+
+def _tag_absmax(x: torch.Tensor, sl) -> None:
+    # consumed by _h2_scaled only while x is unchanged (same storage, same version counter: autograd's
+    # in-place gradient accumulation bumps it)
+    if sl is not None:
+        x._tcx_amax = (sl, x._version, x.data_ptr())
+
+
+def _tagged_slot(t: torch.Tensor):
+    a = getattr(t, "_tcx_amax", None)
+    if a is not None and a[1] == t._version and a[2] == t.data_ptr():
+        return a[0]
+    return None
+
+
 def _h2_scaled(ts):
     """fp32 tensors sharing ONE power-of-two scale s (max |s v| in [2^13, 2^14)) -> their h2 records
-    and a 1-element float tensor holding 1/s (tcx_absmax + tcx_f32_to_h2_scaled)."""
+    and a 1-element float tensor holding 1/s (tcx_absmax + tcx_f32_to_h2_scaled).  A single tensor
+    whose producer already reported its max |value| (_tag_absmax) skips the absmax pass."""
     L = lib()
     st = _st(ts[0])
-    sl = torch.zeros(12, dtype=torch.int32, device=ts[0].device)  # [bits][1.0][1/s], 16 B apart
-    sl[4:5].view(torch.float32).fill_(1.0)
+    sl = _tagged_slot(ts[0]) if len(ts) == 1 else None
+    pre = sl is not None
+    if not pre:
+        sl = _scale_slot(ts[0].device)  # [bits][1.0][1/s], 16 B apart
     bits, one, inv = ptr(sl), ptr(sl) + 16, ptr(sl) + 32
-    for t in ts:
+    for t in ts if not pre else ():
         check(L.tcx_absmax(ptr(t), t.numel(), bits, st), "tcx_absmax")
     hs = []
     for i, t in enumerate(ts):
@@ -388,7 +429,10 @@ class GroupNormActFn(torch.autograd.Function):
         check(L.tcx_gn_stats(ptr(part), B, HW, C, groups, ns, ptr(gamma), ptr(beta), float(eps), ptr(sc), ptr(sh),
                              ptr(mean), ptr(rstd), st), "tcx_gn_stats")
         y = torch.empty_like(x)
-        check(L.tcx_gn_apply_tab(ptr(x), ptr(y), B, HW, C, ptr(sc), ptr(sh), int(silu), st), "tcx_gn_apply_tab")
+        sl = _absmax_slot_for(x, C)
+        check(L.tcx_gn_apply_tab_absmax(ptr(x), ptr(y), B, HW, C, ptr(sc), ptr(sh), int(silu), ptr(sl), st),
+              "tcx_gn_apply_tab")
+        _tag_absmax(y, sl)
         ctx.save_for_backward(x, sc, sh, mean, rstd, gamma)
         ctx.cfg = (groups, int(silu))
         return y
@@ -405,8 +449,11 @@ class GroupNormActFn(torch.autograd.Function):
         dbt = _empty((C,), x) if ctx.needs_input_grad[2] else None
         nb = int(L.tcx_gn_bwd_workspace(B, H * W, C))
         ws = _ws(x.device, nb)
-        check(L.tcx_gn_bwd(ptr(x), ptr(dy), ptr(sc), ptr(sh), ptr(mean), ptr(rstd), ptr(gamma), B, H * W, C, groups,
-                           silu, ptr(dx), ptr(dg), ptr(dbt), ptr(ws), ws.numel(), _st(x)), "tcx_gn_bwd")
+        sl = _absmax_slot_for(x, C)
+        check(L.tcx_gn_bwd_absmax(ptr(x), ptr(dy), ptr(sc), ptr(sh), ptr(mean), ptr(rstd), ptr(gamma), B, H * W, C,
+                                  groups, silu, ptr(dx), ptr(dg), ptr(dbt), ptr(sl), ptr(ws), ws.numel(), _st(x)),
+              "tcx_gn_bwd")
+        _tag_absmax(dx, sl)
         return dx, dg, dbt, None, None, None
 
 
