@@ -1,0 +1,16 @@
+# GroupNorm finalize on 1024 threads (no knob: per-layer vs r03_z) + tile-free first-conv records (TCX_FIRST_REC A/B): full GPU suite, headline and config-5 A/B, per-position traces
+set -o pipefail
+cd /root/repo
+export TMPDIR=/tmp
+T=r03_af
+timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 && \
+for r in 1 2; do
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 2 --fp32-passes 0 --lanes 1 > gpurun_out/${T}_fr1_$r.log 2>&1 || exit 1
+  TCX_FIRST_REC=0 timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 2 --fp32-passes 0 --lanes 1 > gpurun_out/${T}_fr0_$r.log 2>&1 || exit 1
+done && \
+for r in 1 2; do
+  timeout -k 10 300 python -u bench.py --img-size 256 --batch 64 --precision bf16 --steps 1 --warmup 1 --lanes 1 --no-cpu-baseline > gpurun_out/${T}_c5_$r.log 2>&1 || exit 1
+  TCX_FIRST_REC=0 timeout -k 10 300 python -u bench.py --img-size 256 --batch 64 --precision bf16 --steps 1 --warmup 1 --lanes 1 --no-cpu-baseline > gpurun_out/${T}_c5fr0_$r.log 2>&1 || exit 1
+done && \
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${T}_cfg5prof -o run -- python3 bench.py --img-size 256 --batch 64 --precision bf16 --n-steps 6 --steps 1 --warmup 1 --lanes 1 --no-cpu-baseline --fp32-passes 0 > gpurun_out/${T}_cfg5prof.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${T}_prof -o run -- python3 bench.py --n-steps 20 --steps 1 --warmup 1 --lanes 1 --no-cpu-baseline --fp32-passes 0 > gpurun_out/${T}_prof.log 2>&1

@@ -531,6 +531,178 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int H
         if (j < nk) dst[(size_t)(tg + 4 * j) * HW] = acc[j];
 }
 
+// Head, register form (round 3): as k_head8, but each lane's CL channels of w_out (9 taps) and of the
+// image's scale / shift live in VGPRs for the whole block instead of being re-read from LDS for every
+// element (5 LDS reads per element, ~22 LDS clocks per wave-element: the LDS, not HBM, bounded
+// k_head8).  A block takes HR_PASS passes of 32 pixels of one image; the loads of the next two passes
+// are in flight during the current pass's math (~185 VGPRs: 2 waves per SIMD).  Same arithmetic in the
+// same order as k_head8 (bit-identical).
+constexpr int HR_PASS = 8;
+constexpr int HPR = 32 * HR_PASS;
+template <int Q>
+__global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int HW, const float* __restrict__ tsc,
+                                                const float* __restrict__ tsh, const float* __restrict__ w_out,
+                                                float* __restrict__ r) {
+    constexpr int C = 32 * Q;
+    constexpr int CL = 4 * Q;
+    const int p0 = blockIdx.x * HPR;
+    const int b = p0 / HW;
+    const int tid = threadIdx.x;
+    const int sub = tid & 7, pl = tid >> 3;
+    const int c0 = sub * CL;
+    float4 v[Q], vn[Q];  // passes 0 and 1 in flight before the constants are loaded
+    {
+        const float* src = h + (size_t)(p0 + pl) * C + c0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            v[q] = *reinterpret_cast<const float4*>(src + 4 * q);
+            vn[q] = *reinterpret_cast<const float4*>(src + 32 * C + 4 * q);
+        }
+    }
+    float wr[CL][9], scl[CL], shf[CL];
+#pragma unroll
+    for (int j = 0; j < CL; ++j) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wr[j][t] = w_out[(c0 + j) * 9 + t];
+        scl[j] = tsc[(size_t)b * C + c0 + j];
+        shf[j] = tsh[(size_t)b * C + c0 + j];
+    }
+    for (int pass = 0; pass < HR_PASS; ++pass) {
+        const int pg = p0 + pass * 32 + pl;
+        float4 vnn[Q];  // two passes ahead
+        if (pass + 2 < HR_PASS) {
+            const float* src = h + (size_t)(pg + 64) * C + c0;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) vnn[q] = *reinterpret_cast<const float4*>(src + 4 * q);
+        }
+        float acc[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t] = 0.f;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const float xs[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j = 4 * q + e;
+                const float yv = fmaf(xs[e], scl[j], shf[j]);
+                const float x = yv * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * yv));
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc[t] = fmaf(x, wr[j][t], acc[t]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            acc[t] += __shfl_xor(acc[t], 1);
+            acc[t] += __shfl_xor(acc[t], 2);
+            acc[t] += __shfl_xor(acc[t], 4);
+        }
+        const int p = pg - b * HW;
+        float* dst = r + (size_t)b * 9 * HW + p;
+        float mine = acc[0];
+#pragma unroll
+        for (int t = 1; t < 8; ++t)
+            if (sub == t) mine = acc[t];
+        dst[(size_t)sub * HW] = mine;  // lane sub writes tap sub; lane 0 also tap 8
+        if (sub == 0) dst[(size_t)8 * HW] = acc[8];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            v[q] = vn[q];
+            vn[q] = vnn[q];
+        }
+    }
+}
+
+// First conv + GroupNorm_0 + SiLU written straight as down1.net.3's h2 / bf16 records (round 3, the
+// tile-free form of k_conv_first<2>): a workgroup takes FR_PX pixels of one image (one or more whole
+// rows, or part of one); the x_t rows it touches (plus the wrapped row above / below) are staged in LDS
+// once, with the 3x3 weights [tap][C0] and the image's bias / scale / shift rows; then each thread
+// computes whole 8-channel records (item = pixel * C0/8 + group: consecutive lanes write consecutive
+// 32-B records, as the tile form's store phase) from 9 broadcast x reads and 18 b128 weight reads.
+// No fp32 tile, one barrier, ~5-8 KB of LDS (the tile form held 35 KB: 4 workgroups per CU).
+// Needs HW % FR_PX == 0, and FR_PX % W == 0 or W % FR_PX == 0; C0 % 8 == 0.
+constexpr int FR_PX = 128;
+__global__ __launch_bounds__(256) void k_conv_first_rec(const float* __restrict__ x, int bmod, int H, int W, int C0,
+                                                        const float* __restrict__ w0, int kpad,
+                                                        const float* __restrict__ bias_b, char* __restrict__ y,
+                                                        CondTab ct, int Bimg, int cfg, const float* __restrict__ tsc,
+                                                        const float* __restrict__ tsh, unsigned* ovf, int bf) {
+    extern __shared__ __attribute__((aligned(16))) float fr[];  // w[9][C0] | bias[C0] | sc[C0] | sh[C0] | xr[nr][W]
+    float* w = fr;
+    float* bs = w + 9 * C0;
+    float* sc = bs + C0;
+    float* sh = sc + C0;
+    float* xr = sh + C0;
+    const int HW = H * W;
+    const int b = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int p0 = blockIdx.x * FR_PX;
+    const int y0 = p0 / W;                                  // first row of the block's pixels
+    const int nrow = (FR_PX >= W ? FR_PX / W : 1) + 2;     // staged rows y0-1 .. y0+rows
+    const float* xb = x + (size_t)(b % bmod) * HW;
+    for (int i = tid; i < nrow * W; i += 256) {
+        const int r = i / W, c = i - (i / W) * W;
+        xr[i] = xb[(size_t)wrap_idx(y0 - 1 + r, H) * W + c];
+    }
+    for (int i = tid; i < 9 * C0; i += 256) {
+        const int co = i / 9, k = i - (i / 9) * 9;  // w0 packed [co][kpad], k = tap (Cin = 1)
+        w[k * C0 + co] = w0[(size_t)co * kpad + k];
+    }
+    const float* bb = ct.bias_img ? cond_bias_row(ct, b, Bimg, cfg, C0) : bias_b + (size_t)b * C0;
+    for (int c = tid; c < C0; c += 256) {
+        bs[c] = bb[c];
+        sc[c] = tsc[(size_t)b * C0 + c];
+        sh[c] = tsh[(size_t)b * C0 + c];
+    }
+    __syncthreads();
+    const int G8 = C0 / 8;
+    char* dst = y + ((size_t)b * HW + p0) * C0 * 4;
+    bool bad = false;
+    for (int item = tid; item < FR_PX * G8; item += 256) {
+        const int pl = item / G8, g = item - (item / G8) * G8;
+        const int p = p0 + pl;
+        const int yy = p / W, xx = p - (p / W) * W;
+        const int ry = yy - y0;  // staged row of (yy - 1) is ry
+        float xv[9];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) xv[dy * 3 + dx] = xr[(ry + dy) * W + wrap_idx(xx + dx - 1, W)];
+        float4 a0 = *reinterpret_cast<const float4*>(bs + 8 * g);
+        float4 a1 = *reinterpret_cast<const float4*>(bs + 8 * g + 4);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const float4 u = *reinterpret_cast<const float4*>(w + k * C0 + 8 * g);
+            const float4 v = *reinterpret_cast<const float4*>(w + k * C0 + 8 * g + 4);
+            a0.x = fmaf(u.x, xv[k], a0.x); a0.y = fmaf(u.y, xv[k], a0.y);
+            a0.z = fmaf(u.z, xv[k], a0.z); a0.w = fmaf(u.w, xv[k], a0.w);
+            a1.x = fmaf(v.x, xv[k], a1.x); a1.y = fmaf(v.y, xv[k], a1.y);
+            a1.z = fmaf(v.z, xv[k], a1.z); a1.w = fmaf(v.w, xv[k], a1.w);
+        }
+        const float4 s0 = *reinterpret_cast<const float4*>(sc + 8 * g);
+        const float4 s1 = *reinterpret_cast<const float4*>(sc + 8 * g + 4);
+        const float4 t0 = *reinterpret_cast<const float4*>(sh + 8 * g);
+        const float4 t1 = *reinterpret_cast<const float4*>(sh + 8 * g + 4);
+        auto sl = [](float v, float scl, float shf) {
+            const float q = fmaf(v, scl, shf);
+            return q * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * q));
+        };
+        const float4 o0 = make_float4(sl(a0.x, s0.x, t0.x), sl(a0.y, s0.y, t0.y), sl(a0.z, s0.z, t0.z),
+                                      sl(a0.w, s0.w, t0.w));
+        const float4 o1 = make_float4(sl(a1.x, s1.x, t1.x), sl(a1.y, s1.y, t1.y), sl(a1.z, s1.z, t1.z),
+                                      sl(a1.w, s1.w, t1.w));
+        uint2 hi0, lo0, hi1, lo1;
+        split4x(o0, hi0, lo0, bf != 0);
+        split4x(o1, hi1, lo1, bf != 0);
+        if (!bf)
+            bad = bad || h2_bad(o0.x) || h2_bad(o0.y) || h2_bad(o0.z) || h2_bad(o0.w) || h2_bad(o1.x) ||
+                  h2_bad(o1.y) || h2_bad(o1.z) || h2_bad(o1.w);
+        char* gp = dst + (size_t)pl * C0 * 4 + 32 * g;
+        *reinterpret_cast<uint4*>(gp) = make_uint4(hi0.x, hi0.y, hi1.x, hi1.y);
+        *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo0.x, lo0.y, lo1.x, lo1.y);
+    }
+    h2_flag(ovf, bad);
+}
+
 // ---------------------------------------------------------------- 8-lanes-per-pixel forms
 // For C = 32*Q (every split-path net): a pixel's C channels are 8 contiguous runs of 4Q channels,
 // one per lane of an 8-lane group, so a wave reads/writes 8 whole pixels (8*C*4 contiguous bytes)
@@ -954,9 +1126,21 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                 TCX_TRY(check_launch("k_first_gnsum"));
                 ns = 1;
                 TCX_TRY(gn_tab(net, P, 0, P.P0, C, gn, ns, st));
-                hipLaunchKernelGGL(k_conv_first<2>, dim3(H * W / FIRST_PX, Bt), dim3(256), shm, st, x, B, H, W, C,
-                                   c0.w, c0.kpad, P.bias0, P.a64, nullptr, ct, B, cfg, P.sc(0), P.sh(0), h2.ovf,
-                                   h2.bf ? 1 : 0);
+                static const bool first_rec = [] {  // TCX_FIRST_REC=0: the LDS-tile form (A/B)
+                    const char* e = getenv("TCX_FIRST_REC");
+                    return !(e && e[0] == '0');
+                }();
+                if (first_rec && (H * W) % FR_PX == 0 && (FR_PX % W == 0 || W % FR_PX == 0)) {
+                    const int nrow = (FR_PX >= W ? FR_PX / W : 1) + 2;
+                    const size_t shr = ((size_t)12 * C + (size_t)nrow * W) * sizeof(float);
+                    hipLaunchKernelGGL(k_conv_first_rec, dim3(H * W / FR_PX, Bt), dim3(256), shr, st, x, B, H, W, C,
+                                       c0.w, c0.kpad, P.bias0, (char*)P.a64, ct, B, cfg, P.sc(0), P.sh(0), h2.ovf,
+                                       h2.bf ? 1 : 0);
+                } else {
+                    hipLaunchKernelGGL(k_conv_first<2>, dim3(H * W / FIRST_PX, Bt), dim3(256), shm, st, x, B, H, W,
+                                       C, c0.w, c0.kpad, P.bias0, P.a64, nullptr, ct, B, cfg, P.sc(0), P.sh(0),
+                                       h2.ovf, h2.bf ? 1 : 0);
+                }
                 TCX_TRY(check_launch("k_conv_first (GroupNorm+SiLU records)"));
                 first_fused = true;
                 pro[0] = false;
@@ -1064,7 +1248,17 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     {
         TCX_TRY(gn_tab(net, P, 10, P.P0, C, gn, ns, st));
         TCX_REQUIRE(C % 4 == 0, "head: C %% 4");
-        if (P.P0 % HP8 == 0 && (C == 96 || C == 64 || C == 128 || C == 32)) {
+        static const bool head_reg = [] {  // TCX_HEAD_REG=0: the LDS-weight k_head8 (A/B)
+            const char* e = getenv("TCX_HEAD_REG");
+            return !(e && e[0] == '0');
+        }();
+        if (head_reg && P.P0 % HPR == 0 && (C == 96 || C == 64 || C == 32)) {
+            const dim3 gr(Bt * P.P0 / HPR);
+            if (C == 96) hipLaunchKernelGGL(k_head8r<3>, gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
+            else if (C == 64) hipLaunchKernelGGL(k_head8r<2>, gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
+            else hipLaunchKernelGGL(k_head8r<1>, gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
+            TCX_TRY(check_launch("k_head8r"));
+        } else if (P.P0 % HP8 == 0 && (C == 96 || C == 64 || C == 128 || C == 32)) {
             const dim3 g8(Bt * P.P0 / HP8);
             if (C == 96) hipLaunchKernelGGL(k_head8<3>, g8, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
             else if (C == 64) hipLaunchKernelGGL(k_head8<2>, g8, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
