@@ -166,6 +166,41 @@ def test_group_norm_act_fn_vs_torch(C, groups, silu, H):
     assert err(bd.grad, br.grad) < 2e-5
 
 
+def test_group_norm_producer_absmax():
+    """GroupNormActFn reports max |y| (forward) and max |dx| (backward) for the split training conv
+    that consumes them (tcx_gn_apply_tab_absmax / tcx_gn_bwd_absmax): the tagged slot must hold exactly
+    the bits of the tensor's max |value|, and an in-place change (version bump) must drop the tag."""
+    from toycrystals_amd import functional as TF
+    seen = {}
+
+    class Probe(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x.view_as(x)
+
+        @staticmethod
+        def backward(ctx, g):
+            seen["dx"], seen["slot"] = g, TF._tagged_slot(g)
+            return g
+
+    g = torch.Generator().manual_seed(3)
+    B, H, C = 16, 64, 96  # 9 * numel * C above the split threshold: the producer reports
+    x = cu(torch.randn(B, H, H, C, generator=g) * 3 + 0.25).requires_grad_()
+    gm = cu(1 + 0.2 * torch.randn(C, generator=g)).requires_grad_()
+    bt = cu(0.2 * torch.randn(C, generator=g)).requires_grad_()
+    y = TF.GroupNormActFn.apply(Probe.apply(x), gm, bt, 8, 1e-5, 1)
+    sl = TF._tagged_slot(y)
+    assert sl is not None, "forward producer did not tag its output"
+    assert int(sl[0]) == int(y.detach().abs().max().view(torch.int32)), "forward max |y| bits"
+    y.backward(cu(torch.randn(B, H, H, C, generator=g) * 1e-6))
+    assert seen["slot"] is not None, "backward producer did not tag dx"
+    assert int(seen["slot"][0]) == int(seen["dx"].abs().max().view(torch.int32)), "backward max |dx| bits"
+    z = y.detach()
+    z._tcx_amax = y._tcx_amax
+    z.mul_(2.0)  # in place: the tag no longer describes the values
+    assert TF._tagged_slot(z) is None
+
+
 @pytest.mark.parametrize("H,C", [(8, 32), (16, 16), (4, 8)])
 def test_upsample_fn_vs_torch(H, C):
     from toycrystals_amd import functional as TF
