@@ -29,10 +29,12 @@ typedef unsigned u4 __attribute__((ext_vector_type(4)));
 #define TCX_ATT_LOAD(k0) \
     do { \
 _Pragma("unroll") \
-        for (int u = 0; u < KI; ++u) {  /* KT * KP = 32 D: a multiple of 512 for every D here */ \
+        for (int u = 0; u < KI; ++u) {  /* BF: the hi pieces only (global piece 2 pc) */ \
             const int i = tid + 512 * u; \
-            const int j = i / KP, pc = i - (i / KP) * KP; \
-            kreg[u] = *reinterpret_cast<const f4*>(base + (size_t)(k0 + j) * rs + (size_t)(C + h * D) * 4 + pc * 16); \
+            const int j = i / KPL, pc = i - (i / KPL) * KPL; \
+            if (KT * KPL % 512 == 0 || i < KT * KPL) \
+                kreg[u] = *reinterpret_cast<const f4*>(base + (size_t)(k0 + j) * rs + (size_t)(C + h * D) * 4 + \
+                                                       (BF ? 2 * pc : pc) * 16); \
         } \
 _Pragma("unroll") \
         for (int u = 0; u < VI; ++u) { \
@@ -41,9 +43,9 @@ _Pragma("unroll") \
                 const int g = i / (KT / 2), jp = i - g * (KT / 2);  /* key pair (2 jp, 2 jp + 1), dim group g */ \
                 const char* src = base + (size_t)(k0 + 2 * jp) * rs + (size_t)(2 * C + h * D) * 4 + g * 32; \
                 vreg[u][0] = *reinterpret_cast<const u4*>(src); \
-                vreg[u][1] = *reinterpret_cast<const u4*>(src + 16); \
+                if (!BF) vreg[u][1] = *reinterpret_cast<const u4*>(src + 16); \
                 vreg[u][2] = *reinterpret_cast<const u4*>(src + rs); \
-                vreg[u][3] = *reinterpret_cast<const u4*>(src + rs + 16); \
+                if (!BF) vreg[u][3] = *reinterpret_cast<const u4*>(src + rs + 16); \
             } \
         } \
     } while (0)
@@ -55,8 +57,8 @@ _Pragma("unroll") \
 _Pragma("unroll") \
         for (int u = 0; u < KI; ++u) { \
             const int i = tid + 512 * u; \
-            const int j = i / KP, pc = i - (i / KP) * KP; \
-            *reinterpret_cast<f4*>(Ks + j * KSB + pc * 16) = kreg[u]; \
+            const int j = i / KPL, pc = i - (i / KPL) * KPL; \
+            if (KT * KPL % 512 == 0 || i < KT * KPL) *reinterpret_cast<f4*>(Ks + j * KSB + pc * 16) = kreg[u]; \
         } \
 _Pragma("unroll") \
         for (int u = 0; u < VI; ++u) { \
@@ -75,11 +77,15 @@ _Pragma("unroll") \
                     const unsigned a = (h0[e >> 1] >> sh) & 0xffffu, c = (h1[e >> 1] >> sh) & 0xffffu; \
                     const unsigned al = (l0[e >> 1] >> sh) & 0xffffu, cl = (l1[e >> 1] >> sh) & 0xffffu; \
                     Vh[(g * 8 + e) * VSW + col] = a | (c << 16); \
-                    Vl[(g * 8 + e) * VSW + col] = al | (cl << 16); \
+                    if (!BF) Vl[(g * 8 + e) * VSW + col] = al | (cl << 16); \
                 } \
             } \
         } \
     } while (0)
+
+// staged K row: h2 pieces (D * 4 B), or for BF only the hi pieces (D * 2 B: the lo halves of K and V are
+// never loaded), + 16 B pad (both strides an odd number of 16-B units: conflict-free b128 row reads)
+__host__ __device__ constexpr int attn_ksb(int D, bool BF) { return (BF ? D * 2 : D * 4) + 16; }
 
 // BF: bf16 records (h2.hpp), one v_mfma_f32_32x32x16_bf16 (hi x hi) per product, P in bf16
 template <int D, bool BF>
@@ -91,7 +97,7 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     constexpr int DS = D / 16;         // 16-deep steps of Q.K
     constexpr int DT = (D + 31) / 32;  // 32-row tiles of O^T
     constexpr int DP = DT * 32;
-    constexpr int KSB = D * 4 + 16;    // bytes per staged key row (h2) + 16 B pad
+    constexpr int KSB = attn_ksb(D, BF);  // bytes per staged key row (h2, or BF: hi pieces) + 16 B pad
     constexpr int VSW = KT / 2 + 4;    // dwords per V^T row (two f16 slots each) + 16 B pad
     // two LDS stages (tile t computed from one while tile t+1, loaded into registers during that
     // compute, is written to the other): [2][K | V^T hi | V^T lo]
@@ -131,9 +137,9 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     for (int t = 0; t < DT; ++t) oacc[t] = (f32x16){};
     float m = -INFINITY, l = 0.f;
     constexpr int KP = D / 4;  // 16-B pieces per K row
+    constexpr int KPL = BF ? KP / 2 : KP;  // pieces staged per K row (BF: the hi pieces)
     constexpr int G = D / 8;   // 8-dim groups per V row
-    static_assert((KT * KP) % 512 == 0, "K tile pieces must tile the block");
-    constexpr int KI = KT * KP / 512;                // K pieces per thread
+    constexpr int KI = (KT * KPL + 511) / 512;       // K pieces per thread (guarded when ragged)
     constexpr int VI = ((KT / 2) * G + 511) / 512;   // V (key pair, dim group) items per thread
     f4 kreg[KI];        // native vectors: arrays of HIP's float4/uint4 structs stayed in scratch here
     u4 vreg[VI][4];
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
             const char* kr = Ks + (n * 32 + li) * KSB;
 #pragma unroll
             for (int s = 0; s < DS; ++s) {
-                const h8 kh = *reinterpret_cast<const h8*>(kr + (2 * s + lh) * 32);
+                const h8 kh = *reinterpret_cast<const h8*>(kr + (2 * s + lh) * (BF ? 16 : 32));
                 if constexpr (BF) {
                     sacc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, kh),
                                                                       __builtin_bit_cast(bf8, qh[s]), sacc[n], 0, 0, 0);
@@ -166,11 +172,18 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
                 sacc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[s], sacc[n], 0, 0, 0);
             }
         }
-        float mt = -INFINITY;
+        // row max and row sum as NST independent chains combined at the end (one 64-long dependent
+        // chain per lane left the two waves per SIMD stalled on VALU latency)
+        float mtn[NST];
 #pragma unroll
-        for (int n = 0; n < NST; ++n)
+        for (int n = 0; n < NST; ++n) {
+            mtn[n] = sacc[n][0];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sacc[n][r]);
+            for (int r = 1; r < 16; ++r) mtn[n] = fmaxf(mtn[n], sacc[n][r]);
+        }
+        float mt = mtn[0];
+#pragma unroll
+        for (int n = 1; n < NST; ++n) mt = fmaxf(mt, mtn[n]);
         mt = fmaxf(mt, __shfl_xor(mt, 32));
         const float mn = fmaxf(m, mt);
         // exponentials as hardware exp2 of pre-scaled logits (v_exp_f32; the VALU of the
@@ -183,9 +196,11 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
         for (int t = 0; t < DT; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) oacc[t][r] *= alpha;
-        float lt = 0.f;
+        float ltn[NST];
 #pragma unroll
         for (int n = 0; n < NST; ++n) {
+            float& lt = ltn[n];
+            lt = 0.f;
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const int c0 = (n * 32 + 16 * s + 8 * lh) >> 1;
@@ -224,6 +239,9 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
                 }
             }
         }
+        float lt = ltn[0];
+#pragma unroll
+        for (int n = 1; n < NST; ++n) lt += ltn[n];
         lt += __shfl_xor(lt, 32);
         l += lt;
         if (tt + 1 < ntile) TCX_ATT_STORE(cur ^ 1);  // that stage was last read in tile tt - 1
@@ -247,7 +265,7 @@ template <int D, bool BF>
 int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
     const float scale = (float)(1.0 / std::sqrt((double)D));
     constexpr int DP = (D + 31) / 32 * 32;
-    constexpr size_t shm = 2 * ((size_t)128 * (D * 4 + 16) + 2 * (size_t)DP * (128 / 2 + 4) * 4);
+    constexpr size_t shm = 2 * ((size_t)128 * attn_ksb(D, BF) + 2 * (size_t)DP * (128 / 2 + 4) * 4);
     static bool attr_set = false;
     if (!attr_set) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D, BF>),
