@@ -370,8 +370,9 @@ __global__ __launch_bounds__(256) void k_conv_first(const float* __restrict__ x,
 //   sum_p out^2 = HW bias^2 + 2 bias (sum_k w_k) S + sum_{k,l} w_k w_l R(o_l - o_k),  R(d) = sum_q x[q] x[q + d]
 // (circular shifts preserve both sums): per image, S and the 25 circular autocorrelations R(d),
 // d in [-2, 2]^2, then 96 channel sums from them.  Everything in fp64 from the fp32 inputs.
-// k_first_acf: grid (HW / chunk, Bt) -> part[b][chunk][26] (chunk = 4096 pixels where HW allows: the
-// 26 block reductions cost more than the sums at 1024); k_first_gnsum: grid Bt -> the [Bt][1][C0][2]
+// k_first_acf: grid (HW / chunk, Bt) -> part[b][chunk][26] (chunk = 1024 pixels: at 64^2 a 4096-pixel
+// chunk is one workgroup per image, one wave per SIMD with nothing to hide its fp64 chains and loads
+// behind: 44 vs 31 us per launch, r03_af vs r03_z; equal at 256^2); k_first_gnsum: grid Bt -> the [Bt][1][C0][2]
 // GroupNorm partials tcx_gn_finalize reads (one split).
 constexpr int FIRST_ACF_PX = 1024;  // smallest chunk (HW % 1024 == 0)
 __global__ __launch_bounds__(256) void k_first_acf(const float* __restrict__ x, int bmod, int H, int W, int chunk,
@@ -1116,7 +1117,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
             const size_t shm = ((size_t)FIRST_PX * (C + 4) + 9 * (size_t)C) * sizeof(float) +
                                8 * (size_t)C * sizeof(double);
             if (h2.on && first_fuse && (H * W) % FIRST_ACF_PX == 0 && C % 8 == 0) {
-                const int chunk = (H * W) % 4096 == 0 ? 4096 : FIRST_ACF_PX;
+                const int chunk = FIRST_ACF_PX;
                 const int nchunk = H * W / chunk;
                 double* acf = gn + (size_t)Bt * C * 2;  // the autocorrelation partials, past the [Bt][1][C][2] sums
                 hipLaunchKernelGGL(k_first_acf, dim3(nchunk, Bt), dim3(256), 0, st, x, B, H, W, chunk, acf);
