@@ -123,11 +123,16 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     auto Kb = [&](int st) { return smem + st * STAGE; };
     auto Vhb = [&](int st) { return reinterpret_cast<unsigned*>(smem + st * STAGE + KT * KSB); };
     auto Vlb = [&](int st) { return reinterpret_cast<unsigned*>(smem + st * STAGE + KT * KSB + DP * VSW * 4); };
+    // ONES (bf16, D < DP): V^T row D, a padding row of the PV product, is all ones, so
+    // O^T row D accumulates the row sum of P on the MFMA, rescaled with O by the online softmax: no
+    // VALU adds for l (they were a fifth of the softmax VALU, which bounds this loop)
+    constexpr bool ONES = BF && DP > D;  // measured: 256^2 bf16 1390 -> 1313 us; the f16x3 form at N = 256 (two key tiles) lost 7 %
+    constexpr unsigned ONE2 = 0x3F803F80u;  // two bf16 ones per dword
     if (DP > D) {
         for (int i = tid; i < (DP - D) * VSW; i += 512) {
 #pragma unroll
             for (int st = 0; st < 2; ++st) {
-                Vhb(st)[D * VSW + i] = 0u;
+                Vhb(st)[D * VSW + i] = ONES && i < VSW ? ONE2 : 0u;
                 Vlb(st)[D * VSW + i] = 0u;
             }
         }
@@ -191,11 +196,16 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
         const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale2);  // 0 on the first tile (m = -inf)
         const float mb = fmaf(-mn, scale2, 10.f);  // + 10: p is produced pre-scaled by 2^10
         m = mn;
-        l *= alpha;
+        if constexpr (!ONES) l *= alpha;
+        // bf16 (N = 4,096: 32 key tiles): rescale only when some lane's running max moved (x 1 is exact;
+        // after the first tiles the max rarely moves, and the 32 multiplies per tile are VALU the loop
+        // is bound by)
+        if (!BF || __builtin_amdgcn_ballot_w64(alpha != 1.f) != 0) {
 #pragma unroll
-        for (int t = 0; t < DT; ++t)
+            for (int t = 0; t < DT; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) oacc[t][r] *= alpha;
+                for (int r = 0; r < 16; ++r) oacc[t][r] *= alpha;
+        }
         float ltn[NST];
 #pragma unroll
         for (int n = 0; n < NST; ++n) {
@@ -209,7 +219,7 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         const float v = __builtin_amdgcn_exp2f(fmaf(sacc[n][8 * s + e], scale2, mb));
-                        lt += v;
+                        if constexpr (!ONES) lt += v;
                         pb[e] = (__bf16)v;
                     }
 #pragma unroll
@@ -224,7 +234,7 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const float v = __builtin_amdgcn_exp2f(fmaf(sacc[n][8 * s + e], scale2, mb));
-                    lt += v;  // l, like the P operand, carries the 2^10 scale
+                    if constexpr (!ONES) lt += v;  // l, like the P operand, carries the 2^10 scale
                     const _Float16 hh = (_Float16)v;
                     ph[e] = hh;
                     pl[e] = (_Float16)(v - (float)hh);
@@ -239,13 +249,24 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
                 }
             }
         }
-        float lt = ltn[0];
+        if constexpr (!ONES) {
+            float lt = ltn[0];
 #pragma unroll
-        for (int n = 1; n < NST; ++n) lt += ltn[n];
-        lt += __shfl_xor(lt, 32);
-        l += lt;
+            for (int n = 1; n < NST; ++n) lt += ltn[n];
+            lt += __shfl_xor(lt, 32);
+            l += lt;
+        }
         if (tt + 1 < ntile) TCX_ATT_STORE(cur ^ 1);  // that stage was last read in tile tt - 1
         __syncthreads();
+    }
+    if constexpr (ONES) {
+        // row D of O^T: tile D / 32, register 4 ((D % 32) / 8) + (D % 4), held by the lanes of half
+        // ((D % 8) / 4) (= 0 for D % 8 == 0); the other half takes it across the wave
+        constexpr int TD = D / 32, RD = 4 * ((D % 32) / 8) + (D % 4);
+        static_assert(D % 8 == 0, "ONES: the sum row must sit in lane half 0");
+        const float own = oacc[TD][RD];
+        const float other = __shfl_xor(own, 32);
+        l = lh == 0 ? own : other;
     }
     const float inv = 1.f / l;
 #pragma unroll
