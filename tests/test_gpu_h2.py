@@ -345,10 +345,12 @@ def test_gn_apply_h2(inplace):
     ref32 = torch.empty_like(t)
     chk(L().tcx_gn_apply_tab(dev(x).data_ptr(), ref32.data_ptr(), B, HW, C, sc.data_ptr(), sh.data_ptr(), 1, st()))
     r = ref32.cpu().numpy()
-    bad = np.argwhere(np.abs(got - r) > np.abs(r) * 2.0 ** -21 + 2.0 ** -25)
+    # the h2 apply computes SiLU on the hardware exp2 / rcp (as the conv prologues), the fp32 reference
+    # pass with IEEE expf and division: the h2 decode bound plus 8 fp32 ulps
+    bad = np.argwhere(np.abs(got - r) > np.abs(r) * (2.0 ** -21 + 8 * 2.0 ** -23) + 2.0 ** -25)
     if len(bad):
         print("mismatches", len(bad), bad[:8].tolist(), got[tuple(bad[0])], r[tuple(bad[0])])
-    dec_ok(got, r)
+    dec_ok(got, r, fp32_ulps=8)
     assert int(ovf.item()) == 0
 
 

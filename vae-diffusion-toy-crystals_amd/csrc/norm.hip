@@ -670,8 +670,8 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
             v1.x = fmaf(v1.x, sc[c0 + 4], sh[c0 + 4]); v1.y = fmaf(v1.y, sc[c0 + 5], sh[c0 + 5]);
             v1.z = fmaf(v1.z, sc[c0 + 6], sh[c0 + 6]); v1.w = fmaf(v1.w, sc[c0 + 7], sh[c0 + 7]);
             if (silu) {
-                v0.x = silu_f(v0.x); v0.y = silu_f(v0.y); v0.z = silu_f(v0.z); v0.w = silu_f(v0.w);
-                v1.x = silu_f(v1.x); v1.y = silu_f(v1.y); v1.z = silu_f(v1.z); v1.w = silu_f(v1.w);
+                v0.x = silu_hw(v0.x); v0.y = silu_hw(v0.y); v0.z = silu_hw(v0.z); v0.w = silu_hw(v0.w);
+                v1.x = silu_hw(v1.x); v1.y = silu_hw(v1.y); v1.z = silu_hw(v1.z); v1.w = silu_hw(v1.w);
             }
             uint2 h0, l0, h1, l1;
             split4x(v0, h0, l0, bf != 0);
@@ -693,8 +693,8 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
         v1.x = fmaf(v1.x, sc[c0 + 4], sh[c0 + 4]); v1.y = fmaf(v1.y, sc[c0 + 5], sh[c0 + 5]);
         v1.z = fmaf(v1.z, sc[c0 + 6], sh[c0 + 6]); v1.w = fmaf(v1.w, sc[c0 + 7], sh[c0 + 7]);
         if (silu) {
-            v0.x = silu_f(v0.x); v0.y = silu_f(v0.y); v0.z = silu_f(v0.z); v0.w = silu_f(v0.w);
-            v1.x = silu_f(v1.x); v1.y = silu_f(v1.y); v1.z = silu_f(v1.z); v1.w = silu_f(v1.w);
+            v0.x = silu_hw(v0.x); v0.y = silu_hw(v0.y); v0.z = silu_hw(v0.z); v0.w = silu_hw(v0.w);
+            v1.x = silu_hw(v1.x); v1.y = silu_hw(v1.y); v1.z = silu_hw(v1.z); v1.w = silu_hw(v1.w);
         }
         uint2 h0, l0, h1, l1;
         split4x(v0, h0, l0, bf != 0);

@@ -1127,11 +1127,8 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                 TCX_TRY(check_launch("k_first_gnsum"));
                 ns = 1;
                 TCX_TRY(gn_tab(net, P, 0, P.P0, C, gn, ns, st));
-                static const bool first_rec = [] {  // TCX_FIRST_REC=0: the LDS-tile form (A/B)
-                    const char* e = getenv("TCX_FIRST_REC");
-                    return !(e && e[0] == '0');
-                }();
-                if (first_rec && (H * W) % FR_PX == 0 && (FR_PX % W == 0 || W % FR_PX == 0)) {
+                // tile-free record kernel (r03_af: 143 -> 114 us at 64^2); the LDS-tile form for other shapes
+                if ((H * W) % FR_PX == 0 && (FR_PX % W == 0 || W % FR_PX == 0)) {
                     const int nrow = (FR_PX >= W ? FR_PX / W : 1) + 2;
                     const size_t shr = ((size_t)12 * C + (size_t)nrow * W) * sizeof(float);
                     hipLaunchKernelGGL(k_conv_first_rec, dim3(H * W / FR_PX, Bt), dim3(256), shr, st, x, B, H, W, C,
@@ -1249,11 +1246,8 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     {
         TCX_TRY(gn_tab(net, P, 10, P.P0, C, gn, ns, st));
         TCX_REQUIRE(C % 4 == 0, "head: C %% 4");
-        static const bool head_reg = [] {  // TCX_HEAD_REG=0: the LDS-weight k_head8 (A/B)
-            const char* e = getenv("TCX_HEAD_REG");
-            return !(e && e[0] == '0');
-        }();
-        if (head_reg && P.P0 % HPR == 0 && (C == 96 || C == 64 || C == 32)) {
+        // register-weight head (r03_ag: 124 -> 118 us at 64^2); k_head8 for other widths / shapes
+        if (P.P0 % HPR == 0 && (C == 96 || C == 64 || C == 32)) {
             const dim3 gr(Bt * P.P0 / HPR);
             if (C == 96) hipLaunchKernelGGL(k_head8r<3>, gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
             else if (C == 64) hipLaunchKernelGGL(k_head8r<2>, gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);

@@ -120,7 +120,6 @@ def _split_ok(x1, x2, C1, C2, ks, kpad, macs) -> bool:
 
 
 _SLOT_INIT = {}
-_PRODUCER_AMAX = os.environ.get("TCX_TRAIN_AMAX", "1") != "0"  # 0: every split operand gets its own absmax pass (A/B)
 
 
 def _scale_slot(device) -> torch.Tensor:
@@ -137,7 +136,7 @@ def _absmax_slot_for(x: torch.Tensor, C: int) -> torch.Tensor | None:
     """A slot for a producer kernel to raise with max |x| (tcx_gn_apply_tab_absmax / tcx_gn_bwd_absmax)
     when a split training conv may consume x (f16x3, channels % 32, a conv above the split threshold)."""
     from ._lib import conv_precision
-    if not (_PRODUCER_AMAX and _TRAIN_SPLIT and C % 32 == 0 and 9.0 * x.numel() * C >= _SPLIT_MIN_MACS
+    if not (_TRAIN_SPLIT and C % 32 == 0 and 9.0 * x.numel() * C >= _SPLIT_MIN_MACS
             and conv_precision() == "f16x3"):
         return None
     return _scale_slot(x.device)
