@@ -10,15 +10,20 @@ Inputs are synthetic (y_cat = i % 4, theta = linspace(0, pi/3, B), the save_sde_
 :317-321), weights random-init from torch.manual_seed(0), noise from in-kernel Philox; everything
 is resident in HBM before the timed region.
 
-Multi-GPU: one process per GPU (torchrun); sampling shards over independent images, so each rank
-samples its own 128 (weak scaling, no data-path collective); the only collectives are the timing
-barrier and the max-over-ranks reduction of the elapsed time.
+Multi-GPU: one process per GPU.  `--gpus N` without WORLD_SIZE starts the N ranks itself under
+torch.distributed.run (a child process, before any GPU call); under a launcher WORLD_SIZE is the
+world.  Rank r samples images [r*B, (r+1)*B) of ONE global batch of N*B (its conditioning slice and
+Philox element offset), so the N-GPU images are the 1-GPU images of batch N*B bit for bit (weak
+scaling, no data-path collective); the only collectives are the timing barriers and the
+max-over-ranks reduction of the elapsed time (and the image gather of --save-images, after timing).
 
 Also reports, on one JSON line:
-  roofline     — the dominant kernel (the implicit-GEMM conv, k_conv) timed live with HIP events around
-                 every launch in the timed region: achieved algorithmic (fp32-equivalent) TFLOP/s vs
-                 the peak of the MFMA it runs on — f16x3 split path (default): the 2.5 PFLOP/s dense
-                 f16 MFMA peak / 3 MFMA products per fp32 multiply-add = 833.3; fp32 path
+  roofline     — the split-path conv kernels (k_conv3lg / k_conv3g / k_conv4s2g / k_lin1x1), timed with
+                 HIP events around every conv launch on its own stream in a SEPARATE one-lane pass of the
+                 same K sampling passes after the timed region (`one_lane`; with 4 lanes' kernels co-running
+                 a per-launch event no longer times one kernel): achieved algorithmic (fp32-equivalent)
+                 TFLOP/s vs the peak of the MFMA it runs on — f16x3 split path (default): the 2.5 PFLOP/s
+                 dense f16 MFMA peak / 3 MFMA products per fp32 multiply-add = 833.3; fp32 path
                  (--precision fp32): the 157.3 TFLOP/s fp32 MFMA peak (MI355X_MICROARCH.md).
   fp32_path    — the same sampler with the fp32-MFMA convs (one lane), value + roofline, beside the f16x3 line.
   cpu_baseline — the reference's CPU arithmetic (oracle/score_model_torch.py: torch CPU ops) on the same
@@ -104,9 +109,33 @@ def cpu_baseline(state_dict, B: int, steps_a: int, steps_b: int, cfg: float, t_e
                       f"extrapolated to the {FWD_PER_IMG} calls of the 300-step run; torch threads {threads}"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher: run the N ranks under torch.distributed.run as
+    a CHILD process (never exec: nothing here has touched the GPU yet, and the ranks initialise it
+    themselves) with this script's own arguments; rank 0's JSON line goes to the inherited stdout."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    env.setdefault("OMP_NUM_THREADS", "1")  # torchrun would otherwise warn and set it itself
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (one rank each).  Without WORLD_SIZE in the environment, N > 1 "
+                         "launches `torch.distributed.run --nproc-per-node N` on this script as a child "
+                         "process (before any GPU call) and relays its JSON line and exit code; under "
+                         "torchrun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=3, help="timed sampling passes (each = 300 sampler steps)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
@@ -128,9 +157,16 @@ def main() -> int:
                          "(`fp32_path`; 0 skips)")
     ap.add_argument("--cpu-steps-a", type=int, default=2)
     ap.add_argument("--cpu-steps-b", type=int, default=4)
+    ap.add_argument("--save-images", default="",
+                    help="write the last timed pass's denoised images of ALL ranks (gathered in rank order) to "
+                         "this .npy file from rank 0 (tests: an N-rank run equals the 1-rank run of N x batch)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        return _spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     from toycrystals_amd.dist import all_reduce_, dist_backend, local_device
@@ -149,9 +185,13 @@ def main() -> int:
     model = CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=args.base_ch).to(device).eval()
     sde = VPSDE(beta_min=0.1, beta_max=30.0)
     B = args.batch
-    y_cat = (torch.arange(B) % 4).to(device)
-    y_cont = torch.zeros(B, 4, device=device)
-    y_cont[:, 1] = torch.linspace(0.0, math.pi / 3.0, B, device=device)
+    # rank r holds images [r*B, (r+1)*B) of ONE global batch of world*B (its conditioning slice and,
+    # in run(), its Philox element offset), so the gathered images equal a 1-GPU run of world*B
+    G = world * B
+    y_cat = (torch.arange(G) % 4)[rank * B:(rank + 1) * B].to(device)
+    y_cont = torch.zeros(G, 4)
+    y_cont[:, 1] = torch.linspace(0.0, math.pi / 3.0, G)
+    y_cont = y_cont[rank * B:(rank + 1) * B].to(device)
     S = args.img_size
     shape = (B, 1, S, S)
 
@@ -190,6 +230,7 @@ def main() -> int:
         run(-1 - i)
     torch.cuda.synchronize(device)
     elapsed = timed(lambda i: run(i))
+    timed_out = _last_out[0]
     L.tcx_set_sample_lanes(prev_lanes)
     # the precision the evaluator actually ran (bf16 falls back to f16x3 where the split attention does
     # not apply, a split run to fp32 after a range overflow): a line labelled with another is invalid
@@ -292,6 +333,16 @@ def main() -> int:
     }
     if fp32_path is not None:
         result["fp32_path"] = fp32_path
+    if args.save_images:
+        imgs = timed_out
+        if world > 1:
+            from toycrystals_amd.dist import all_gather_
+            bufs = [torch.empty_like(imgs) for _ in range(world)]
+            all_gather_(bufs, imgs.contiguous())
+            imgs = torch.cat(bufs, 0)
+        if rank == 0:
+            import numpy as np
+            np.save(args.save_images, imgs.cpu().numpy())
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model.state_dict(), args.cpu_batch, args.cpu_steps_a, args.cpu_steps_b,
                                               args.cfg, args.t_end)

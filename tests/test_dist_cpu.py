@@ -143,9 +143,15 @@ def _presence_worker(rank, world, port, q):
         never = torch.nn.Parameter(torch.ones(5))   # no rank produces a gradient
         ar = BucketedGradAllReduce([used, some, never], bucket_mb=1e-6)  # one bucket per parameter
         ok = True
-        for step in range(2):  # step 0 from grad None, step 1 from zero_grad()'s bucket views
+        # step 0 from grad None, step 1 from zero_grad()'s bucket views, step 2 from grads set to
+        # None again WITHOUT zero_grad() (opt.zero_grad(set_to_none=True)): the buckets still hold
+        # step 1's averages, which must not leak into the slot of a parameter this rank skipped
+        for step in range(3):
             if step == 1:
                 ar.zero_grad()
+            elif step == 2:
+                for p in (used, some, never):
+                    p.grad = None
             loss = (used * (rank + 1)).sum()
             if rank == 0:
                 loss = loss + (some * 4.0).sum()

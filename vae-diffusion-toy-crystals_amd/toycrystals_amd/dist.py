@@ -233,9 +233,14 @@ class BucketedGradAllReduce:
         ps, flat, n = self.buckets[bi]
         if len(self.arrived[bi]) == len(ps):
             flat[n:].fill_(1.0)
-        else:  # some parameter got no gradient on this rank: presence 0 in its slot (zeros in its data)
+        else:  # some parameter got no gradient on this rank: presence 0 in its slot, zeros in its data
             pres = torch.tensor([1.0 if id(p) in self.arrived[bi] else 0.0 for p in ps], dtype=flat.dtype)
             flat[n:].copy_(pres)
+            # A step not begun with zero_grad() (e.g. opt.zero_grad(set_to_none=True)) leaves the
+            # previous step's averaged gradient in the slice: it must not enter this sum.
+            for p in ps:
+                if id(p) not in self.arrived[bi]:
+                    self._view(p).zero_()
         self.works[bi] = all_reduce_(flat, group=self.group, async_op=True)
 
     def _launch_ready(self) -> None:
