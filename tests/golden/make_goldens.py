@@ -476,6 +476,109 @@ def gen_train_prior(name: str) -> None:
          T=np.int64(200), beta_end=np.float64(1.0), **ck, **grads)
 
 
+def gen_train_prior_w1024(name: str) -> None:
+    """Config 4's prior training step at its size (train_diffusion_prior.py:251-277 over
+    diffusion_prior.py:39-127): DiffusionPriorFiLM width 1024, 8 blocks (103 M parameters),
+    T = 1000 (beta 1e-4 .. 0.05), B = 32; t = clamp(long(u^2 T)), q_sample, MSE, backward.
+    Seeded weights (not stored) with perturbed LayerNorm affines (stored: 18 x 1024 values);
+    gradients as checksums + 256 fixed-index samples per tensor (full for tensors <= 4096)."""
+    torch.manual_seed(0)
+    model = ref_prior.DiffusionPriorFiLM(z_dim=32, n_types=4, y_cont_dim=4, t_emb_dim=64, width=1024, n_blocks=8,
+                                         y_cat_emb_dim=64)
+    ck = sd_checksums(model)  # of the seeded init, before the norm perturbation
+    perturb_norms(model, 17)
+    norms = {"w/" + k: v.detach().numpy().copy() for k, v in model.state_dict().items() if ".norm" in k or "norm" in k.split(".")[-2]}
+    model.train()
+    T = 1000
+    sched = ref_prior.DiffusionSchedule.linear(T=T, beta_start=1e-4, beta_end=0.05, device=torch.device("cpu"))
+    g = torch.Generator().manual_seed(71)
+    B = 32
+    z0 = torch.randn(B, 32, generator=g)
+    y_cat = torch.tensor([i % 4 for i in range(B)])
+    y_cont = torch.zeros(B, 4)
+    y_cont[:, 1] = torch.rand(B, generator=g) * (math.pi / 3)
+    torch.manual_seed(81)
+    u = torch.rand((B,))
+    t = torch.clamp((u ** 2 * T).long(), 0, T - 1)
+    eps = torch.randn_like(z0)
+    z_t = sched.q_sample(z0=z0, t=t, eps=eps)
+    eps_pred = model(z_t, t, y_cat, y_cont)
+    loss = torch.mean((eps_pred - eps) ** 2)
+    loss.backward()
+    gs = {}
+    for k, p in model.named_parameters():
+        a = p.grad.detach().double().reshape(-1).numpy()
+        gs["gck/" + k] = np.array([a.sum(), np.abs(a).sum(), float(np.abs(a).max())])
+        if a.size <= 4096:
+            gs["g/" + k] = p.grad.detach().numpy().copy()
+        else:
+            idx = np.sort(np.random.RandomState(len(k) * 7919 + a.size % 100003).choice(a.size, size=256, replace=False))
+            gs["gi/" + k] = idx.astype(np.int64)
+            gs["gs/" + k] = a[idx].astype(np.float32)
+    save(name, z0=z0.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), u=u.numpy(), t=t.numpy(), eps=eps.numpy(),
+         z_t=z_t.detach().numpy(), eps_pred=eps_pred.detach().numpy(), loss=np.float64(loss.item()),
+         T=np.int64(T), beta_end=np.float64(0.05), norm_seed=np.int64(17), **ck, **norms, **gs)
+
+
+def gen_bf16_emulated(name: str) -> None:
+    """Error model for config 5's bf16 path ("bf16 MFMA conv-as-GEMM", BASELINE.json configs[4]):
+    the REFERENCE's own 300-step reverse SDE (CFG 1.5, t_end 0.005) on the trained base-96 model with
+    the recorded draws of sde96_trained_300, but with every conv operand rounded to bf16 (RNE) and
+    fp32 accumulation — each nn.Conv2d's weight once and its input at every call (forward
+    pre-hook), the bias kept fp32 — and the attention's q, k, v and softmax P rounded to bf16 (the
+    operands of the two bf16 MFMA products).  Its distance from the fp32 run is the drift bf16
+    operand rounding alone causes on this trajectory; the GPU test gates the bf16 path at 2x it."""
+    import torch.nn.functional as Fn
+    sd = {k: torch.from_numpy(v) for k, v in np.load(os.path.join(HERE, "trained96_ema.npz")).items()}
+    torch.manual_seed(0)
+    model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=96)
+    model.load_state_dict(sd)
+    model.eval()
+    bf = lambda t: t.to(torch.bfloat16).to(torch.float32)  # noqa: E731
+    hooks = []
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, torch.nn.Conv2d):
+                m.weight.copy_(bf(m.weight))
+                hooks.append(m.register_forward_pre_hook(lambda mod, inp: (bf(inp[0]),) + tuple(inp[1:])))
+    sdpa = Fn.scaled_dot_product_attention
+
+    def sdpa_bf16(q, k, v, *a, **kw):
+        assert not a and not kw
+        s = bf(q) @ bf(k).transpose(-2, -1) / math.sqrt(q.shape[-1])
+        return bf(torch.softmax(s, dim=-1)) @ bf(v)
+
+    Fn.scaled_dot_product_attention = sdpa_bf16
+    try:
+        sde = ref_sde.VPSDE(beta_min=0.1, beta_max=30.0)
+        B, steps, H = 8, 300, 64
+        y_cat = torch.tensor([i % 4 for i in range(B)], dtype=torch.int64)
+        y_cont = torch.zeros(B, 4)
+        y_cont[:, 1] = torch.linspace(0.0, math.pi / 3, B)
+        shape = (B, 1, H, H)
+        seed = 1234
+        t0 = time.time()
+        torch.manual_seed(seed)
+        with torch.no_grad():
+            out = ref_sde.sample_reverse_sde_euler_maruyama(model=model, sde=sde, y_cat=y_cat, y_cont=y_cont,
+                                                            img_shape=shape, n_steps=steps, guidance_scale=1.5,
+                                                            t_end=0.005)
+            torch.manual_seed(seed)
+            x0 = _unclamped(model, sde, y_cat, y_cont, shape, steps, 1.5, 0.005, "sde")
+        print(f"  {name}: bf16-emulated reference sampler {time.time() - t0:.1f}s")
+    finally:
+        Fn.scaled_dot_product_attention = sdpa
+        for h in hooks:
+            h.remove()
+    ref = np.load(os.path.join(HERE, "sde96_trained_300.npz"))
+    assert int(ref["noise_seed"]) == seed and int(ref["B"]) == B
+    d = np.abs(out.numpy() - ref["out"])
+    print(f"  emulated bf16 vs fp32 reference: image max {d.max():.3e} mean {d.mean():.3e} "
+          f"p99 {np.quantile(d, 0.99):.3e} off>1e-2 {100 * (d > 1e-2).mean():.2f} %")
+    save(name, out=out.numpy(), x0_unclamped=x0.numpy(), noise_seed=np.int64(seed), B=np.int64(B),
+         steps=np.int64(steps))
+
+
 def main() -> int:
     torch.set_num_threads(8)
     which = set(sys.argv[1:])
@@ -528,6 +631,10 @@ def main() -> int:
         gen_train_score("train16_b3")
         gen_train_vae("train_condvae_b4")
         gen_train_prior("train_prior_w64")
+    if want("bf16emu"):
+        gen_bf16_emulated("sde96_trained_300_bf16emu")
+    if want("train_prior_w1024"):
+        gen_train_prior_w1024("train_prior_w1024_b32")
     return 0
 
 

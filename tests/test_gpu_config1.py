@@ -65,3 +65,86 @@ def test_config1_train_vae_5k_b128_vs_reference_cpu_run(tmp_path, golden):
         worst = max(worst, (e, k))
     print(f"final parameters (64 sampled entries per tensor): worst {worst[1]} differs by {worst[0]:.3e} lr")
     assert worst[0] < 1.0
+
+
+def test_config1_teacher_forced_gradients_vs_reference(golden):
+    """Where the mirror's CondVAE training step could depart from the reference's, separated from
+    trajectory drift: at steps 1, 2, 10 and 38 of the config-1 run both implementations evaluate the
+    SAME parameters (the reference's parameters before that step, rebuilt from int8 codes around the
+    seeded init, tests/golden/make_config1_grads.py) on the same batch (recorded item order, rendered
+    here: uint8-exact, float within 1 ulp) and reparameterisation draw.  Everything may then differ
+    by fp32 rounding only: gates 1e-5 relative on loss / recon / kl_used / kl_raw, 1e-5 of the
+    tensor's max on mu, logvar, x_hat samples, the step-1 encoder activations and every gradient
+    tensor's entries (all of a tensor <= 4096 entries, else 1,024 random + its 64 largest), 1e-5
+    relative on each gradient's sum of squares.  /root/reference/scripts/train_vae.py:17-36,292-321."""
+    import torch
+    from toycrystals_amd import functional as TF
+    from toycrystals_amd.data import ToyCrystalsDataset
+    from toycrystals_amd.models.vae import CondVAE
+    g = golden("config1_grads")
+    c = golden("config1_vae_5k_b128")
+    seed, n, img, B, z, lr, beta, fb = c["cfg"]
+    B, z = int(B), int(z)
+    torch.manual_seed(int(seed))
+    m = CondVAE(z_dim=z, n_types=4, y_cont_dim=4, cond_drop=0.0)
+    init = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    for k, v in init.items():
+        ck = g["init_ck/" + k]
+        assert abs(float(v.double().sum()) - ck[0]) <= 1e-9 * max(1.0, ck[1]), k
+    m = m.cuda().train()
+    ds = ToyCrystalsDataset(n_samples=int(n), img_size=int(img), seed=int(seed), device="cuda")
+    U = float(g["unit"][0])
+    b = float(beta) * min(1.0, 1.0 / 5.0)
+    fails = []
+
+    def gate(label, got, ref, scale, tol=1e-5):
+        e = float(np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64)).max()) / max(float(scale), 1e-30)
+        if e > tol:
+            fails.append((label, e))
+        return e
+
+    for s in [int(v) for v in g["steps"]]:
+        sd = {}
+        for k, v in init.items():
+            sd[k] = v.clone() if s == 1 else (v.double() + torch.from_numpy(g[f"q{s}/{k}"]).double() * U).float()
+        m.load_state_dict(sd)
+        idx = [int(i) for i in c["order"][(s - 1) * B: s * B]]
+        x, y_cat, y_cont = ds.render(idx)
+        eps = torch.from_numpy(c["eps"][s - 1]).cuda()
+        for p in m.parameters():
+            p.grad = None
+        x_hat, mu, lv = m(x, y_cat, y_cont, draws=(eps, None))
+        recon = TF.mse_loss(x_hat, x)
+        ku, kr = TF.kl_stats(mu, lv, float(fb))
+        loss = recon + b * ku
+        loss.backward()
+        sc = np.array([float(loss), float(recon), float(ku), float(kr)])
+        ref = g[f"sc{s}"]
+        e_sc = np.abs(sc - ref) / np.abs(ref)
+        for j, name in enumerate(("loss", "recon", "kl_used", "kl_raw")):
+            if e_sc[j] > 1e-5:
+                fails.append((f"step {s} {name}", float(e_sc[j])))
+        e_mu = gate(f"step {s} mu", mu.detach().cpu().numpy(), g[f"mu{s}"], np.abs(g[f"mu{s}"]).max())
+        e_lv = gate(f"step {s} logvar", lv.detach().cpu().numpy(), g[f"lv{s}"], np.abs(g[f"lv{s}"]).max())
+        xa = x_hat.detach().cpu().numpy().ravel()
+        e_xh = gate(f"step {s} x_hat", xa[g[f"xh{s}_idx"]], g[f"xh{s}"], 1.0)
+        worst = (0.0, "")
+        for k, p in m.named_parameters():
+            ga = p.grad.detach().double().cpu().numpy().ravel()
+            st = g[f"gst{s}/{k}"]
+            e = gate(f"step {s} grad {k}", ga[g[f"gi{s}/{k}"]], g[f"gv{s}/{k}"], st[2])
+            e2 = abs(float((ga * ga).sum()) - st[1]) / max(st[1], 1e-30)
+            if e2 > 1e-5:
+                fails.append((f"step {s} grad {k} sumsq", e2))
+            worst = max(worst, (max(e, e2), k))
+        print(f"step {s:2d}: scalars {e_sc.max():.1e}, mu {e_mu:.1e}, logvar {e_lv:.1e}, x_hat {e_xh:.1e}, "
+              f"worst gradient {worst[1]} {worst[0]:.1e} of its max")
+        if s == 1:
+            with torch.no_grad():
+                h = x.float().contiguous().view(B, x.shape[2], x.shape[3], 1)
+                for j, i in enumerate((0, 2, 4, 6)):
+                    h = TF.act(TF.conv2d(h, None, m.enc[i]), TF.ACT_RELU)
+                    a = h.permute(0, 3, 1, 2).contiguous().double().cpu().numpy().ravel()  # NCHW flat index
+                    ea = gate(f"step 1 enc act {j}", a[g[f"act/{j}_idx"]], g[f"act/{j}"], np.abs(g[f"act/{j}"]).max())
+                    print(f"  encoder activation {j} (after enc.{i} + ReLU): {ea:.1e} of its max")
+    assert not fails, fails

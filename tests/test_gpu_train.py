@@ -513,3 +513,54 @@ def test_prior_training_step_vs_reference(golden):
         ref = gd["g/" + k]
         got = p.grad.detach().cpu().numpy()
         assert float(np.abs(got - ref).max()) <= 1e-4 * max(float(np.abs(ref).max()), 1e-6), k
+
+
+def test_prior_training_step_w1024_vs_reference(golden):
+    """Config 4's prior training step at its size (train_diffusion_prior.py:251-277 over
+    diffusion_prior.py:39-127): width 1024 x 8 FiLM blocks (103 M parameters), T = 1000, B = 32,
+    perturbed LayerNorm affines.  Gates: eps_pred 2e-5, loss 1e-5 relative, every gradient tensor's
+    sampled entries (all of it for tensors <= 4096) within 1e-4 of that tensor's max |g|, and its
+    sum within 1e-4 of its |g| sum."""
+    from toycrystals_amd import functional as TF
+    from toycrystals_amd._lib import check, lib, ptr, stream_ptr
+    from toycrystals_amd.models.diffusion_prior import DiffusionPriorFiLM, DiffusionSchedule
+    gd = golden("train_prior_w1024_b32")
+    torch.manual_seed(0)
+    m = DiffusionPriorFiLM(z_dim=32, n_types=4, y_cont_dim=4, t_emb_dim=64, width=1024, n_blocks=8, y_cat_emb_dim=64)
+    _check_checksums(m, gd)
+    with torch.no_grad():
+        sd = m.state_dict()
+        for key in gd:
+            if key.startswith("w/"):
+                sd[key[2:]].copy_(torch.from_numpy(gd[key]))
+    m = m.cuda().train()
+    T = int(gd["T"])
+    sched = DiffusionSchedule.linear(T=T, beta_start=1e-4, beta_end=float(gd["beta_end"]), device=torch.device("cuda"))
+    z0, eps, u = cu(gd["z0"]), cu(gd["eps"]), cu(gd["u"])
+    B, Z = z0.shape
+    t = torch.empty((B,), device="cuda", dtype=torch.int64)
+    z_t = torch.empty_like(z0)
+    check(lib().tcx_prior_qsample(ptr(z0), ptr(eps), ptr(u), ptr(sched.sqrt_alpha_bars),
+                                  ptr(sched.sqrt_one_minus_alpha_bars), T, B, Z, ptr(t), ptr(z_t), stream_ptr()), "qs")
+    assert torch.equal(t.cpu(), torch.from_numpy(gd["t"]))
+    assert err(z_t, torch.from_numpy(gd["z_t"])) < 2e-6
+    eps_pred = m(z_t, t, cu(gd["y_cat"], torch.int64), cu(gd["y_cont"]))
+    loss = TF.mse_loss(eps_pred, eps)
+    loss.backward()
+    e_pred = err(eps_pred, torch.from_numpy(gd["eps_pred"]))
+    e_loss = abs(float(loss.detach()) - float(gd["loss"])) / float(gd["loss"])
+    worst = (0.0, "")
+    for k, p in m.named_parameters():
+        g = p.grad.detach().double().cpu().reshape(-1).numpy()
+        ck = gd["gck/" + k]
+        if "g/" + k in gd:
+            ref, got = gd["g/" + k].reshape(-1).astype(np.float64), g
+        else:
+            ref, got = gd["gs/" + k].astype(np.float64), g[gd["gi/" + k]]
+        e = float(np.abs(got - ref).max()) / max(float(ck[2]), 1e-12)
+        es = abs(float(g.sum()) - float(ck[0])) / max(float(ck[1]), 1e-12)
+        worst = max(worst, (max(e, es), k))
+        assert e <= 1e-4 and es <= 1e-4, (k, e, es)
+    print(f"w1024x8 prior step: eps_pred {e_pred:.2e}, loss {e_loss:.2e} relative, worst gradient {worst[1]} "
+          f"{worst[0]:.2e} of its max")
+    assert e_pred < 2e-5 and e_loss <= 1e-5

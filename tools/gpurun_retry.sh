@@ -3,7 +3,7 @@
 # an infrastructure "status=transient" outcome (nothing ran, nothing charged); any real result,
 # failure or refusal is returned as is.  usage: tools/gpurun_retry.sh <timeout-s> <command>
 T=$1; shift
-for i in 1 2 3 4 5 6; do
+for i in $(seq 1 20); do
     out=$(timeout $((T + 900)) /usr/local/graft/bin/gpurun --timeout "$T" -- "$@" 2>&1)
     rc=$?
     echo "$out" | grep -v "every call sends" | tail -3

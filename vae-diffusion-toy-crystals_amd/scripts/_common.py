@@ -45,6 +45,21 @@ def lead_only_rng(device):
     return torch.random.fork_rng(devices=[device])
 
 
+def sync_rng_from_lead(world: int, device) -> None:
+    """Every rank adopts rank 0's torch CPU and device generator states (identity at world 1).
+    For work rank 0 does ALONE whose draws the one-GPU run also makes (the latent-cache build with
+    --z-target sample): the one-GPU run's generators have advanced by those draws, so the ranks
+    must continue from rank 0's advanced state, not roll it back."""
+    if world <= 1:
+        return
+    st = [None]
+    if dist.get_rank() == 0:
+        st = [(torch.get_rng_state(), torch.cuda.get_rng_state(device))]
+    dist.broadcast_object_list(st, src=0)
+    torch.set_rng_state(st[0][0])
+    torch.cuda.set_rng_state(st[0][1], device)
+
+
 def shutdown_dp(world: int) -> None:
     if world > 1 and dist.is_initialized():
         dist.barrier()

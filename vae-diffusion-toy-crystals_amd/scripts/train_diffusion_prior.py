@@ -144,6 +144,9 @@ def main() -> int:
             print(f"saved latents: {args.latent_cache}  z0={tuple(z0.shape)}")
         latents = [z0, y_cat, y_cont, z_mean, z_std]
     z0, y_cat, y_cont, z_mean, z_std = _common.broadcast_from_lead(latents, world, device)
+    # rank 0's build drew reparameterisation noise (--z-target sample) as the one-GPU run does:
+    # continue every rank from its generator state so the --global-draws streams stay equal
+    _common.sync_rng_from_lead(world, device)
     z0n = ((z0 - z_mean) / z_std).to(device).contiguous()
     y_cat_d, y_cont_d = y_cat.to(device).contiguous(), y_cont.to(device).contiguous()
     prior = DiffusionPriorFiLM(z_dim=args.z_dim, n_types=args.n_types, y_cont_dim=args.y_cont_dim,

@@ -183,7 +183,23 @@ def main() -> int:
             raise SystemExit("--replay-draws covers the conditional VAE with --cond-drop 0 (reparameterise draws only)")
     dl = DeviceBatches(ds, args.batch_size, device, shuffle=True, drop_last=True, rank=rank, world=world,
                        fixed_order=None if replay is None else replay["order"])
+    if replay is not None:  # the recording must cover every step of this run at this batch size
+        need = args.epochs * len(dl)
+        if replay["eps"].ndim != 3 or replay["eps"].shape[0] < need or replay["eps"].shape[1] != args.batch_size \
+                or replay["eps"].shape[2] != args.z_dim:
+            raise SystemExit(f"--replay-draws: eps {tuple(replay['eps'].shape)} does not cover {args.epochs} epoch(s) x "
+                             f"{len(dl)} steps of batch {args.batch_size}, z_dim {args.z_dim}")
+        if args.epochs > 1:
+            raise SystemExit("--replay-draws records ONE epoch's item order: run it with --epochs 1")
     step_log = open(os.path.join("results", "vae_steps.jsonl"), "w", encoding="utf-8") if (replay and lead) else None
+    try:
+        return _train(args, rank, world, device, lead, ds, dl, replay, step_log)
+    finally:
+        if step_log is not None:
+            step_log.close()
+
+
+def _train(args, rank, world, device, lead, ds, dl, replay, step_log) -> int:
     if args.uncond:
         model = VAE(z_dim=args.z_dim).to(device)
     else:
