@@ -233,21 +233,24 @@ def test_bf16_sde_256px_vs_reference(golden, bf16):
 
 
 def test_bf16_trained_sde300_trajectory_drift(golden):
-    """How far the bf16 path's 300-step reverse SDE (CFG 1.5, t_end 0.005) drifts from the fp32-grade
-    f16x3 trajectory and from the reference's own fp32 run, on the trained base-96 model
+    """The bf16 path's 300-step reverse SDE (CFG 1.5, t_end 0.005) on the trained base-96 model
     (trained96_ema, B = 8, the reference's recorded draws; /root/reference/src/toycrystals/models/
-    sde_score_model.py:507-569).  Measured (r03_a): the image differs from the f16x3 trajectory by
-    2.4e-3 mean-abs, but single pixels by up to 0.33 (x0_hat up to 0.62 of its scale): the per-step
-    bf16 rounding (~7e-3 of a forward) is absorbed on most of the image and amplified at a few
-    unstable pixels of the stochastic trajectory (p99 4.7e-2, p99.9 0.15, 4.5 % of the pixels off by
-    more than 1e-2).  Stated bounds vs both references: image mean-abs <= 5e-3, max-abs <= 0.5, p99 <=
-    0.1, at most 8 % of the pixels off by more than 1e-2 (printed)."""
+    sde_score_model.py:507-569) against the reference's fp32 run, gated by an ERROR MODEL: the
+    reference's own run of the same trajectory with every conv operand and the attention's q, k, v, P
+    rounded to bf16 and fp32 accumulation (tests/golden/make_goldens.py gen_bf16_emulated,
+    sde96_trained_300_bf16emu.npz) drifts from its fp32 run by image mean-abs 3.0e-3, p99 3.4e-2,
+    max 0.25, 6.7 % of the pixels off by more than 1e-2: per-step bf16 rounding (~7e-3 of a forward)
+    is absorbed on most of the image and amplified at a few unstable pixels of the stochastic
+    trajectory.  Gate: each of those four statistics of the bf16 path vs the fp32 reference at most
+    2x the emulated reference's (printed), and the fp32-grade f16x3 path on the same run within 1e-4."""
     from test_gpu_models import run_sde, unet
     from toycrystals_amd import _lib
     from toycrystals_amd.models.sde_score_model import host_noise
     g = golden("sde96_trained_300")
+    emu = golden("sde96_trained_300_bf16emu")
     m = unet(96, golden("trained96_ema"))
     B, steps = int(g["B"]), int(g["steps"])
+    assert int(emu["B"]) == B and int(emu["noise_seed"]) == int(g["noise_seed"]) and int(emu["steps"]) == steps
     torch.manual_seed(int(g["noise_seed"]))
     noise = host_noise((B, 1, 64, 64), steps + 1).cuda()
     old = _lib.conv_precision()
@@ -258,16 +261,19 @@ def test_bf16_trained_sde300_trajectory_drift(golden):
         out_bf, x0_bf = run_sde(m, g, noise, (B, 1, 64, 64))
     finally:
         _lib.set_conv_precision(old)
-    scale = max(1.0, float(np.abs(g["x0_unclamped"]).max()))
-    for what, ref_img, ref_x0 in (("f16x3", out_h2, x0_h2), ("reference fp32", g["out"], g["x0_unclamped"])):
-        d = np.abs(out_bf - ref_img)
-        x0e = float(np.abs(x0_bf - ref_x0).max()) / scale
-        off = float((d > 1e-2).mean())
-        print(f"bf16 300-step vs {what}: image max-abs {float(d.max()):.3e} mean-abs {float(d.mean()):.3e}, "
-              f"p99 {float(np.quantile(d, 0.99)):.3e}, p99.9 {float(np.quantile(d, 0.999)):.3e}, "
-              f"pixels off by > 1e-2: {100 * off:.2f} %, x0_hat rel {x0e:.3e}")
-        assert float(d.mean()) <= 5e-3 and float(d.max()) <= 0.5 and off <= 0.08
-        assert float(np.quantile(d, 0.99)) <= 0.1
+
+    def stats(img):
+        d = np.abs(img - g["out"])
+        return {"mean": float(d.mean()), "p99": float(np.quantile(d, 0.99)), "max": float(d.max()),
+                "off": float((d > 1e-2).mean())}
+    model, got = stats(emu["out"]), stats(out_bf)
+    for k in model:
+        print(f"bf16 300-step vs fp32 reference, {k}: bf16 path {got[k]:.3e}, bf16-emulated reference "
+              f"{model[k]:.3e} (gate {2 * model[k]:.3e})")
+    d_emu = np.abs(out_bf - emu["out"])
+    print(f"bf16 path vs the bf16-emulated reference: mean {float(d_emu.mean()):.3e} max {float(d_emu.max()):.3e}")
+    for k in model:
+        assert got[k] <= 2.0 * model[k], (k, got[k], model[k])
     assert float(np.abs(out_h2 - g["out"]).max()) < 1e-4  # the fp32-grade path on the same run
     assert float(np.abs(out_bf - out_h2).max()) > 1e-5  # really the bf16 path
 

@@ -18,7 +18,13 @@ enc.4.bias 0.36 lr on the r03_i box, 1.8e-2 of that tensor's scale).  The KL ter
 gradient of kl_used is zero for every latent dim below the threshold, so which dims sit above it is
 decided by rounding-level differences late in the epoch (observed |d kl_used| 4e-3 of 1.6, |d kl_raw|
 1.3e-2 of 0.7 at step 38 on the r03_b box; 1.66e-2 / 1.66e-2 on the r03_i box, where the loss still
-agreed to 1.6e-5; beta * kl is 1 % of the loss): gates 5e-2 nats for both (3 % of kl_used)."""
+agreed to 1.6e-5; beta * kl is 1 % of the loss): gates 5e-2 nats for both (3 % of kl_used).
+
+Why these trajectory gates are wider than rounding, with evidence: the teacher-forced test below
+evaluates the mirror and the reference on the SAME parameters (the reference's own, before steps 1, 2,
+10 and 38), batch and draw; there every gradient tensor agrees to <= 7e-6 of its max, mu / logvar to
+4e-7, the loss terms to 6e-7 (r04_b, profiles/r04_b_tests.log) — the backward is the reference's to
+rounding, and the drift above is Adam carrying rounding-level differences along the trajectory."""
 import json
 import os
 import subprocess
