@@ -39,6 +39,11 @@ int tcx_version(void);
  * time, the launch count and the summed algorithmic FLOPs (2*M*Cout*ks^2*Cin per launch). */
 int tcx_prof_enable(int on);
 int tcx_prof_read(double* total_ms, long long* launches, double* flops);
+/* Diagnostic timeline of the 16x16x32 3x3 conv (k_conv3m): with buf non-null, each of the first n
+ * workgroups of every later launch writes 8 u64 at buf[8 * workgroup]: s_memrealtime (100 MHz) at
+ * entry, prologue done, tap loop done, epilogue stores issued and exit, s_memtime at entry and at
+ * loop end, and HW_ID | XCC_ID << 16.  buf = NULL (the default) turns it off.  Test / profiling only. */
+int tcx_debug_conv_stamps(void* buf, int n);
 
 /* ------------------------------------------------------------------ primitive ops */
 

@@ -456,3 +456,23 @@ def test_unet_range_fallback_to_fp32():
     finally:
         _lib.set_conv_precision(old)
     assert torch.equal(e, e32)
+
+
+@pytest.mark.parametrize("H,Ci,Co", [(64, 96, 96), (32, 192, 192), (16, 192, 192), (64, 32, 96)])
+def test_conv_h2_16x16_kernel_bmod_act_out_h2_gn(H, Ci, Co):
+    """The h2-source 3x3 conv on v_mfma_f32_16x16x32_f16 (k_conv3m: rows of 16 / 32 / 64 px, one or
+    several 16-channel chunk pairs) with CFG batch aliasing (bmod), SiLU epilogue, h2 output and fused
+    GroupNorm partials, against the fp64 oracle at the fp32 conv's gate."""
+    x = rng.standard_normal((2, Ci, H, H))
+    w = rng.standard_normal((Co, Ci, 3, 3)) / np.sqrt(Ci * 9)
+    b = rng.standard_normal(Co)
+    xx = np.concatenate([x, x], 0)
+    ref = nn_np.conv2d(xx, w, b, padding=1, mode="circular")
+    ref = ref / (1 + np.exp(-ref))
+    got, part = run_conv_h2(x, w, b, 1, 1, True, bmod=2, Bt=4, act=3, gn=True, out_h2=True)
+    fp32 = run_conv(x, w, b, 1, 1, True, bmod=2, Bt=4, act=3)
+    fp32_grade(got, fp32, ref)
+    s = part.sum(axis=1)
+    r = ref.reshape(4, Co, -1)
+    np.testing.assert_allclose(s[..., 0], r.sum(-1), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[..., 1], (r * r).sum(-1), rtol=1e-5, atol=1e-3)

@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Per-position kernel timing of one U-Net evaluation from a rocprofv3 rocpd database (kernel trace
+of a one-lane sampling pass): evaluations start at k_first_acf; median duration per position.
+usage: rocpd_layers.py run_results.db [out.txt]"""
+import collections
+import sqlite3
+import statistics
+import sys
+
+
+def short(n: str) -> str:
+    n = n.replace("void ", "").replace("tcx::(anonymous namespace)::", "")
+    return n.split("(tcx::")[0].split("(float")[0].split("(double")[0].split("(int")[0].split("(unsigned")[0][:60]
+
+
+def main() -> int:
+    db = sqlite3.connect(sys.argv[1])
+    rows = db.execute("select name, start, end, grid_x from kernels order by start").fetchall()
+    rows = [r for r in rows if "tcx::" in r[0]]
+    seq, cur = [], []
+    for r in rows:
+        if "k_first_acf" in r[0] and cur:
+            seq.append(cur)
+            cur = []
+        cur.append(r)
+    seq.append(cur)
+    L = collections.Counter(len(s) for s in seq).most_common(1)[0][0]
+    ev = [s for s in seq if len(s) == L][5:]
+    out = open(sys.argv[2], "w") if len(sys.argv) > 2 else sys.stdout
+    tot = 0.0
+    for i in range(L):
+        d = statistics.median((s[i][2] - s[i][1]) / 1e3 for s in ev)
+        tot += d
+        print(f"{i:2d} {short(ev[0][i][0]):60s} grid={ev[0][i][3]:>8d} {d:9.1f} us", file=out)
+    span = statistics.median((s[-1][2] - s[0][1]) / 1e3 for s in ev)
+    print(f"sum of kernel medians {tot:.1f} us; first-start..last-end {span:.1f} us per eval ({len(ev)} evals)", file=out)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

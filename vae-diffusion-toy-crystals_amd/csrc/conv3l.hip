@@ -855,7 +855,12 @@ int launch3lg16(const ConvParams& p, hipStream_t st) {
     return check_launch("tcx_conv2d_h2(halo 3lg16)");
 }
 
+// conv3m.hip: the h2-source form on v_mfma_f32_16x16x32_f16
+bool conv3m_takes(const ConvParams& p);
+int launch_conv3m(const ConvParams& p, hipStream_t st);
+
 int launch_conv3l(const ConvParams& p, hipStream_t st) {
+    if (conv3m_takes(p)) return launch_conv3m(p, st);
     if (p.W == 16) return launch3lg16<0>(p, st);
     return p.W == 64 ? launch3l<64>(p, st) : launch3l<32>(p, st);
 }

@@ -1,0 +1,446 @@
+// k_conv3m: the U-Net's 3x3 stride-1 circular conv with h2 sources at rows of 16 / 32 / 64 pixels
+// (every _ConvBlock / us*_conv conv without a GroupNorm prologue: /root/reference/src/toycrystals/
+// models/sde_score_model.py:102,105,218,222) on v_mfma_f32_16x16x32_f16 instead of k_conv3lg's
+// v_mfma_f32_32x32x16_f16.
+//
+// Why: at equal FLOPs and equal LDS bytes per FLOP the 16x16x32 loop runs 1.12x the 32x32x16 loop
+// on this chip (tools/probe/mfma_shape_probe.hip, profiles/r04_b_mfma_shape.log: 1,670 vs 1,490
+// TFLOP/s of f16 MFMA on random operands read from LDS; MI355X_MICROARCH.md "DVFS give-back" item 7
+// measured the same for bf16): the smaller MFMA holds a higher clock under load.
+//
+// Same tile (256 pixels x 96 output channels, 4 waves of 64 pixels), the same LDS-DMA staging with
+// split wave roles as k_conv3lg (waves 0-1 move the fragment-ordered weights, waves 2-3 the halo:
+// no wave's vmcnt mixes L2 and HBM loads), the same 16-channel halo chunks (64-B h2 slots) and the
+// same weight copy (tcx_pack_conv_weight_h2_frag).  What changes is the unit of work: a 32-deep
+// MFMA k step is a PAIR of taps of the global tap sequence c = 9 j + t (j chunk, t tap), k = 2 q and
+// 2 q + 1 — exactly the weight ring's pair — with lanes 0-31 reading tap 2q and lanes 32-63 tap
+// 2q + 1 (the A operand's k = 8 (lane >> 4) + e: k blocks 0, 1 = channels 0-7, 8-15 of the first
+// tap, 2, 3 of the second).  Two chunks = 18 taps = 9 pairs (q = 0..8), one of which (q = 4) pairs
+// tap 8 of the even chunk with tap 0 of the odd one: the loop body is that 9-pair period with every
+// lane's halo address a precomputed VGPR per pair type (aq[q]) plus an immediate per 16-pixel
+// row block.
+//
+// Per wave: 4 row blocks (16 px) x 6 column blocks (16 channels) of 16x16 accumulators, 3 MFMAs
+// (hi.lo, lo.hi, hi.hi) each per pair = 72 MFMAs per pair in two halves by column blocks 0-2 / 3-5,
+// one barrier per pair between them:
+//   H1: ds_read B(k, cols 3-5) -> set 1 | 36 MFMAs with A(k), B set 0
+//   mid: lgkmcnt(0) [+ weight waves vmcnt(0): pair k+1 landed; halo waves at q = 3 / 8: chunk landed]
+//        s_barrier; weight waves DMA pair k+2 into slot k & 1 (its B fragments are all in registers);
+//        halo waves DMA a third of the next chunk when its buffer has been freed
+//   H2: ds_read B(k+1, cols 0-2) -> set 0 | per row block: 9 MFMAs with B set 1, then A(k+1) of
+//       that row block (its last use of A(k) has issued)
+// Halo of chunk J (buffer J & 1) is issued in thirds at the mids of pairs 4, 5, 6 (even J) / 8, 0,
+// 1 (odd J) of the period in which its buffer's previous chunk was last read, waited for at the
+// mid of pair 8 / 3: at least one pair of latency cover after the last third, four after the first.
+//
+// Halo slot: 64 B = pieces [hi c0-7][lo c0-7][hi c8-15][lo c8-15] (logical 2 g + h), physical piece
+// = logical ^ ((col >> 2) & 1): the A read of a ds_read_b128 lane group ({0-3,12-15,20-27} etc.:
+// 16 pixels of a row block, two 8-channel groups) lands on 16 distinct 16-B bank quads at every tap
+// offset (exhaustive check over the three column phases of a tap; the k_conv3lg swizzle (col >> 2) & 3
+// would be 2-way here).  B reads come from the weight ring as laid out by k_conv3lg (per tap [32-col
+// n][hi, lo][lane][16 B]) with a per-lane gather address (conflict-free).
+#include "conv_common.hpp"
+
+#include <type_traits>
+#include <utility>
+
+namespace tcx {
+namespace {
+
+constexpr int M_KC = 16;               // input channels per chunk
+constexpr int M_NW = 4;                // waves per workgroup
+constexpr int M_TP = 64 * M_NW;        // pixels per tile
+constexpr int M_PAIR = 12288;          // bytes of B fragments per tap pair (2 taps x 3 x [hi, lo] x 1 KB)
+constexpr int M_BN = 96;               // output channels per tile
+
+__host__ __device__ constexpr int m_npx(int W) { return (M_TP / W + 2) * (W + 2); }
+template <int W>
+constexpr size_t conv3m_lds_bytes() { return (size_t)2 * ((m_npx(W) + 15) / 16) * 16 * 64 + 2 * (size_t)M_PAIR; }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void m_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+// Diagnostic timeline (tcx_debug_conv_stamps; null in production, a uniform branch): per workgroup
+// [entry, prologue done, tap loop done, epilogue stores issued, exit] s_memrealtime (100 MHz), the
+// s_memtime (shader clock) at entry and at loop end, and HW_ID | XCC_ID << 16, from wave 0
+__device__ unsigned long long* g_m_stamps = nullptr;
+__device__ int g_m_stamps_n = 0;
+
+constexpr int M_WAIT_VM0 = 0x0F70;    // s_waitcnt vmcnt(0)
+constexpr int M_WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
+
+template <int W>
+__global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
+    constexpr int W2 = W + 2;
+    constexpr int NPX = m_npx(W);
+    constexpr int NI = (NPX + 15) / 16;  // halo DMA instructions per chunk (16 slots each)
+    constexpr int NIH = (NI + 1) / 2;    // per halo wave (wave 2: even i, wave 3: odd i)
+    constexpr int HB = NI * 16 * 64;
+    constexpr int RING = 2 * HB;
+    static_assert(W == 16 || W == 32 || W == 64, "k_conv3m: rows of 16, 32 or 64 pixels");
+    auto sw = [](int col) { return (col >> 2) & 1; };
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    char* const smc = reinterpret_cast<char*>(sm);
+    // LDS-DMA destinations from a base the optimiser cannot fold to a constant (k_conv3lg's note)
+    int lz;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(lz));
+    char* const smd = smc + lz;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    unsigned long long* const stp = g_m_stamps;
+    const bool stamp = stp != nullptr && (int)blockIdx.x < g_m_stamps_n && wv == 0;
+    unsigned long long ts[7] = {};
+    if (stamp) {
+        ts[0] = __builtin_amdgcn_s_memrealtime();
+        ts[5] = __builtin_amdgcn_s_memtime();
+    }
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mblk = tile / p.n_nblk;
+    const int nblk = tile - mblk * p.n_nblk;
+    const int m0 = mblk * M_TP, n0 = nblk * M_BN;
+    const int b = m0 / p.HoWo;
+    const int r0 = (m0 - b * p.HoWo) / W;
+    const int bs = p.bmod > 0 ? b % p.bmod : b;
+    const int H = p.H;
+    const int cpt = p.Cin / M_KC;
+    const int npair = 9 * cpt / 2;
+
+    const __amdgpu_buffer_rsrc_t r1 = mk_rsrc(p.x1, p.bytes1);
+    const __amdgpu_buffer_rsrc_t r2 = mk_rsrc(p.x2 ? p.x2 : p.x1, p.x2 ? p.bytes2 : p.bytes1);
+    const __amdgpu_buffer_rsrc_t rw = mk_rsrc(reinterpret_cast<const float*>(p.wf), p.bytesw);
+
+    // ---- halo DMA (waves 2, 3): lane l of instruction i fills slot 16 i + l / 4, physical piece l % 4,
+    // so it reads logical piece (l % 4) ^ sw(col) of that pixel (the swizzle rides on the source address)
+    const int hw = wv & 1;
+    const int rowb = p.C1 * 4;
+    const int img0 = bs * H;
+    const int ls = lane >> 2;
+    auto halo_voff = [&](int i) {
+        const int hr0 = (16 * i) / W2;
+        const int th = W2 * (hr0 + 1) - 16 * i;
+        const int y0 = wrap_idx(r0 + hr0 - 1, H), y1 = wrap_idx(r0 + hr0, H);
+        const int yo0 = (img0 + y0) * W * rowb, yo1 = (img0 + y1) * W * rowb;
+        const bool nx = ls >= th;
+        int hc = 16 * i - hr0 * W2 + ls - (nx ? W2 : 0);
+        const int sl = 16 * i + ls;
+        const int hcs = hc;
+        if (sl >= NPX) hc = (NPX - 1) % W2;  // padding slots read a valid pixel
+        const int x = hc == 0 ? W - 1 : (hc == W + 1 ? 0 : hc - 1);
+        const int yo = (sl >= NPX) ? (img0 + wrap_idx(r0 + (NPX - 1) / W2 - 1, H)) * W * rowb : (nx ? yo1 : yo0);
+        return yo + x * rowb + 16 * ((lane & 3) ^ sw(hcs));
+    };
+    // third `th` (0..2) of chunk j's halo into buffer buf
+    auto halo_third = [&](int j, int buf, int th) {
+        const int ci0 = j * M_KC;
+        const bool s1 = ci0 < p.C1;
+        const int cc = (s1 ? ci0 : ci0 - p.C1) * 4;
+        const __amdgpu_buffer_rsrc_t rs = s1 ? r1 : r2;
+        const int q0 = (NIH * th) / 3, q1 = (NIH * (th + 1)) / 3;
+#pragma unroll
+        for (int q = 0; q < NIH; ++q) {
+            if (q < q0 || q >= q1) continue;
+            const int i = 2 * q + hw;
+            if (i < NI) m_dma16(rs, smd + buf * HB + i * 1024, halo_voff(i), cc);
+        }
+    };
+    // weight pair k (12 KB) -> ring slot k & 1; wave w (0, 1) moves KB [6 w, 6 w + 6)
+    auto pair_issue = [&](int k) {
+        const int base = (nblk * 2 * npair + 2 * k) * 6144 + wv * 6144;
+        char* const d = smd + RING + (k & 1) * M_PAIR + wv * 6144;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) m_dma16(rw, d + i * 1024, lane * 16, base + i * 1024);
+    };
+
+    // ---- A addresses: lane (li = pixel in a 16-px row block, k block kb: g = kb & 1 channel group,
+    // tap half th = kb >> 1) of row block 0 for pair type q (taps c = 2 q + th of the 18-tap period)
+    const int li = lane & 15, g = (lane >> 4) & 1, th = lane >> 5;
+    int aq[9];
+    {
+        const int mloc = wv * 64 + li;
+        const int rr = mloc / W, cc = mloc % W;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            const int c = 2 * q + th;  // 0..17
+            const int hb = c >= 9 ? 1 : 0;
+            const int t = c - 9 * hb;
+            const int dy = t / 3, dx = t - 3 * (t / 3);
+            aq[q] = hb * HB + ((rr + dy) * W2 + cc + dx) * 64 + 16 * ((2 * g) ^ sw(cc + dx));
+        }
+    }
+    // row block rb of a wave: 16 px on in the row (W = 64), half / next row (32), next row (16)
+    auto rbo = [](int rb) {
+        return W == 64 ? rb * 16 * 64 : (W == 32 ? (rb >> 1) * W2 * 64 + (rb & 1) * 16 * 64 : rb * W2 * 64);
+    };
+    // B: per-lane gather address inside a pair slot of the ring (k_conv3lg's [tap][32-col n][hi, lo][lane])
+    const int bq = RING + (lane >> 5) * 6144 + ((lane >> 4) & 1) * 512 + (lane & 15) * 16;
+
+    f32x4 acc[4][6];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int n = 0; n < 6; ++n) acc[rb][n] = (f32x4){};
+    h8 a_h[4], a_l[4], b_h[3], b_l[3];
+    auto rd_a = [&](int q, int rb) {
+        a_h[rb] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + aq[q] + rbo(rb)));
+        a_l[rb] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + (aq[q] ^ 16) + rbo(rb)));
+    };
+    // B fragments (hi, lo) of pair k, column block nb, into register slot i
+    auto rd_b = [&](int i, int k, int nb) {
+        const char* B = smc + bq + (k & 1) * M_PAIR + (nb >> 1) * 2048 + (nb & 1) * 256;
+        b_h[i] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(B));
+        b_l[i] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(B + 1024));
+    };
+    // the 3 MFMAs (hi.lo, lo.hi, hi.hi) of row block rb and column block nb with B slot i
+    auto mf3 = [&](int rb, int nb, int i) {
+        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h[rb], b_l[i], acc[rb][nb], 0, 0, 0);
+        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_l[rb], b_h[i], acc[rb][nb], 0, 0, 0);
+        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h[rb], b_h[i], acc[rb][nb], 0, 0, 0);
+    };
+    // the 12 MFMAs of column block nb over the 4 row blocks (4 independent accumulators between the
+    // dependent products of one block: rb-inner)
+    auto mf_col = [&](int nb, int i) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+            acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h[rb], b_l[i], acc[rb][nb], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+            acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_l[rb], b_h[i], acc[rb][nb], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+            acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h[rb], b_h[i], acc[rb][nb], 0, 0, 0);
+    };
+
+    // ---- prologue: pairs 0, 1 and halo chunk 0 in LDS; the first third of chunk 1 issued
+    if (wv < 2) {
+        pair_issue(0);
+        pair_issue(1);
+    } else {
+#pragma unroll
+        for (int t3 = 0; t3 < 3; ++t3) halo_third(0, 0, t3);
+    }
+    __builtin_amdgcn_s_waitcnt(M_WAIT_VM0);
+    __builtin_amdgcn_s_waitcnt(M_WAIT_LGKM0);
+    __builtin_amdgcn_s_barrier();
+    if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
+    if (wv >= 2 && cpt > 1) halo_third(1, 1, 0);
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) rd_a(0, rb);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) rd_b(i, 0, i);
+
+    auto pair_iter = [&](int pp, auto Q) {
+        constexpr int q = decltype(Q)::value;
+        constexpr int qn = q == 8 ? 0 : q + 1;
+        const int k = 9 * pp + q;
+        // H1: column blocks 0-2 (B slots 0-2); each slot, once its 12 MFMAs have issued, takes block 3 + i
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            mf_col(i, i);
+            __builtin_amdgcn_sched_barrier(0);
+            rd_b(i, k, 3 + i);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // mid: every wave's ring reads of pair k done; pair k+1 (weights) / a halo chunk published
+        __builtin_amdgcn_s_waitcnt(M_WAIT_LGKM0);
+        if (wv < 2 || q == 3 || q == 8) __builtin_amdgcn_s_waitcnt(M_WAIT_VM0);
+        __builtin_amdgcn_s_barrier();
+        if (wv < 2) {
+            if (k + 2 < npair) pair_issue(k + 2);
+        } else {
+            if constexpr (q >= 4 && q <= 6) {  // chunk 2 pp + 2 -> buffer 0 (chunk 2 pp was last read by pair 4)
+                if (2 * pp + 2 < cpt) halo_third(2 * pp + 2, 0, q - 4);
+            } else if constexpr (q == 8) {     // chunk 2 pp + 3 -> buffer 1 (chunk 2 pp + 1 last read by pair 8)
+                if (2 * pp + 3 < cpt) halo_third(2 * pp + 3, 1, 0);
+            } else if constexpr (q <= 1) {     // the rest of chunk 2 pp + 1 (its first third: pair 8 before)
+                if (2 * pp + 1 < cpt) halo_third(2 * pp + 1, 1, q + 1);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // H2: column blocks 3-5; slots 0, 1 then take B(k+1) blocks 0, 1; block 5 runs row block by row
+        // block so that A(k+1) of each row block is read right after its last use of A(k), then slot 2
+        // takes B(k+1) block 2
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            mf_col(3 + i, i);
+            __builtin_amdgcn_sched_barrier(0);
+            rd_b(i, k + 1, i);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+            mf3(rb, 5, 2);
+            __builtin_amdgcn_sched_barrier(0);
+            rd_a(qn, rb);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        rd_b(2, k + 1, 2);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int pp = 0; pp < cpt / 2; ++pp) {
+        pair_iter(pp, std::integral_constant<int, 0>{});
+        pair_iter(pp, std::integral_constant<int, 1>{});
+        pair_iter(pp, std::integral_constant<int, 2>{});
+        pair_iter(pp, std::integral_constant<int, 3>{});
+        pair_iter(pp, std::integral_constant<int, 4>{});
+        pair_iter(pp, std::integral_constant<int, 5>{});
+        pair_iter(pp, std::integral_constant<int, 6>{});
+        pair_iter(pp, std::integral_constant<int, 7>{});
+        pair_iter(pp, std::integral_constant<int, 8>{});
+    }
+
+    if (stamp) {
+        ts[2] = __builtin_amdgcn_s_memrealtime();
+        ts[6] = __builtin_amdgcn_s_memtime();
+    }
+    __builtin_amdgcn_s_waitcnt(M_WAIT_VM0);
+    __syncthreads();  // LDS -> epilogue reduction scratch
+
+    // ---- epilogue (the fast path of conv_common.hpp for the 16x16 accumulator layout: lane l holds
+    // column l & 15 of each 16x16 block, rows 4 (l >> 4) .. + 3): bias, activation, fp32 or h2 store,
+    // fp64 GroupNorm partials per 128-pixel group (waves 0-1, 2-3)
+    double* red = reinterpret_cast<double*>(sm);
+    {
+        const int col = lane & 15, rg = lane >> 4;
+        const bool odd = (col & 1) != 0;
+        const float wsc = *p.wscale;
+        const f32x2 wsc2 = {wsc, wsc};
+        const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, (unsigned)((long long)p.M * p.Cout * 4));
+        const int rowo = p.Cout * 4;
+        const int pixb = m0 + 64 * wv + 4 * rg;
+#pragma unroll
+        for (int nb = 0; nb < 6; ++nb) {
+            const int co = n0 + 16 * nb + col;
+            const float bc = p.bias ? p.bias[co] : 0.f;
+            const f32x2 bc2 = {bc, bc};
+            const int vo = p.out_h2 ? pixb * rowo + (co & ~7) * 4 + (odd ? 16 : 0) + 2 * ((co & 7) & ~1)
+                                    : (pixb * p.Cout + co) * 4;
+            f32x2 s2 = {0.f, 0.f}, ss2 = {0.f, 0.f};
+            bool bad = false;
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const f32x2 a = {acc[rb][nb][2 * h], acc[rb][nb][2 * h + 1]};
+                    f32x2 v2 = a * wsc2 + bc2;
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        float v = v2[e];
+                        if (p.act == 1) v = fmaxf(v, 0.f);
+                        else if (p.act == 2) v = 1.f / (1.f + expf(-v));
+                        else if (p.act == 3) v = silu_f(v);
+                        v2[e] = v;
+                        const int so = (16 * rb + 2 * h + e) * rowo;
+                        if (p.out_h2) {
+                            // lane pairs (2j, 2j+1) of an 8-channel group swap halves (quad_perm [1,0,3,2])
+                            const unsigned sp = split1(v);
+                            const unsigned oth = (unsigned)__builtin_amdgcn_mov_dpp(
+                                (int)(odd ? (sp & 0xffffu) : (sp >> 16)), 0xB1, 0xF, 0xF, false);
+                            const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
+                            __builtin_amdgcn_raw_buffer_store_b32(word, ry, vo, so, 0);
+                            bad = bad || h2_bad(v);
+                        } else {
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, vo, so, 0);
+                        }
+                    }
+                    s2 += v2;
+                    ss2 = v2 * v2 + ss2;
+                }
+            }
+            h2_flag(p.ovf, bad);
+            if (p.gn) {
+                double ds = (double)s2.x + (double)s2.y, dss = (double)ss2.x + (double)ss2.y;
+                ds += __shfl_xor(ds, 16);
+                dss += __shfl_xor(dss, 16);
+                ds += __shfl_xor(ds, 32);
+                dss += __shfl_xor(dss, 32);
+                if (rg == 0) {
+                    red[(wv * M_BN + 16 * nb + col) * 2 + 0] = ds;
+                    red[(wv * M_BN + 16 * nb + col) * 2 + 1] = dss;
+                }
+            }
+        }
+    }
+    if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
+    if (p.gn) {
+        __syncthreads();
+        for (int e = tid; e < 2 * M_BN; e += 64 * M_NW) {
+            const int gi = e / M_BN, cl = e - gi * M_BN;
+            const int co = n0 + cl;
+            const double s = red[((2 * gi) * M_BN + cl) * 2 + 0] + red[((2 * gi + 1) * M_BN + cl) * 2 + 0];
+            const double ss = red[((2 * gi) * M_BN + cl) * 2 + 1] + red[((2 * gi + 1) * M_BN + cl) * 2 + 1];
+            const int mg = m0 + 128 * gi;
+            const int bb = mg / p.HoWo;
+            const int split = (mg - bb * p.HoWo) / 128;
+            double* dst = p.gn + (((size_t)bb * p.nsplit + split) * p.Cout + co) * 2;
+            dst[0] = s;
+            dst[1] = ss;
+        }
+    }
+    if (stamp) {  // vector stores from lanes 0..7 of wave 0
+        const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
+        const unsigned hw = __builtin_amdgcn_s_getreg(0xF804) & 0xffffu;  // HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg(0xF814) & 0xffffu; // XCC_ID
+        unsigned long long v = lane == 0 ? ts[0] : lane == 1 ? ts[1] : lane == 2 ? ts[2] : lane == 3 ? ts[3]
+                             : lane == 4 ? t4 : lane == 5 ? ts[5] : lane == 6 ? ts[6]
+                             : ((unsigned long long)hw | ((unsigned long long)xcc << 16));
+        if (lane < 8) stp[(size_t)blockIdx.x * 8 + lane] = v;
+    }
+}
+
+template <int W>
+int launch3m(const ConvParams& p, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3m<W>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)conv3m_lds_bytes<W>()) != hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3m_lds_bytes<W>());
+            return TCX_EHIP;
+        }
+        attr = true;
+    }
+    const int grid = (p.M / M_TP) * p.n_nblk;
+    hipLaunchKernelGGL(k_conv3m<W>, dim3(grid), dim3(64 * M_NW), conv3m_lds_bytes<W>(), st, p);
+    return check_launch("tcx_conv2d_h2(3x3 16x16x32)");
+}
+
+}  // namespace
+
+// TCX_CONV3M=0 keeps k_conv3lg for the h2-source convs (A/B measurements)
+bool conv3m_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("TCX_CONV3M");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// called by launch_conv3l for the h2-source (PRO 0) form: k_conv3lg's conditions plus the fast
+// epilogue's (dense NHWC fp32 / h2 output, no per-batch bias or residual, 32-bit offsets)
+bool conv3m_takes(const ConvParams& p) {
+    return conv3m_enabled() && !p.bf && p.circular && p.sc1 == nullptr && !(p.C2 > 0 && p.sc2 != nullptr) &&
+           (p.W == 16 || p.W == 32 || p.W == 64) && p.M % M_TP == 0 && p.HoWo % M_TP == 0 && p.Cin % 32 == 0 &&
+           p.Cin <= 384 && p.Cout % M_BN == 0 && p.osy == 1 && p.osx == 1 && p.bias_b == nullptr &&
+           p.resid == nullptr && (long long)p.M * p.Cout < (1ll << 29) && p.wscale != nullptr;
+}
+
+extern "C" int tcx_debug_conv_stamps(void* buf, int n) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_m_stamps), &buf, sizeof(buf)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_m_stamps_n), &n, sizeof(n)) != hipSuccess) {
+        set_error("tcx_debug_conv_stamps: hipMemcpyToSymbol failed");
+        return TCX_EHIP;
+    }
+    return TCX_OK;
+}
+
+int launch_conv3m(const ConvParams& p, hipStream_t st) {
+    if (p.W == 64) return launch3m<64>(p, st);
+    if (p.W == 32) return launch3m<32>(p, st);
+    return launch3m<16>(p, st);
+}
+
+}  // namespace tcx

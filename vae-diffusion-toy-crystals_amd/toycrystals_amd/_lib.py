@@ -71,6 +71,7 @@ _SIGS = {
     "tcx_last_error": (ctypes.c_char_p, []),
     "tcx_version": (c_int, []),
     "tcx_prof_enable": (c_int, [c_int]),
+    "tcx_debug_conv_stamps": (c_int, [c_fp, c_int]),
     "tcx_prof_read": (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                               ctypes.POINTER(ctypes.c_double)]),
     "tcx_conv2d": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp, c_fp, c_int,
