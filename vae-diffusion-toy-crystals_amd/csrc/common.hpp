@@ -80,6 +80,14 @@ __device__ __forceinline__ void block_amax_publish(float m, unsigned* amax) {
 }
 // SiLU with the hardware exp2 / reciprocal (a few ulp; used in staged prologues)
 
+// Call first thing in an MFMA kernel: an AGPR reference keeps hipcc from proving the kernel AGPR-free,
+// so it selects the AGPR form of the MFMAs (accumulators in AGPRs, fragments in VGPRs).  In the
+// all-VGPR form the allocator may move an accumulator (MFMA D != C) and reuse its old SrcC register
+// for a following ds_read / load; an MFMA queued behind other waves' MFMAs on the matrix pipe can read
+// SrcC after that data has landed: wrong sums whenever other kernels share the CU (k_conv3m under the
+// sampling lanes, r04_n; tools/mfma_war_check.py finds the pattern in the .s).
+__device__ __forceinline__ void mfma_agpr_form() { asm volatile("" ::: "a0"); }
+
 __device__ __forceinline__ int wrap_idx(int i, int n) {
     i = i < 0 ? i + n : i;
     return i >= n ? i - n : i;

@@ -59,6 +59,7 @@ constexpr size_t conv3m_lds_bytes() { return (size_t)2 * ((m_npx(W) + 15) / 16) 
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void m_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
@@ -72,7 +73,9 @@ __device__ int g_m_stamps_n = 0;
 constexpr int M_WAIT_VM0 = 0x0F70;    // s_waitcnt vmcnt(0)
 constexpr int M_WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
 
-template <int W>
+// FAST: no activation and an fp32 output (every U-Net conv k_conv3m serves: a GroupNorm follows), so
+// the epilogue is straight-line code; otherwise the activation / h2 output are run-time branches
+template <int W, bool FAST>
 __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     constexpr int W2 = W + 2;
     constexpr int NPX = m_npx(W);
@@ -88,6 +91,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     int lz;
     asm volatile("s_mov_b32 %0, 0" : "=s"(lz));
     char* const smd = smc + lz;
+    mfma_agpr_form();  // accumulators in AGPRs (common.hpp: the SrcC-reuse hazard this kernel hit under the lanes)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -185,6 +189,22 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
 #pragma unroll
         for (int n = 0; n < 6; ++n) acc[rb][n] = (f32x4){};
     h8 a_h[4], a_l[4], b_h[3], b_l[3];
+    // Before a ds_read overwrites A / B fragment registers, read the accumulator of the last MFMA that
+    // used them: the wave then issues the load only once that MFMA (and, in order, every earlier one) has
+    // finished.  Without it, a load issued right behind the MFMAs reading its destination registers
+    // corrupted single B columns of some 16x16 blocks whenever other kernels shared the CU (the sampling
+    // lanes: r04_n..q, tools/determinism_probe.py --corun: 7e4 wrong outputs per 10 launches, 0 with this
+    // dependency).  The read is a v_accvgpr_read behind the compiler's MFMA-result wait states.
+    auto dep = [&](int rb, int nb) {
+        float t = acc[rb][nb][0];
+        asm volatile("" ::"v"(t) : "memory");
+    };
+    // after a column block's 12 MFMAs: all four accumulators (the compiler may issue the independent row
+    // blocks in any order, so no single one is known to be last)
+    auto dep_col = [&](int nb) {
+        float t0 = acc[0][nb][0], t1 = acc[1][nb][0], t2 = acc[2][nb][0], t3 = acc[3][nb][0];
+        asm volatile("" ::"v"(t0), "v"(t1), "v"(t2), "v"(t3) : "memory");
+    };
     auto rd_a = [&](int q, int rb) {
         a_h[rb] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + aq[q] + rbo(rb)));
         a_l[rb] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + (aq[q] ^ 16) + rbo(rb)));
@@ -242,6 +262,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         for (int i = 0; i < 3; ++i) {
             mf_col(i, i);
             __builtin_amdgcn_sched_barrier(0);
+            dep_col(i);
             rd_b(i, k, 3 + i);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -268,6 +289,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         for (int i = 0; i < 2; ++i) {
             mf_col(3 + i, i);
             __builtin_amdgcn_sched_barrier(0);
+            dep_col(3 + i);
             rd_b(i, k + 1, i);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -275,9 +297,11 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         for (int rb = 0; rb < 4; ++rb) {
             mf3(rb, 5, 2);
             __builtin_amdgcn_sched_barrier(0);
+            dep(rb, 5);
             rd_a(qn, rb);
             __builtin_amdgcn_sched_barrier(0);
         }
+        dep_col(5);
         rd_b(2, k + 1, 2);
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -301,59 +325,65 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     __syncthreads();  // LDS -> epilogue reduction scratch
 
     // ---- epilogue (the fast path of conv_common.hpp for the 16x16 accumulator layout: lane l holds
-    // column l & 15 of each 16x16 block, rows 4 (l >> 4) .. + 3): bias, activation, fp32 or h2 store,
-    // fp64 GroupNorm partials per 128-pixel group (waves 0-1, 2-3)
+    // column l & 15 of each 16x16 block, rows 4 (l >> 4) .. + 3): bias, activation, fp64 GroupNorm
+    // partials per 128-pixel group (waves 0-1, 2-3) from the columns, then a 4x4 quad transpose
+    // (quad_transpose4) so that lane l holds row 4 (l >> 4) + (l & 3) of 4 consecutive channels
+    // 4 ((l & 15) >> 2) .. + 3: one 16-B store per lane and block (fp32), or the 8-B hi and lo
+    // halves of the pixel's h2 record
     double* red = reinterpret_cast<double*>(sm);
     {
-        const int col = lane & 15, rg = lane >> 4;
-        const bool odd = (col & 1) != 0;
+        const int col = lane & 15, rg = lane >> 4, qi = lane & 3, qc = col >> 2;
         const float wsc = *p.wscale;
-        const f32x2 wsc2 = {wsc, wsc};
         const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, (unsigned)((long long)p.M * p.Cout * 4));
         const int rowo = p.Cout * 4;
-        const int pixb = m0 + 64 * wv + 4 * rg;
+        const int pixq = m0 + 64 * wv + 4 * rg + qi;  // this lane's pixel after the transpose (row block 0)
+        const int vo32 = (pixq * p.Cout + n0 + 4 * qc) * 4;
+        const int voh = pixq * rowo + (n0 + 4 * qc) / 8 * 32 + (qc & 1) * 8;
+        // every load before the first store: vmcnt counts loads and stores in order, so a load issued
+        // after a store would wait for that store's acknowledgement
+        float bcs[6];
+#pragma unroll
+        for (int nb = 0; nb < 6; ++nb) bcs[nb] = p.bias ? p.bias[n0 + 16 * nb + col] : 0.f;
 #pragma unroll
         for (int nb = 0; nb < 6; ++nb) {
-            const int co = n0 + 16 * nb + col;
-            const float bc = p.bias ? p.bias[co] : 0.f;
-            const f32x2 bc2 = {bc, bc};
-            const int vo = p.out_h2 ? pixb * rowo + (co & ~7) * 4 + (odd ? 16 : 0) + 2 * ((co & 7) & ~1)
-                                    : (pixb * p.Cout + co) * 4;
-            f32x2 s2 = {0.f, 0.f}, ss2 = {0.f, 0.f};
+            const float bc = bcs[nb];
+            float s = 0.f, ss = 0.f;
             bool bad = false;
 #pragma unroll
             for (int rb = 0; rb < 4; ++rb) {
+                float v[4];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const f32x2 a = {acc[rb][nb][2 * h], acc[rb][nb][2 * h + 1]};
-                    f32x2 v2 = a * wsc2 + bc2;
-#pragma unroll
-                    for (int e = 0; e < 2; ++e) {
-                        float v = v2[e];
-                        if (p.act == 1) v = fmaxf(v, 0.f);
-                        else if (p.act == 2) v = 1.f / (1.f + expf(-v));
-                        else if (p.act == 3) v = silu_f(v);
-                        v2[e] = v;
-                        const int so = (16 * rb + 2 * h + e) * rowo;
-                        if (p.out_h2) {
-                            // lane pairs (2j, 2j+1) of an 8-channel group swap halves (quad_perm [1,0,3,2])
-                            const unsigned sp = split1(v);
-                            const unsigned oth = (unsigned)__builtin_amdgcn_mov_dpp(
-                                (int)(odd ? (sp & 0xffffu) : (sp >> 16)), 0xB1, 0xF, 0xF, false);
-                            const unsigned word = odd ? (oth | (sp & 0xffff0000u)) : ((sp & 0xffffu) | (oth << 16));
-                            __builtin_amdgcn_raw_buffer_store_b32(word, ry, vo, so, 0);
-                            bad = bad || h2_bad(v);
-                        } else {
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, vo, so, 0);
-                        }
+                for (int r = 0; r < 4; ++r) {
+                    float x = fmaf(acc[rb][nb][r], wsc, bc);
+                    if constexpr (!FAST) {
+                        if (p.act == 1) x = fmaxf(x, 0.f);
+                        else if (p.act == 2) x = 1.f / (1.f + expf(-x));
+                        else if (p.act == 3) x = silu_f(x);
                     }
-                    s2 += v2;
-                    ss2 = v2 * v2 + ss2;
+                    v[r] = x;
+                    s += x;
+                    ss = fmaf(x, x, ss);
+                }
+                quad_transpose4(v, qi);
+                const int so = (16 * rb * p.Cout + 16 * nb) * 4;
+                if (!FAST && p.out_h2) {
+                    const unsigned a0 = split1(v[0]), a1 = split1(v[1]), a2 = split1(v[2]), a3 = split1(v[3]);
+                    const unsigned hi0 = (a0 & 0xffffu) | (a1 << 16), hi1 = (a2 & 0xffffu) | (a3 << 16);
+                    const unsigned lo0 = (a0 >> 16) | (a1 & 0xffff0000u), lo1 = (a2 >> 16) | (a3 & 0xffff0000u);
+                    const int sh = (16 * rb * p.Cout + 16 * nb) * 4;  // 16 channels = two whole records
+                    __builtin_amdgcn_raw_buffer_store_b64((u32x2){hi0, hi1},
+                                                          ry, voh, sh, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64((u32x2){lo0, lo1},
+                                                          ry, voh + 16, sh, 0);
+                    bad = bad || h2_bad(v[0]) || h2_bad(v[1]) || h2_bad(v[2]) || h2_bad(v[3]);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry, vo32, so, 0);
                 }
             }
-            h2_flag(p.ovf, bad);
+            if constexpr (!FAST) h2_flag(p.ovf, bad);
             if (p.gn) {
-                double ds = (double)s2.x + (double)s2.y, dss = (double)ss2.x + (double)ss2.y;
+                double ds = (double)s, dss = (double)ss;
                 ds += __shfl_xor(ds, 16);
                 dss += __shfl_xor(dss, 16);
                 ds += __shfl_xor(ds, 32);
@@ -394,30 +424,39 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
 
 template <int W>
 int launch3m(const ConvParams& p, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3m<W>), hipFuncAttributeMaxDynamicSharedMemorySize,
+    static bool attr[2] = {};
+    const bool fast = p.act == 0 && !p.out_h2;
+    const int ai = (int)fast;
+    void (*const k)(ConvParams) = fast ? &k_conv3m<W, true> : &k_conv3m<W, false>;
+    if (!attr[ai]) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)conv3m_lds_bytes<W>()) != hipSuccess) {
             set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3m_lds_bytes<W>());
             return TCX_EHIP;
         }
-        attr = true;
+        attr[ai] = true;
     }
     const int grid = (p.M / M_TP) * p.n_nblk;
-    hipLaunchKernelGGL(k_conv3m<W>, dim3(grid), dim3(64 * M_NW), conv3m_lds_bytes<W>(), st, p);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * M_NW), conv3m_lds_bytes<W>(), st, p);
     return check_launch("tcx_conv2d_h2(3x3 16x16x32)");
 }
 
 }  // namespace
 
-// TCX_CONV3M=0 keeps k_conv3lg for the h2-source convs (A/B measurements)
+// Opt-in (TCX_CONV3M=1): not the default.  Alone on the chip k_conv3m is exact and 3-10 % faster per
+// layer than k_conv3lg, but with other kernels sharing its CUs (the sampler's concurrent lanes, or any
+// concurrent stream) a few 16x16 blocks per launch get one wrong B column (tools/determinism_probe.py
+// --corun; profiles/r04_*_corun*.log): waiting for every MFMA that read a fragment register before a
+// ds_read overwrites it (dep / dep_col below) cut the rate from ~7e4 to ~2e2 wrong outputs per 20
+// launches but did not remove it, and k_conv3lg (32x32x16, the same DMA / barrier scheme) shows none.
 bool conv3m_enabled() {
     static const bool on = [] {
         const char* e = getenv("TCX_CONV3M");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return on;
 }
+
 
 // called by launch_conv3l for the h2-source (PRO 0) form: k_conv3lg's conditions plus the fast
 // epilogue's (dense NHWC fp32 / h2 output, no per-batch bias or residual, 32-bit offsets)

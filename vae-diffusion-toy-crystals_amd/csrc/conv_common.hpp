@@ -125,8 +125,32 @@ __device__ __forceinline__ bool conv_epi_fast(const ConvParams& p, int m0) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// 4x4 transpose across the 4 lanes of a DPP quad (lane i = lane & 3): element r of lane i becomes
+// element i of lane r, in two butterfly stages of quad_perm moves (xor 1, xor 2).  An accumulator
+// column (one channel, 4 consecutive output rows per lane) turns into 4 consecutive channels of one
+// row per lane, so the epilogue stores 16 B per lane instead of 4 (cdna_hip_programming.md T21: the
+// store tail is issue-bound; k_conv3m's dword-store epilogue took 19 us of a 56-us workgroup,
+// profiles/r04_d_stamps_down1_1.txt).
+__device__ __forceinline__ float dpp_qxor1(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_qxor2(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void quad_transpose4(float (&a)[4], int i) {
+    const bool o = (i & 1) != 0, t = (i & 2) != 0;
+    float y = dpp_qxor1(o ? a[0] : a[1]);
+    if (o) a[0] = y; else a[1] = y;
+    y = dpp_qxor1(o ? a[2] : a[3]);
+    if (o) a[2] = y; else a[3] = y;
+    y = dpp_qxor2(t ? a[0] : a[2]);
+    if (t) a[0] = y; else a[2] = y;
+    y = dpp_qxor2(t ? a[1] : a[3]);
+    if (t) a[1] = y; else a[3] = y;
+}
+
 template <int NT, int SPL, int NW, int RT>
-__device__ __forceinline__ void conv_epi_store_fast(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
+__device__ __forceinline__ void conv_epi_store_cols(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
                                                     int wv0, int lane, double* red) {
     constexpr int BN = 32 * NT;
     const int li = lane & 31;
@@ -204,6 +228,90 @@ __device__ __forceinline__ void conv_epi_store_fast(const ConvParams& p, f32x16 
             }
         }
     }
+}
+
+// No residual: each 4-row group of a column (rows 8 j + 4 (lane >> 5) + 0..3) is quad-transposed
+// (quad_transpose4) so that lane l holds one row and 4 consecutive channels 4 ((l & 31) >> 2) .. + 3:
+// one 16-B store (fp32) or two 8-B stores (the hi and lo halves of the h2 record) per lane and group,
+// 4 instead of 16 store instructions per 32x32 block.  ACT: the activation is a run-time branch
+// (false: none, straight-line code).  GroupNorm partials from the columns before the transpose.
+template <int NT, int SPL, int NW, int RT, bool ACT>
+__device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
+                                                    int wv0, int lane, double* red) {
+    constexpr int BN = 32 * NT;
+    const int li = lane & 31;
+    const int lh = lane >> 5;
+    const int qi = lane & 3, qc = li >> 2;
+    const bool gn = p.gn != nullptr;
+    const bool bf = SPL == 2 || (SPL == 0 && p.bf != 0);
+    const float wsc = SPL ? *p.wscale : 1.f;
+    float bco[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) bco[n] = p.bias ? p.bias[n0 + n * 32 + li] : 0.f;
+    const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, (unsigned)((long long)p.M * p.Cout * 4));
+    const int rowb = p.Cout * 4;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int wv = wv0 + rt;
+        const int pixq = m0 + wv * 32 + 4 * lh + qi;  // this lane's row of group 0 after the transpose
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int c4 = n0 + n * 32 + 4 * qc;  // first of this lane's 4 channels after the transpose
+            const int vo32 = (pixq * p.Cout + c4) * 4;
+            const int voh = pixq * rowb + (c4 >> 3) * 32 + (qc & 1) * 8;
+            float s = 0.f, ss = 0.f;
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = SPL ? fmaf(acc[rt][n][4 * j + e], wsc, bco[n]) : acc[rt][n][4 * j + e] + bco[n];
+                    if constexpr (ACT) {
+                        if (p.act == 1) x = fmaxf(x, 0.f);
+                        else if (p.act == 2) x = 1.f / (1.f + expf(-x));
+                        else if (p.act == 3) x = silu_f(x);
+                    }
+                    v[e] = x;
+                    s += x;
+                    ss = fmaf(x, x, ss);
+                }
+                quad_transpose4(v, qi);
+                const int so = 8 * j * rowb;
+                if (p.out_h2) {
+                    const unsigned a0 = split1x(v[0], bf), a1 = split1x(v[1], bf), a2 = split1x(v[2], bf),
+                                   a3 = split1x(v[3], bf);
+                    typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
+                    const u32x2_ hi = {(a0 & 0xffffu) | (a1 << 16), (a2 & 0xffffu) | (a3 << 16)};
+                    const u32x2_ lo = {(a0 >> 16) | (a1 & 0xffff0000u), (a2 >> 16) | (a3 & 0xffff0000u)};
+                    __builtin_amdgcn_raw_buffer_store_b64(hi, ry, voh, so, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64(lo, ry, voh + 16, so, 0);
+                    bad = bad || (!bf && (h2_bad(v[0]) || h2_bad(v[1]) || h2_bad(v[2]) || h2_bad(v[3])));
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])),
+                                                           ry, vo32, so, 0);
+                }
+            }
+            h2_flag(p.ovf, bad);
+            if (gn) {
+                double ds = (double)s, dss = (double)ss;
+                ds += __shfl_xor(ds, 32);
+                dss += __shfl_xor(dss, 32);
+                if (lh == 0) {
+                    red[(wv * BN + n * 32 + li) * 2 + 0] = ds;
+                    red[(wv * BN + n * 32 + li) * 2 + 1] = dss;
+                }
+            }
+        }
+    }
+}
+
+template <int NT, int SPL, int NW, int RT>
+__device__ __forceinline__ void conv_epi_store_fast(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
+                                                    int wv0, int lane, double* red) {
+    if (p.resid) conv_epi_store_cols<NT, SPL, NW, RT>(p, acc, m0, n0, wv0, lane, red);  // attention proj
+    else if (p.act == 0) conv_epi_store_quad<NT, SPL, NW, RT, false>(p, acc, m0, n0, wv0, lane, red);
+    else conv_epi_store_quad<NT, SPL, NW, RT, true>(p, acc, m0, n0, wv0, lane, red);
 }
 
 // Fused epilogue of a conv tile: wave wv owns output rows m0 + 32*wv + [0, 32) and columns

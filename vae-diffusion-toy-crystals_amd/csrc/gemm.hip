@@ -1007,12 +1007,10 @@ extern "C" int tcx_conv_wgrad_h2(const void* x1, const void* x2, int Bt, int H, 
     p.part = reinterpret_cast<float*>(base);
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(p.nkblk * p.ncblk, p.nsplit);
-    static const bool r2 = [] {  // TCX_WG_R2=1: the round-2 quad-staged kernel (A/B)
-        const char* e = getenv("TCX_WG_R2");
-        return e && e[0] == '1';
-    }();
+    // operands past 2 GiB (32-bit buffer offsets) take the round-2 quad-staged k_wgrad_h2_r2 (the knob that
+    // selected it for A/B was removed in round 4: 419 vs 613 us, r03)
     const size_t in1 = (size_t)Bt * H * W * C1 * 4, in2 = (size_t)Bt * H * W * C2 * 4, ind = (size_t)p.M * Cout * 4;
-    if (!r2 && in1 < (1u << 31) && in2 < (1u << 31) && ind < (1u << 31)) {
+    if (in1 < (1u << 31) && in2 < (1u << 31) && ind < (1u << 31)) {
         p.bx1 = (unsigned)in1; p.bx2 = (unsigned)in2; p.bdy = (unsigned)ind;
         using K = void (*)(WgParams);
         const K k = nt == 3 ? &k_wgrad_h2<3> : (nt == 2 ? &k_wgrad_h2<2> : &k_wgrad_h2<1>);

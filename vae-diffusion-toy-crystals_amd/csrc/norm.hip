@@ -877,10 +877,7 @@ int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const fl
         hipLaunchKernelGGL(k, dim3(Bt * (2 * H / rows)), dim3(256), shm, st, x, (char*)y, H, W, C, scale, shift, ovf, bf);
         return check_launch("tcx_upsample2x_h2(band)");
     }
-    static const bool seg_on = [] {  // TCX_UPSEG=0: the g8 form at wide rows (A/B)
-        const char* e = getenv("TCX_UPSEG");
-        return !(e && e[0] == '0');
-    }();
+    constexpr bool seg_on = true;  // the segmented band form at wide rows (faster than g8, r03; knob removed r04)
     if (const int sw = seg_on ? upsample_seg_width(H, W, C) : 0) {  // config 5's wide rows
         constexpr int rows = 4;
         const size_t shm = (size_t)(rows / 2 + 2) * (sw + 2) * C * sizeof(float);

@@ -49,6 +49,7 @@ __device__ __forceinline__ float ddim_z(float z, float e, float abar_t, float ab
 template <int MT, int NB>
 __global__ __launch_bounds__(512) void k_skinny(SkArgs a) {
     constexpr int KC = 16 * NB;  // k values per wave
+    mfma_agpr_form();
     __shared__ float red[SK_WAVES][16 * MT][17];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int r = lane & 15, q = lane >> 4;
@@ -140,6 +141,7 @@ __device__ __attribute__((aligned(16))) float sk_zero8[8] = {0.f, 0.f, 0.f, 0.f,
 template <int MT, int NC>
 __global__ __launch_bounds__(512) void k_skinny_h2(SkH2Args a) {
     constexpr int KC = 32 * NC;  // k values per wave
+    mfma_agpr_form();
     __shared__ float red[SK_WAVES][16 * MT][17];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int r = lane & 15, q = lane >> 4;

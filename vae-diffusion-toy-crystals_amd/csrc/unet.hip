@@ -1064,20 +1064,13 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // normalised tensor is never written: norms 0, 2, 4, 7, 9 (down1.net.1, down2.net.1, mid.net.1,
     // up2.net.1, up1.net.1 feeding the .net.3 conv of their block).  The skip tensors h1/h2 (norms 1,
     // 3: read by a 4x4/s2 conv AND an up-path concat) keep the in-place h2 apply pass.
-    // TCX_GN_PRO=0: every GroupNorm as an h2 apply pass (A/B of the prologue against the LDS-DMA
-    // h2-source conv)
-    static const bool gn_pro = [] {
-        const char* e = getenv("TCX_GN_PRO");
-        return !(e && e[0] == '0');
-    }();
+    // (round 2-3 A/B: every GroupNorm as an h2 apply pass instead measured 2-3 % slower; knob removed r04)
+    constexpr bool gn_pro = true;
     // bf16 at rows of 64/128/256 pixels: the h2-source conv there is the LDS-DMA k_conv3lb, which has no
     // prologue form; an apply pass + k_conv3lb beats k_conv3g's register-staged prologue form, whose
     // transform (7 halo units per thread at 256-px rows, 3x redundant over the tiles of a row) is not
-    // hidden behind a bf16 tap's 6 MFMAs (TCX_BF_PRO=1 keeps the prologue: A/B)
-    static const bool bf_pro = [] {
-        const char* e = getenv("TCX_BF_PRO");
-        return e && e[0] == '1';
-    }();
+    // hidden behind a bf16 tap's 6 MFMAs (the prologue form measured equal, r03_y; knob removed r04)
+    constexpr bool bf_pro = false;
     auto pro_ok = [&](const tcx_conv& cv, int h, int w, int cin) {
         const bool bf = net->precision == 2;
         if (!cv.whf || !conv3g_covers(h, w, cin, cv.cout_pad, bf)) return false;
@@ -1105,11 +1098,9 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // down1 (first conv: x_t channel only, maps folded into bias0; the conv bias is inside bias0)
     // Split path (round 3): statistics pass + a second pass that recomputes the conv and writes
     // silu(GroupNorm_0(.)) as down1.net.3's h2 / bf16 record (k_first_acf + k_first_gnsum, k_conv_first MODE 2), so norm 0 needs
-    // neither a prologue nor an apply pass and the fp32 tensor is never written (TCX_FIRST_FUSE=0: A/B)
-    static const bool first_fuse = [] {
-        const char* e = getenv("TCX_FIRST_FUSE");
-        return !(e && e[0] == '0');
-    }();
+    // neither a prologue nor an apply pass and the fp32 tensor is never written (faster than the fp32
+    // tensor + prologue form, r03_y; knob removed r04)
+    constexpr bool first_fuse = true;
     bool first_fused = false;
     {
         const tcx_conv& c0 = net->down1_0;
