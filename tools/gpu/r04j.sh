@@ -1,0 +1,12 @@
+# Round 4: bf16 256^2 epilogue bisect (column epilogue for bf16 only) + determinism at 64^2; f16x3 GEMM tests; prior step.
+cd /root/repo
+export TMPDIR=/tmp
+T=r04_x
+timeout -k 10 200 python -u tools/dbg_bf16.py --lib build_dbg/libtcx_v1.so > gpurun_out/${T}_dbg_v1.log 2>&1 && \
+timeout -k 10 200 python -u tools/dbg_bf16.py --name unet96_b2 > gpurun_out/${T}_dbg_quad64.log 2>&1 && \
+timeout -k 10 300 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_gpu_gemm_x3.py "tests/test_gpu_train.py::test_prior_training_step_vs_reference" "tests/test_gpu_train.py::test_prior_training_step_w1024_vs_reference" > gpurun_out/${T}_x3.log 2>&1
+rc=$?
+echo "rc $rc"
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+STEPS=10 WARM=3 timeout -k 10 200 python -u tools/train_bench.py prior > gpurun_out/${T}_prior.log 2>&1 && \
+STEPS=3 WARM=2 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_priorprof -o run -- python3 tools/train_bench.py prior > gpurun_out/${T}_priorprof.log 2>&1

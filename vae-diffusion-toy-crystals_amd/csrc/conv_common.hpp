@@ -306,10 +306,16 @@ __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 
     }
 }
 
+// bf16 (SPL 2) keeps the column form: with the quad form, k_conv3lb<128 / 256> (config 5's 256^2 rows)
+// returned run-to-run different outputs (tools/dbg_bf16.py: 1.25e-1 .. 1.59e-1 of the output scale,
+// errors in 64-pixel blocks; profiles/r04_w_dbg_quad.log) while the column form is deterministic and
+// within the bf16 gate (7.8e-3, r04_x_dbg_v1.log); the quad form at 64^2 bf16 and every f16x3 / fp32
+// kernel are deterministic (determinism probe, r04_u).  Cause not isolated (no SrcC reuse hazard in
+// either form: tools/mfma_war_check.py).
 template <int NT, int SPL, int NW, int RT>
 __device__ __forceinline__ void conv_epi_store_fast(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
                                                     int wv0, int lane, double* red) {
-    if (p.resid) conv_epi_store_cols<NT, SPL, NW, RT>(p, acc, m0, n0, wv0, lane, red);  // attention proj
+    if (p.resid || SPL == 2) conv_epi_store_cols<NT, SPL, NW, RT>(p, acc, m0, n0, wv0, lane, red);  // attention proj, bf16
     else if (p.act == 0) conv_epi_store_quad<NT, SPL, NW, RT, false>(p, acc, m0, n0, wv0, lane, red);
     else conv_epi_store_quad<NT, SPL, NW, RT, true>(p, acc, m0, n0, wv0, lane, red);
 }
