@@ -171,9 +171,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
     const int nch_all = (p.K + GBK - 1) / GBK;
     const int cb = p.part ? sk * p.kcs : 0;
     const int nch = p.part ? min(p.kcs, nch_all - cb) : nch_all;
+    // raw barrier per chunk: LDS drained (lgkmcnt 0) but the next chunk's global loads left in flight
+    // (__syncthreads() also waits for vmcnt(0): the prefetch was then exposed every chunk)
+    auto barrier = [&]() {
+        asm volatile("" ::: "memory");       // no LDS access moves across (the intrinsics are IntrNoMem)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
     load(cb * GBK);
     store(0);
-    __syncthreads();
+    barrier();
     for (int c = 0; c < nch; ++c) {
         const int cur = c & 1;
         if (c + 1 < nch) load((cb + c + 1) * GBK);
@@ -194,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
             for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.w, fb[n].w, acc[n], 0, 0, 0);
         }
         if (c + 1 < nch) store(cur ^ 1);
-        __syncthreads();
+        barrier();
     }
     if (p.part) {  // raw partial sums of this K split, dense [M][N]
         float* P = p.part + ((size_t)sk * gridDim.y / p.nsplit + z) * (size_t)p.M * p.N;
@@ -210,20 +218,39 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
         }
         return;
     }
+    // every load (bias, beta C) before the first store: vmcnt orders loads and stores together, so a load
+    // behind a store waits for the store's acknowledgement (the old per-element C read between the
+    // stores serialised the epilogue of the beta = 1 residual linears)
+    float bv[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int col = min(n0 + n * 32 + li, p.N - 1);
+        bv[n] = p.bias ? p.bias[col] : 0.f;
+    }
+    if (p.beta != 0.f) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int col = min(n0 + n * 32 + li, p.N - 1);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = min(m0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, p.M - 1);
+                acc[n][r] = p.alpha * acc[n][r] + p.beta * C[row * p.scm + col * p.scn];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[n][r] = p.alpha * acc[n][r];
+    }
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
         const int col = n0 + n * 32 + li;
         if (col >= p.N) continue;
-        const float bv = p.bias ? p.bias[col] : 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = m0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (row < p.M) {
-                float* cp = C + row * p.scm + col * p.scn;
-                float v = p.alpha * acc[n][r];
-                if (p.beta != 0.f) v += p.beta * *cp;
-                *cp = v + bv;
-            }
+            if (row < p.M) C[row * p.scm + col * p.scn] = acc[n][r] + bv[n];
         }
     }
 }
