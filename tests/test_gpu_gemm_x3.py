@@ -170,3 +170,27 @@ def test_h2_records_roundtrip():
         rowmax = ref.abs().max(dim=1, keepdim=True).values
         assert ((val - ref).abs() <= rowmax * 2.0 ** -21).all()
         assert torch.equal(torch.log2(inv), torch.round(torch.log2(inv)))
+
+
+def test_linear_fn_x3_vs_fp32():
+    """functional.LinearFn with the weight's max word (f16x3 forward, dgrad, wgrad) against the fp32-MFMA
+    LinearFn on the same inputs: outputs and all three gradients within 4e-6 of their bounds"""
+    from toycrystals_amd import functional as TF
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, K, N = 256, 1024, 512
+    x = torch.randn(M, K, device="cuda", generator=g).requires_grad_()
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.03).requires_grad_()
+    b = torch.randn(N, device="cuda", generator=g).requires_grad_()
+    r = torch.randn(M, N, device="cuda", generator=g)
+    gy = torch.randn(M, N, device="cuda", generator=g) * 1e-3
+    outs = []
+    for aw in (None, words(w)):
+        y = TF.LinearFn.apply(x, w, b, r, aw)
+        dx, dw, db = torch.autograd.grad(y, (x, w, b), gy)
+        outs.append((y, dx, dw, db))
+    (y0, dx0, dw0, db0), (y1, dx1, dw1, db1) = outs
+    x64, w64, g64 = x.detach().double(), w.detach().double(), gy.double()
+    for a, c, bound in ((y1, y0, x64.abs() @ w64.abs().t() + 1.0), (dx1, dx0, g64.abs() @ w64.abs()),
+                        (dw1, dw0, g64.abs().t() @ x64.abs())):
+        assert ((a.double() - c.double()).abs() / bound).max().item() <= 2 * TOL
+    assert torch.equal(db1, db0)

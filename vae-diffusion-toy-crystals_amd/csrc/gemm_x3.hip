@@ -20,8 +20,8 @@
 // the fp32-MFMA rate per instruction (5.3x per fp32-equivalent FLOP).
 //
 // Tile 128 x 128, 4 waves of 64 x 64 (2 x 2 MFMA tiles, 64 accumulator AGPRs), LDS images of 128 rows
-// x 128 B per operand, double buffered (64 KB: two workgroups per CU), global loads one chunk ahead in
-// registers.  The 16-B unit u (k group u >> 1, hi / lo u & 1) of row r sits at u ^ ((r >> 1) & 7): a
+// x 128 B per operand, double buffered (64 KB: two workgroups per CU), global loads X3_PF chunks ahead
+// in registers.  The 16-B unit u (k group u >> 1, hi / lo u & 1) of row r sits at u ^ ((r >> 1) & 7): a
 // ds_read_b128 lane group (16 rows of one k group) covers 16 distinct 16-B bank slots.  When the
 // output tiles cannot fill the chip the reduction is split (grid.y) into raw partials [split][M][N],
 // folded in a fixed order by k_x3_reduce with the epilogue (deterministic).
@@ -29,6 +29,8 @@
 #include "h2.hpp"
 
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 
 namespace tcx {
 namespace {
@@ -39,6 +41,12 @@ constexpr int XT = 128;          // tile rows of either operand
 constexpr int XK = 32;           // reduction depth per chunk
 constexpr int XROW = 128;        // LDS bytes per tile row: 4 k groups x (hi 16 B + lo 16 B)
 constexpr int XIMG = XT * XROW;  // one operand image (16 KB)
+constexpr int X3_PF = 4;         // register stages of the global-load pipeline
+
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
 
 struct X3Params {
     int M, N, K;
@@ -171,7 +179,7 @@ struct X3Stage {
 };
 
 template <int LB>
-__global__ __launch_bounds__(256, 2) void k_gemm_x3(X3Params p) {
+__global__ __launch_bounds__(256, 1) void k_gemm_x3(X3Params p) {
     mfma_agpr_form();
     __shared__ __attribute__((aligned(16))) char lds[2 * 2 * XIMG];  // [buf][A | B]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 31, lh = lane >> 5;
@@ -184,16 +192,21 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(X3Params p) {
     const int eb = LB == 2 ? 0 : x3_exp_bits(*p.amax_b);
     const float sb = __builtin_ldexpf(1.f, eb);
 
-    X3Stage<2> sta;
-    X3Stage<LB> stb;
-    auto load = [&](int c) {
-        sta.load_h2(p.A, p.M, p.K, m0, c * XK, tid);
-        if constexpr (LB == 2) stb.load_h2(p.Bh, p.N, p.K, n0, c * XK, tid);
-        else stb.load_f32(p.B, (int)p.sbn, (int)p.sbk, p.N, p.K, n0, c * XK, tid);
+    // PF register stages: chunk i is loaded PF iterations before it is consumed (stage (i - c0) % PF),
+    // stored to LDS buffer (i - c0) & 1 at the end of iteration i - 1; PF - 1 iterations of MFMA cover
+    // each load's latency (one stage ahead left it exposed: r04_y, ~30 us per fc1-sized GEMM)
+    X3Stage<2> sta[X3_PF];
+    X3Stage<LB> stb[X3_PF];
+    auto load = [&](int c, auto Q) {
+        constexpr int q = decltype(Q)::value;
+        sta[q].load_h2(p.A, p.M, p.K, m0, c * XK, tid);
+        if constexpr (LB == 2) stb[q].load_h2(p.Bh, p.N, p.K, n0, c * XK, tid);
+        else stb[q].load_f32(p.B, (int)p.sbn, (int)p.sbk, p.N, p.K, n0, c * XK, tid);
     };
-    auto store = [&](int buf) {
-        sta.store(lds + buf * 2 * XIMG, 1.f, tid);
-        stb.store(lds + buf * 2 * XIMG + XIMG, sb, tid);
+    auto store = [&](int buf, auto Q) {
+        constexpr int q = decltype(Q)::value;
+        sta[q].store(lds + buf * 2 * XIMG, 1.f, tid);
+        stb[q].store(lds + buf * 2 * XIMG + XIMG, sb, tid);
     };
 
     f32x16 acc[2][2];
@@ -212,14 +225,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(X3Params p) {
         uo[s][0] = ((2 * g) ^ sw) << 4;
         uo[s][1] = ((2 * g + 1) ^ sw) << 4;
     }
-    if (c0 < c1) {
-        load(c0);
-        store(0);
-    }
-    __syncthreads();
-    for (int c = c0; c < c1; ++c) {
-        const int cur = (c - c0) & 1;
-        if (c + 1 < c1) load(c + 1);
+    auto compute = [&](int cur) {
         const char* ia = lds + cur * 2 * XIMG;
         const char* ib = ia + XIMG;
 #pragma unroll
@@ -246,28 +252,87 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(X3Params p) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
-        if (c + 1 < c1) store(cur ^ 1);
-        __syncthreads();
+    };
+    // raw barrier: LDS traffic drained (lgkmcnt 0), the global loads of later chunks left in flight —
+    // __syncthreads() would also wait for vmcnt(0), i.e. for every prefetch issued this iteration
+    auto barrier = [&]() {
+        asm volatile("" ::: "memory");       // no LDS access moves across (the intrinsics are IntrNoMem)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    static_for([&](auto Q) {
+        if (c0 + decltype(Q)::value < c1) load(c0 + decltype(Q)::value, Q);
+    }, std::make_integer_sequence<int, X3_PF>{});
+    if (c0 < c1) store(0, std::integral_constant<int, 0>{});
+    barrier();
+    for (int base = c0; base < c1; base += X3_PF) {
+        static_for([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            const int i = base + q;
+            if (i < c1) {
+                if (i + X3_PF < c1) load(i + X3_PF, Q);
+                compute((i - c0) & 1);
+                if (i + 1 < c1) store((i + 1 - c0) & 1, std::integral_constant<int, (q + 1) % X3_PF>{});
+                barrier();
+            }
+        }, std::make_integer_sequence<int, X3_PF>{});
     }
+    // Epilogue: every load (row / column scales, bias, residual, beta C) is issued before the first
+    // store — vmcnt counts loads and stores in one order, so a load behind a store would wait for that
+    // store's acknowledgement (the first form loaded inv_a[m] per element between the stores: ~30 us per
+    // GEMM of serialised round trips, r04_za)
     const float ib_t = __builtin_ldexpf(1.f, -eb);
     float* P = p.part ? p.part + (size_t)split * p.M * p.N : nullptr;
+    float sa_r[2][16], sb_c[2], bias_c[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            sa_r[i][r] = p.inva[m < p.M ? m : p.M - 1];
+        }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = min(n0 + wn * 64 + 32 * j + li, p.N - 1);
+        sb_c[j] = LB == 2 ? p.invb[n] : ib_t;
+        bias_c[j] = (!P && p.bias) ? p.bias[n] : 0.f;
+    }
+    const bool extra = !P && (p.resid || p.beta != 0.f);
+    if (extra) {  // residual / beta C of all 64 outputs, into the accumulators' scaled values
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = min(m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh, p.M - 1);
+                    const int n = min(n0 + wn * 64 + 32 * j + li, p.N - 1);
+                    float add = 0.f;
+                    if (p.resid) add = p.resid[(size_t)m * p.ldr + n];
+                    if (p.beta != 0.f) add += p.beta * p.C[(size_t)m * p.ldc + n];
+                    acc[i][j][r] = fmaf(p.alpha, acc[i][j][r] * sa_r[i][r] * sb_c[j], add);
+                }
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int n = n0 + wn * 64 + 32 * j + li;
         if (n >= p.N) continue;
-        const float ibn = LB == 2 ? p.invb[n] : ib_t;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
                 if (m >= p.M) continue;
-                const float v = acc[i][j][r] * p.inva[m] * ibn;
                 if (P) {
-                    P[(size_t)m * p.N + n] = v;
+                    P[(size_t)m * p.N + n] = acc[i][j][r] * sa_r[i][r] * sb_c[j];
                 } else {
-                    float* cp = p.C + (size_t)m * p.ldc + n;
-                    *cp = x3_epi(p, v, m, n, cp);
+                    float v = extra ? acc[i][j][r] : p.alpha * (acc[i][j][r] * sa_r[i][r] * sb_c[j]);
+                    v += bias_c[j];
+                    if (p.act == 1) v = fmaxf(v, 0.f);
+                    else if (p.act == 2) v = 1.f / (1.f + expf(-v));
+                    else if (p.act == 3) v = silu_f(v);
+                    p.C[(size_t)m * p.ldc + n] = v;
                 }
             }
         }
@@ -312,26 +377,28 @@ __global__ __launch_bounds__(256) void k_h2_rows(const float* __restrict__ x, in
 }
 
 // h2 rows of x^T for x [R][C] (row stride ldx): output row c = column c of x (R values, R % 8 == 0),
-// scaled by the column's max.  One workgroup per 64 columns: pass 1 the column maxima (thread: column
-// tid & 63, rows tid >> 6 + 4 i), pass 2 (L2-hot) the records, 8 rows of one column per unit.
+// scaled by the column's max.  One workgroup per 16 columns (thread: column tid & 15, row group
+// tid >> 4): pass 1 the column maxima, pass 2 (L2-hot) the records, 8 rows of one column per unit.
 __global__ __launch_bounds__(256) void k_h2_cols(const float* __restrict__ x, int R, int C, long long ldx, char* out,
                                                  float* inv) {
-    __shared__ float cm[4][64];
-    const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + cl;
+    __shared__ float cm[16][17];
+    const int cl = threadIdx.x & 15, q = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + cl;
     const bool cv = c < C;
     float m = 0.f;
     if (cv)
-        for (int r = q; r < R; r += 4) m = fmaxf(m, fabsf(x[(size_t)r * ldx + c]));
+        for (int r = q; r < R; r += 16) m = fmaxf(m, fabsf(x[(size_t)r * ldx + c]));
     cm[q][cl] = m;
     __syncthreads();
-    m = fmaxf(fmaxf(cm[0][cl], cm[1][cl]), fmaxf(cm[2][cl], cm[3][cl]));
+    m = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m = fmaxf(m, cm[i][cl]);
     const int e = x3_exp_bits(__float_as_uint(m));
     const float s = __builtin_ldexpf(1.f, e);
     if (!cv) return;
     if (q == 0) inv[c] = __builtin_ldexpf(1.f, -e);
     char* orow = out + (size_t)c * R * 4;
-    for (int g = q; g < R / 8; g += 4) {
+    for (int g = q; g < R / 8; g += 16) {
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = x[(size_t)(8 * g + j) * ldx + c];
@@ -397,7 +464,7 @@ extern "C" int tcx_h2_cols(const float* x, int R, int C, long long ldx, void* ou
     TCX_REQUIRE(x && out && inv && R > 0 && R % 8 == 0 && C >= 0 && ldx >= C && aligned16(out),
                 "tcx_h2_cols: R %% 8");
     if (C == 0) return TCX_OK;
-    hipLaunchKernelGGL(k_h2_cols, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, x, R, C, ldx,
+    hipLaunchKernelGGL(k_h2_cols, dim3(cdiv(C, 16)), dim3(256), 0, (hipStream_t)stream, x, R, C, ldx,
                        static_cast<char*>(out), inv);
     return check_launch("tcx_h2_cols");
 }

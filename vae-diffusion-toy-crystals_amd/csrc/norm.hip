@@ -650,17 +650,30 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
     bool bad = false;
     // In place (x == y): the compiler must assume each store may alias the next loads, so the
     // loads of GU groups are issued explicitly before any of their stores (each thread's groups
-    // are distinct elements) — one group in flight per thread measured 4.85 TB/s.
+    // are distinct elements) — one group in flight per thread measured 4.85 TB/s.  Software-pipelined:
+    // the NEXT batch's loads are issued before this batch's stores, since vmcnt orders loads and
+    // stores together (a load issued behind a store cannot be waited for without that store's
+    // acknowledgement, which serialised the batches).
     constexpr int GU = 4;
     int i = threadIdx.x;
+    float4 n0[GU], n1[GU];
+    auto issue = [&](int at) {
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+            const float* src = x + base + (size_t)(at + 256 * k) * 8;
+            n0[k] = *reinterpret_cast<const float4*>(src);
+            n1[k] = *reinterpret_cast<const float4*>(src + 4);
+        }
+    };
+    if (i + (GU - 1) * 256 < n8) issue(i);
     for (; i + (GU - 1) * 256 < n8; i += GU * 256) {
         float4 u0[GU], u1[GU];
 #pragma unroll
         for (int k = 0; k < GU; ++k) {
-            const float* src = x + base + (size_t)(i + 256 * k) * 8;
-            u0[k] = *reinterpret_cast<const float4*>(src);
-            u1[k] = *reinterpret_cast<const float4*>(src + 4);
+            u0[k] = n0[k];
+            u1[k] = n1[k];
         }
+        if (i + GU * 256 + (GU - 1) * 256 < n8) issue(i + GU * 256);
 #pragma unroll
         for (int k = 0; k < GU; ++k) {
             const int c0 = ((i + 256 * k) % C8) * 8;

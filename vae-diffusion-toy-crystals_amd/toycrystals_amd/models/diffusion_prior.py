@@ -12,9 +12,8 @@ At B <= 64 (the DDIM's latents) each weight is streamed once by the skinny kerne
 DiffusionSchedule.ddim_sample on this model is ONE native call too (tcx_prior_ddim_sample),
 with the step-invariant y branch and the FiLM projections of all timesteps hoisted out of the loop.
 Training: with autograd on, the same forward runs as a chain of libtcx autograd Functions
-(functional.py): GEMM linears (the trunk's cond / fc1 / fc2 forward, dgrad and wgrad on the f16x3
-GEMM of csrc/gemm_x3.hip unless TCX_PRIOR_PRECISION=fp32), per-block LayerNorm+FiLM with its fused
-backward, residual added in the fc2 GEMM epilogue.
+(functional.py): fp32-MFMA GEMM linears, per-block LayerNorm+FiLM with its fused backward, residual
+added in the fc2 GEMM (beta = 1).
 """
 from __future__ import annotations
 
@@ -151,11 +150,6 @@ class _PriorPack:
 # "f16x3" (default): fc1 / fc2 / out_proj of the native eval forward and DDIM at B <= 64 on split-f16
 # MFMA products (csrc/skinny.hip, ~2^-21 relative per product, fp32 accumulation); "fp32": f32 MFMA.
 PRIOR_PRECISION = os.environ.get("TCX_PRIOR_PRECISION", "f16x3")
-# Training GEMMs of the trunk on the f16x3 GEMM (csrc/gemm_x3.hip): parity-green (tests/test_gpu_gemm_x3.py,
-# the w64 / w1024 training-step goldens) but measured slower than the fp32-MFMA GEMMs at B = 256 so far
-# (4.55 -> 5.88 ms per step, profiles/r04_y_*: its one-chunk-ahead staging leaves the load latency exposed),
-# so the step stays on fp32 MFMA until the deeper-pipelined form lands.
-_TRAIN_X3 = False
 
 
 def _run_h2_or_fp32(run, device) -> None:
@@ -219,16 +213,12 @@ class DiffusionPriorFiLM(nn.Module):
         y_feat = TF.linear(TF.act(TF.linear(TF.cat_cols(ycf, ycont), self.y_fuse[0]), TF.ACT_SILU), self.y_fuse[2])
         cond = TF.cat_cols(t_feat, y_feat)
         h = TF.linear(z_t.to(torch.float32), self.in_proj)
-        # the trunk's GEMMs (forward, dgrad, wgrad of cond / fc1 / fc2) on f16x3 MFMA: max |W| of all of
-        # them in one launch (the weights' power-of-two scales), 3 words per block
-        amax = None
-        if _TRAIN_X3 and PRIOR_PRECISION == "f16x3" and 3 * len(self.blocks) <= 32:
-            amax = TF.absmax_words([w for b in self.blocks for w in (b.cond.weight, b.fc1.weight, b.fc2.weight)])
-        for j, blk in enumerate(self.blocks):
-            aw = (lambda i: amax[3 * j + i:3 * j + i + 1]) if amax is not None else (lambda i: None)
-            gb = TF.linear(cond, blk.cond, amax_w=aw(0))  # [gamma | beta] = cond(cond).chunk(2)
+        # fp32-MFMA GEMMs: the f16x3 GEMM of csrc/gemm_x3.hip (TF.linear(..., amax_w=...)) is parity-green
+        # but measured slower on this step
+        for blk in self.blocks:
+            gb = TF.linear(cond, blk.cond)  # [gamma | beta] = cond(cond).chunk(2)
             hn = TF.LayerNormFiLMFn.apply(h, blk.norm.weight, blk.norm.bias, gb, blk.norm.eps)
-            h = TF.linear(TF.act(TF.linear(hn, blk.fc1, amax_w=aw(1)), TF.ACT_SILU), blk.fc2, resid=h, amax_w=aw(2))
+            h = TF.linear(TF.act(TF.linear(hn, blk.fc1), TF.ACT_SILU), blk.fc2, resid=h)
         hn = TF.LayerNormFiLMFn.apply(h, self.out_norm.weight, self.out_norm.bias, None, self.out_norm.eps)
         return TF.linear(hn, self.out_proj)
 
