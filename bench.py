@@ -52,15 +52,16 @@ FP32_PEAK_TFLOPS = 157.3         # MI355X fp32 MFMA (= vector) peak, MI355X_MICR
 F16_PEAK_TFLOPS = 2500.0         # MI355X dense f16/bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 multiply-add
 # HBM bytes per conv launch (the launches the roofline times), measured by rocprofv3 PMC passes on
-# this sampler (tools/gpu/verify.sh -> tools/pmc_traffic.py, profiles/r02_zq_pmc_traffic.txt):
+# this sampler in the roofline's own configuration (one lane: Bt = 256 rows per launch, as the timed
+# one-lane pass; tools/gpu/r04r.sh -> tools/pmc_traffic.py, profiles/r04_fin_pmc_traffic.txt):
 # FETCH_SIZE x 2 (gfx950 reports half of 16-B/lane reads) + WRITE_SIZE, averaged over the conv
-# launches of an evaluation.  A counter pass cannot run inside this process, so the
-# measured value is carried here with its source; it applies to the f16x3 path it was taken on.
-TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 262.1e6}
-TRAFFIC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE, averaged over the 270 split-path conv launches "
-                  "(k_conv3lg 16/32/64 h2 and 32/64 GN+SiLU prologue, k_conv3g 16 prologue, k_conv4s2g, k_lin1x1) of "
-                  "two sampler steps, profiles/r03_r_pmc_traffic.txt (earlier rounds' 503 MB also averaged in the "
-                  "fp32 comparison pass's k_conv launches, ~1.2 GB each)")
+# launches of two sampler steps.  A counter pass cannot run inside this process, so the measured
+# value is carried here with its source; it applies to the f16x3 path it was taken on.
+TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 523.1e6}
+TRAFFIC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE in separate passes over bench.py --lanes 1 "
+                  "(Bt = 256 per launch, the one-lane pass the roofline times), averaged over the 135 split-path "
+                  "conv launches (k_conv3lg 16/32/64 h2 and 32/64 GN+SiLU prologue, k_conv3g 16 prologue, "
+                  "k_conv4s2g, k_lin1x1) of two sampler steps, profiles/r04_fin_pmc_traffic.txt")
 
 
 def _cpu_model() -> str:
