@@ -67,12 +67,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
     const int m0 = mblk * GBM, n0 = nblk * BN;
     const int tid = threadIdx.x;
 
-    // two register stages (chunk c + 2 loads while chunk c multiplies and chunk c + 1 is stored)
-    float ra2[2][16];
-    float rb2[2][4 * NT];
-    auto load = [&](int k0, int S) {
-        float* ra = ra2[S];
-        float* rb = rb2[S];
+    float ra[16];
+    float rb[4 * NT];
+    auto load = [&](int k0) {
         // A tile: 128 rows x 32 k
         if constexpr (LA == 0) {
             const int k4 = tid & 7, pr = tid >> 3;
@@ -126,9 +123,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
             }
         }
     };
-    auto store = [&](int buf, int S) {
-        const float* ra = ra2[S];
-        const float* rb = rb2[S];
+    auto store = [&](int buf) {
         if constexpr (LA == 0) {
             const int k4 = tid & 7, pr = tid >> 3;
 #pragma unroll
@@ -184,13 +179,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-    if (nch > 0) load(cb * GBK, 0);
-    if (nch > 1) load((cb + 1) * GBK, 1);
-    if (nch > 0) store(0, 0);
+    load(cb * GBK);
+    store(0);
     barrier();
-    auto step = [&](int c, int S) {
+    for (int c = 0; c < nch; ++c) {
         const int cur = c & 1;
-        if (c + 2 < nch) load((cb + c + 2) * GBK, S);
+        if (c + 1 < nch) load((cb + c + 1) * GBK);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const float4 fa = *reinterpret_cast<const float4*>(&As[cur][(wv * 32 + li) * GLD + lh * 16 + g * 4]);
@@ -207,12 +201,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmParams p) {
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.w, fb[n].w, acc[n], 0, 0, 0);
         }
-        if (c + 1 < nch) store(cur ^ 1, S ^ 1);
+        if (c + 1 < nch) store(cur ^ 1);
         barrier();
-    };
-    for (int c = 0; c < nch; c += 2) {
-        step(c, 0);
-        if (c + 1 < nch) step(c + 1, 1);
     }
     if (p.part) {  // raw partial sums of this K split, dense [M][N]
         float* P = p.part + ((size_t)sk * gridDim.y / p.nsplit + z) * (size_t)p.M * p.N;
@@ -641,11 +631,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
     const bool asrc1 = aci < p.C1;
     const int aC = asrc1 ? p.C1 : p.C2;
     const int aoff = (asrc1 ? aci : aci - p.C1) * 4 + 16 * apl;  // byte offset within the pixel record
-    // two register stages: chunk c + 2 is loaded while chunk c is multiplied and chunk c + 1 (loaded one
-    // iteration earlier) is stored, so a load has a whole iteration of MFMAs to land (one stage left
-    // the next chunk's load latency exposed before every store)
-    float4 ra[2][4], rb[2][NT];
-    auto load = [&](int c, int S) {
+    float4 ra[4], rb[NT];
+    auto load = [&](int c) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = (tid >> 5) + 8 * i;
@@ -663,7 +650,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
                 ok = ok && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
             }
             const int off = ok ? ((b * p.H + yy) * p.W + xx) * aC * 4 + aoff : OOB;
-            ra[S][i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc1 ? r1 : r2, off, 0, 0));
+            ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc1 ? r1 : r2, off, 0, 0));
         }
 #pragma unroll
         for (int i = 0; i < NT; ++i) {  // B pieces: idx = tid + 256 i -> row idx / (2 OB), piece idx % (2 OB)
@@ -674,23 +661,23 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
             const int co = c0 + 8 * oc;
             const bool ok = m < p.M && co < p.Cout;
             const int off = ok ? (m * p.Cout + co) * 4 + 16 * pl : OOB;
-            rb[S][i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0));
+            rb[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0));
         }
     };
-    auto store = [&](int buf, int S) {
+    auto store = [&](int buf) {
         char* A = wsm + buf * STG;
         char* B = A + AB;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = (tid >> 5) + 8 * i;
-            *reinterpret_cast<float4*>(A + row * ROWB + 16 * (16 * apl + (aoc ^ (4 * (row & 3))))) = ra[S][i];
+            *reinterpret_cast<float4*>(A + row * ROWB + 16 * (16 * apl + (aoc ^ (4 * (row & 3))))) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             const int idx = tid + 256 * i;
             const int row = idx / (2 * OB), q = idx - row * (2 * OB);
             const int pl = q / OB, oc = q - pl * OB;
-            *reinterpret_cast<float4*>(B + row * ROWB + 16 * (16 * pl + (oc ^ (4 * (row & 3))))) = rb[S][i];
+            *reinterpret_cast<float4*>(B + row * ROWB + 16 * (16 * pl + (oc ^ (4 * (row & 3))))) = rb[i];
         }
     };
     f32x16 acc[NT];
@@ -715,21 +702,14 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
         const v8s u = __builtin_shufflevector(u0, u1, 0, 1, 2, 3, 4, 5, 6, 7);
         return __builtin_bit_cast(h8, u);
     };
-    // raw barrier: LDS drained, the next chunks' global loads left in flight (__syncthreads() would also
-    // wait for vmcnt(0)); the empty asm keeps LDS accesses from moving across it
-    auto barrier = [&]() {
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    if (chunk0 < chunk1) load(chunk0, 0);
-    if (chunk0 + 1 < chunk1) load(chunk0 + 1, 1);
-    if (chunk0 < chunk1) store(0, 0);
-    barrier();
-    auto step = [&](int c, int S) {  // chunk c sits in LDS buffer (c - chunk0) & 1; its stage S is free
+    if (chunk0 < chunk1) {
+        load(chunk0);
+        store(0);
+    }
+    __syncthreads();
+    for (int c = chunk0; c < chunk1; ++c) {
         const int cur = (c - chunk0) & 1;
-        if (c + 2 < chunk1) load(c + 2, S);
+        if (c + 1 < chunk1) load(c + 1);
         const char* A = wsm + cur * STG;
         const char* B = A + AB;
 #pragma unroll
@@ -750,12 +730,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h2(WgParams p) {
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah, fbh[n], acc[n], 0, 0, 0);
         }
-        if (c + 1 < chunk1) store(cur ^ 1, S ^ 1);
-        barrier();
-    };
-    for (int c = chunk0; c < chunk1; c += 2) {
-        step(c, 0);
-        if (c + 1 < chunk1) step(c + 1, 1);
+        if (c + 1 < chunk1) store(cur ^ 1);
+        __syncthreads();
     }
     const float sc = *p.comb;
     float* dst = p.part + (size_t)split * p.K * p.Cout;
