@@ -125,6 +125,22 @@ __device__ __forceinline__ bool conv_epi_fast(const ConvParams& p, int m0) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// A VMEM store of more than 8 bytes reads its data VGPRs after it issues, so a VALU write to those
+// VGPRs must not follow it directly.  hipcc pads that hazard inside a basic block but not across the
+// join of an if / else whose branch ends in the store: the next block's first instruction rewrote
+// the store's first dword with no wait state, and the stored value was the old or the new one at
+// random — the bf16 quad-epilogue nondeterminism (one dword per 32 x 32 block: rt 0, n 1, rows
+// 24-31, channels 12 / 28, tools/lbbench.py WHERE=1, profiles/r04_lbwhere.log) and k_conv3m's
+// co-run differences (45 such sites).  Every 16-B epilogue store goes through this: a sched_barrier
+// keeps the scheduler from moving the overwrite above the s_nop.  tools/store_hazard_check.py scans
+// the assembly for the pattern (0 sites at HEAD).
+__device__ __forceinline__ void store_b128_guarded(u32x4 v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 1");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // 4x4 transpose across the 4 lanes of a DPP quad (lane i = lane & 3): element r of lane i becomes
 // element i of lane r, in two butterfly stages of quad_perm moves (xor 1, xor 2).  An accumulator
 // column (one channel, 4 consecutive output rows per lane) turns into 4 consecutive channels of one
@@ -288,8 +304,7 @@ __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 
                     __builtin_amdgcn_raw_buffer_store_b64(lo, ry, voh + 16, so, 0);
                     bad = bad || (!bf && (h2_bad(v[0]) || h2_bad(v[1]) || h2_bad(v[2]) || h2_bad(v[3])));
                 } else {
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])),
-                                                           ry, vo32, so, 0);
+                    store_b128_guarded(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry, vo32, so);
                 }
             }
             h2_flag(p.ovf, bad);
@@ -306,16 +321,12 @@ __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 
     }
 }
 
-// bf16 (SPL 2) keeps the column form: with the quad form, k_conv3lb<128 / 256> (config 5's 256^2 rows)
-// returned run-to-run different outputs (tools/dbg_bf16.py: 1.25e-1 .. 1.59e-1 of the output scale,
-// errors in 64-pixel blocks; profiles/r04_w_dbg_quad.log) while the column form is deterministic and
-// within the bf16 gate (7.8e-3, r04_x_dbg_v1.log); the quad form at 64^2 bf16 and every f16x3 / fp32
-// kernel are deterministic (determinism probe, r04_u).  Cause not isolated (no SrcC reuse hazard in
-// either form: tools/mfma_war_check.py).
+// (Round 4: bf16 had kept the column form after the quad form gave run-to-run different outputs in
+// k_conv3lb; the cause was the store-data hazard of store_b128_guarded, now padded.)
 template <int NT, int SPL, int NW, int RT>
 __device__ __forceinline__ void conv_epi_store_fast(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
                                                     int wv0, int lane, double* red) {
-    if (p.resid || SPL == 2) conv_epi_store_cols<NT, SPL, NW, RT>(p, acc, m0, n0, wv0, lane, red);  // attention proj, bf16
+    if (p.resid) conv_epi_store_cols<NT, SPL, NW, RT>(p, acc, m0, n0, wv0, lane, red);  // attention proj
     else if (p.act == 0) conv_epi_store_quad<NT, SPL, NW, RT, false>(p, acc, m0, n0, wv0, lane, red);
     else conv_epi_store_quad<NT, SPL, NW, RT, true>(p, acc, m0, n0, wv0, lane, red);
 }
