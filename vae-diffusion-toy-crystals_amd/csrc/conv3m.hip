@@ -189,22 +189,6 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
 #pragma unroll
         for (int n = 0; n < 6; ++n) acc[rb][n] = (f32x4){};
     h8 a_h[4], a_l[4], b_h[3], b_l[3];
-    // Before a ds_read overwrites A / B fragment registers, read the accumulator of the last MFMA that
-    // used them: the wave then issues the load only once that MFMA (and, in order, every earlier one) has
-    // finished.  Without it, a load issued right behind the MFMAs reading its destination registers
-    // corrupted single B columns of some 16x16 blocks whenever other kernels shared the CU (the sampling
-    // lanes: r04_n..q, tools/determinism_probe.py --corun: 7e4 wrong outputs per 10 launches, 0 with this
-    // dependency).  The read is a v_accvgpr_read behind the compiler's MFMA-result wait states.
-    auto dep = [&](int rb, int nb) {
-        float t = acc[rb][nb][0];
-        asm volatile("" ::"v"(t) : "memory");
-    };
-    // after a column block's 12 MFMAs: all four accumulators (the compiler may issue the independent row
-    // blocks in any order, so no single one is known to be last)
-    auto dep_col = [&](int nb) {
-        float t0 = acc[0][nb][0], t1 = acc[1][nb][0], t2 = acc[2][nb][0], t3 = acc[3][nb][0];
-        asm volatile("" ::"v"(t0), "v"(t1), "v"(t2), "v"(t3) : "memory");
-    };
     auto rd_a = [&](int q, int rb) {
         a_h[rb] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + aq[q] + rbo(rb)));
         a_l[rb] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + (aq[q] ^ 16) + rbo(rb)));
@@ -262,7 +246,6 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         for (int i = 0; i < 3; ++i) {
             mf_col(i, i);
             __builtin_amdgcn_sched_barrier(0);
-            dep_col(i);
             rd_b(i, k, 3 + i);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -289,7 +272,6 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         for (int i = 0; i < 2; ++i) {
             mf_col(3 + i, i);
             __builtin_amdgcn_sched_barrier(0);
-            dep_col(3 + i);
             rd_b(i, k + 1, i);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -297,11 +279,9 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         for (int rb = 0; rb < 4; ++rb) {
             mf3(rb, 5, 2);
             __builtin_amdgcn_sched_barrier(0);
-            dep(rb, 5);
             rd_a(qn, rb);
             __builtin_amdgcn_sched_barrier(0);
         }
-        dep_col(5);
         rd_b(2, k + 1, 2);
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -377,8 +357,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
                                                           ry, voh + 16, sh, 0);
                     bad = bad || h2_bad(v[0]) || h2_bad(v[1]) || h2_bad(v[2]) || h2_bad(v[3]);
                 } else {
-                    __builtin_amdgcn_raw_buffer_store_b128(
-                        __builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry, vo32, so, 0);
+                    store_b128_guarded(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry, vo32, so);
                 }
             }
             if constexpr (!FAST) h2_flag(p.ovf, bad);
@@ -443,25 +422,18 @@ int launch3m(const ConvParams& p, hipStream_t st) {
 
 }  // namespace
 
-// Opt-in (TCX_CONV3M=1): not the default.  Alone on the chip k_conv3m is exact and 3-10 % faster per
-// layer than k_conv3lg, but with other kernels sharing its CUs (the sampler's concurrent lanes, or any
-// concurrent stream) a few 16x16 blocks per launch get one wrong B column (tools/determinism_probe.py
-// --corun; profiles/r04_*_corun*.log): waiting for every MFMA that read a fragment register before a
-// ds_read overwrites it (dep / dep_col below) cut the rate from ~7e4 to ~2e2 wrong outputs per 20
-// launches but did not remove it, and k_conv3lg (32x32x16, the same DMA / barrier scheme) shows none.
-bool conv3m_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("TCX_CONV3M");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
+// Default for the h2-source 3x3 convs it covers (round 4).  It had been opt-in: with other kernels
+// sharing its CUs a few 16x16 blocks per launch got one wrong channel.  The cause was the store-data
+// hazard of its quad epilogue (a 16-B store's first data VGPR rewritten across an if/else join with no
+// wait state, conv_common.hpp store_b128_guarded), not the MFMA / ds_read order: with the pad and
+// without the MFMA-dependency waits that had only made it rarer, the co-run and sampler probes are
+// deterministic (profiles/r04_m_*) and the headline runs 79.9-80.1 -> 82.6-82.7 images/s.
 
 
 // called by launch_conv3l for the h2-source (PRO 0) form: k_conv3lg's conditions plus the fast
 // epilogue's (dense NHWC fp32 / h2 output, no per-batch bias or residual, 32-bit offsets)
 bool conv3m_takes(const ConvParams& p) {
-    return conv3m_enabled() && !p.bf && p.circular && p.sc1 == nullptr && !(p.C2 > 0 && p.sc2 != nullptr) &&
+    return !p.bf && p.circular && p.sc1 == nullptr && !(p.C2 > 0 && p.sc2 != nullptr) &&
            (p.W == 16 || p.W == 32 || p.W == 64) && p.M % M_TP == 0 && p.HoWo % M_TP == 0 && p.Cin % 32 == 0 &&
            p.Cin <= 384 && p.Cout % M_BN == 0 && p.osy == 1 && p.osx == 1 && p.bias_b == nullptr &&
            p.resid == nullptr && (long long)p.M * p.Cout < (1ll << 29) && p.wscale != nullptr;
