@@ -427,7 +427,7 @@ int launch3m(const ConvParams& p, hipStream_t st) {
 // hazard of its quad epilogue (a 16-B store's first data VGPR rewritten across an if/else join with no
 // wait state, conv_common.hpp store_b128_guarded), not the MFMA / ds_read order: with the pad and
 // without the MFMA-dependency waits that had only made it rarer, the co-run and sampler probes are
-// deterministic (profiles/r04_m_*) and the headline runs 79.9-80.1 -> 82.6-82.7 images/s.
+// deterministic (profiles/r04_m2_*) and the headline runs 79.9-80.1 -> 82.6-82.7 images/s.
 
 
 // called by launch_conv3l for the h2-source (PRO 0) form: k_conv3lg's conditions plus the fast
