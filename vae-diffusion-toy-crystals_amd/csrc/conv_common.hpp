@@ -134,8 +134,14 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // co-run differences (45 such sites).  Every 16-B epilogue store goes through this: a sched_barrier
 // keeps the scheduler from moving the overwrite above the s_nop.  tools/store_hazard_check.py scans
 // the assembly for the pattern (0 sites at HEAD).
+// AUX: the store's cache policy.  EPI_NT (non-temporal) for the bf16 convs' fp32 output, which at 256^2
+// (1.1 GB per launch) leaves the caches long before the apply pass reads it: k_conv3lb 64-px rows
+// 136-141 -> 124-125 us, 256-px rows 827-838 -> 787-822 us, config 5 7.00-7.02 -> 7.07-7.08 images/s
+// (profiles/r04_nt_*, alternating libraries in one call).
+constexpr int EPI_NT = 2;
+template <int AUX = 0>
 __device__ __forceinline__ void store_b128_guarded(u32x4 v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, AUX);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 1");
     __builtin_amdgcn_sched_barrier(0);
@@ -304,7 +310,7 @@ __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 
                     __builtin_amdgcn_raw_buffer_store_b64(lo, ry, voh + 16, so, 0);
                     bad = bad || (!bf && (h2_bad(v[0]) || h2_bad(v[1]) || h2_bad(v[2]) || h2_bad(v[3])));
                 } else {
-                    store_b128_guarded(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry, vo32, so);
+                    store_b128_guarded<SPL == 2 ? EPI_NT : 0>(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry, vo32, so);
                 }
             }
             h2_flag(p.ovf, bad);
