@@ -134,6 +134,42 @@ def test_bf16_convs_vs_float64_on_rounded_operands(B, C1, C2, H, co, ks, stride,
     assert err < 5e-6
 
 
+@pytest.mark.parametrize("Bt,H,C1,C2,co", [(8, 256, 96, 0, 96), (4, 256, 96, 96, 96), (16, 128, 96, 0, 192),
+                                            (32, 64, 192, 0, 192)])
+def test_bf16_conv3lb_repeats_bit_for_bit(Bt, H, C1, C2, co):
+    """k_conv3lb with the quad-transposed epilogue repeats bit for bit (output and GroupNorm partials)
+    into a NaN-filled output: the regression test of the store-data hazard (conv_common.hpp
+    store_b128_guarded) that made one dword per 32 x 32 block come out old or new at random
+    (profiles/r04_lbwhere.txt)."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x1 = to_bf16_records(torch.randn((Bt, H, H, C1), device="cuda", generator=g))
+    x2 = to_bf16_records(torch.randn((Bt, H, H, C2), device="cuda", generator=g)) if C2 else None
+    w = (rng.standard_normal((co, C1 + C2, 3, 3)) / np.sqrt(9 * (C1 + C2))).astype(np.float32)
+    wh, ws, cpad, kpad = pack_bf16(w)
+    wf = pack_frag(wh, cpad, kpad, C1 + C2)
+    b = dev(rng.standard_normal(co).astype(np.float32))
+    y = torch.empty((Bt, H, H, co), device="cuda")
+    gn = torch.zeros((Bt, H * H // 128, co, 2), dtype=torch.float64, device="cuda")
+
+    def run():
+        y.fill_(float("nan"))
+        gn.zero_()
+        chk(L().tcx_conv2d_h2_pro(x1.data_ptr(), x2.data_ptr() if x2 is not None else None, Bt, 0, H, H, C1, C2,
+                                  wh.data_ptr(), wf.data_ptr(), ws.data_ptr(), b.data_ptr(), None, None, y.data_ptr(),
+                                  0, co, cpad, kpad, 3, 1, 1, 1, 0, gn.data_ptr(), None, None, None, None, 1, None,
+                                  st()))
+        torch.cuda.synchronize()
+        return y.clone(), gn.clone()
+    y0, g0 = run()
+    assert not bool(torch.isnan(y0).any())
+    bad = 0
+    for _ in range(6):
+        y1, g1 = run()
+        bad += int((y1 != y0).sum()) + int((g1 != g0).sum())
+    print(f"k_conv3lb Bt={Bt} {H}² {C1}+{C2}->{co}: 6 repeats, {bad} differing values")
+    assert bad == 0
+
+
 @pytest.mark.parametrize("B,H", [(2, 64), (1, 256)])
 def test_bf16_conv3g_gn_prologue_vs_float64(B, H):
     """the prologue applies silu(x*scale+shift) in fp32 and rounds the result to bf16 in registers
