@@ -321,6 +321,20 @@ int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const
                       int B, int H, int W, int n_steps, float guidance, const float* scal_table,
                       int flags, void* ws, size_t ws_bytes, void* stream);
 
+/* Workspace of one sampler call (the library never allocates: every buffer is the caller's): the
+ * U-Net workspace of the (CFG-doubled) rows under the current lane setting, the conditioning tables
+ * of the call's n_steps + 1 step-table rows (time / condition maps and the per-(step, image)
+ * first-conv bias rows that replace the reference's per-call _make_maps, sde_score_model.py:227-241)
+ * and, for the PF-ODE, its drift / Euler-point images.  A smaller ws_bytes is TCX_EWS.  Query after
+ * tcx_set_sample_lanes. */
+size_t tcx_sde_workspace_size(const tcx_unet* net, int B, int H, int W, int n_steps, float guidance);
+size_t tcx_ode_workspace_size(const tcx_unet* net, int B, int H, int W, int n_steps, float guidance);
+
+/* Test hook for the samplers' error paths: the k-th U-Net evaluation after the call (k > 0) fails
+ * with TCX_EINVAL before launching anything (one shot; 0 disarms).  Every sampler exit joins its
+ * lane streams back into the caller's stream, so a failed call leaves nothing running unordered. */
+int tcx_debug_fail_eval(int k);
+
 /* tcx_sde_sample_ex on one shard of a larger sampling batch (batch-DP sampling):
  * the Philox counter of element i of x is e_base + i, so images [s, e) of a B-image batch sampled
  * with e_base = s*H*W are bit-identical to those rows of the whole batch sampled in one call with the

@@ -174,7 +174,8 @@ def test_trained_ode20_vs_reference(golden, prec):
     check_sampler_outputs("ode32_trained_20", out, x0, g)
 
 
-def test_trained_sde300_vs_reference(golden, prec, monkeypatch):
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_trained_sde300_vs_reference(golden, prec, monkeypatch, lanes):
     """The metric's sampler (300-step reverse SDE, CFG 1.5, t_end 0.005, base_ch 96) end to end on
     a genuinely trained model — tests/golden/trained96_ema.npz, the EMA weights of the README recipe
     (40 epochs, profiles/r02_a_recipe40_metrics.jsonl) — against the REFERENCE's CPU run of the same
@@ -185,8 +186,13 @@ def test_trained_sde300_vs_reference(golden, prec, monkeypatch):
     3.0e-5 relative on x0_hat (tests/golden/sde96_trained_300_fp64.npz, make_fp64_floor.py); this
     path is gated at 1e-4 against BOTH.  A single step-table scalar perturbed by 1e-5 moves x0_hat
     by at most ~2e-5 (printed), below that floor: no gate can see it.  Discrimination: alpha(t_end)
-    scaled by 1 + 2e-4 (a ~2e-4 change of x0_hat, ~7x the floor) must fail the gate."""
+    scaled by 1 + 2e-4 (a ~2e-4 change of x0_hat, ~7x the floor) must fail the gate.
+
+    `lanes` = 4 is bench.py's timed configuration (tcx_set_sample_lanes(4): the batch as four
+    concurrent per-stream chains, two images each here): the same gates, and the outputs must equal
+    the one-lane run bit for bit."""
     import toycrystals_amd.models.sde_score_model as S
+    from toycrystals_amd._lib import lib
     from toycrystals_amd.models.sde_score_model import host_noise
     g = golden("sde96_trained_300")
     f64 = golden("sde96_trained_300_fp64")["x0_fp64"]
@@ -194,12 +200,24 @@ def test_trained_sde300_vs_reference(golden, prec, monkeypatch):
     B, steps = int(g["B"]), int(g["steps"])
     torch.manual_seed(int(g["noise_seed"]))
     noise = host_noise((B, 1, 64, 64), steps + 1).cuda()
-    out, x0 = run_sde(m, g, noise, (B, 1, 64, 64))
-    check_sampler_outputs(f"sde96_trained_300 ({prec})", out, x0, g)
+    prev = lib().tcx_set_sample_lanes(lanes)
+    try:
+        out, x0 = run_sde(m, g, noise, (B, 1, 64, 64))
+    finally:
+        lib().tcx_set_sample_lanes(prev)
+    check_sampler_outputs(f"sde96_trained_300 ({prec}, {lanes} lanes)", out, x0, g)
     e64 = rel_err(x0, f64)
     print(f"  x0_hat rel err vs the fp64 trajectory {e64:.3e} (fp32 reference vs fp64: "
           f"{rel_err(g['x0_unclamped'], f64):.3e})")
     assert e64 < 1e-4
+    if lanes != 1:
+        prev = lib().tcx_set_sample_lanes(1)
+        try:
+            out1, x01 = run_sde(m, g, noise, (B, 1, 64, 64))
+        finally:
+            lib().tcx_set_sample_lanes(prev)
+        assert np.array_equal(out, out1) and np.array_equal(x0, x01)
+        return
     base = S.step_table
 
     def perturbed_run(row, col, f):

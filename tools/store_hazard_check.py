@@ -42,8 +42,59 @@ def dst_regs(line):
     return vregs(parts[1].split(",")[0].strip())
 
 
+WAIT_STATES = 2  # VALU write of a >8-byte VMEM store's data VGPRs: wait states required on gfx940+ (gfx950)
+ADDR = re.compile(r"//\s*([0-9A-Fa-f]{8,}):")
+OBJ_TGT = re.compile(r"<(_Z[^+>\s]+)\+0x([0-9a-f]+)>")
+FUNC = re.compile(r"^([0-9a-f]+) <(_Z[^>\s]+)>:")
+
+
+def _index(lines):
+    """instruction line -> address (objdump listings) and label / address -> line of the target"""
+    addr_line, label_line, func_addr = {}, {}, {}
+    for i, l in enumerate(lines):
+        m = FUNC.match(l)
+        if m:
+            func_addr[m.group(2)] = int(m.group(1), 16)
+            continue
+        m = re.match(r"^(\.L[A-Za-z0-9_$.]+):", l)
+        if m:
+            label_line[m.group(1)] = i
+            continue
+        m = ADDR.search(l)
+        if m and INSTR.match(l):
+            addr_line[int(m.group(1), 16)] = i
+    return addr_line, label_line, func_addr
+
+
+def _branch_target(l, addr_line, label_line, func_addr):
+    m = OBJ_TGT.search(l)
+    if m and m.group(1) in func_addr:
+        return addr_line.get(func_addr[m.group(1)] + int(m.group(2), 16))
+    parts = l.split(None, 1)
+    if len(parts) > 1:
+        tok = parts[1].split("//")[0].strip().split(",")[0].strip()
+        if tok in label_line:
+            return label_line[tok]
+    return None
+
+
+def _next_instr(lines, j):
+    while j < len(lines):
+        l = lines[j]
+        if l.startswith(".Lfunc_end") or FUNC.match(l):
+            return None
+        if INSTR.match(l) and not l.strip().startswith(";") and not l.strip().startswith("."):
+            return j
+        j += 1
+    return None
+
+
 def scan(path):
+    """every >8-byte VMEM store whose data VGPRs a VALU instruction writes within WAIT_STATES wait
+    states on ANY path: the fall-through, the target of an s_branch and both sides of an s_cbranch
+    (each instruction in between is one wait state, s_nop N is N + 1)"""
     lines = open(path).read().split("\n")
+    addr_line, label_line, func_addr = _index(lines)
     fn = "?"
     found = 0
     for i, l in enumerate(lines):
@@ -54,19 +105,39 @@ def scan(path):
         if not sm:
             continue
         regs = data_regs(l, sm.group(1))
-        # the next real instruction on the fall-through path (labels and comments skipped)
-        j = i + 1
-        while j < len(lines) and (not INSTR.match(lines[j]) or lines[j].strip().startswith(";")):
-            if lines[j].startswith(".Lfunc_end"):
-                break
-            j += 1
-        if j >= len(lines):
-            continue
-        nxt = lines[j]
-        op = INSTR.match(nxt).group(1) if INSTR.match(nxt) else ""
-        if op.startswith("v_") and not op.startswith("v_cmp") and dst_regs(nxt) & regs:
+        work = [(i + 1, 0)]
+        seen = set()
+        hit = None
+        while work and hit is None:
+            j0, ws = work.pop()
+            j = _next_instr(lines, j0)
+            while j is not None and ws < WAIT_STATES:
+                if (j, ws) in seen:
+                    break
+                seen.add((j, ws))
+                nxt = lines[j]
+                op = INSTR.match(nxt).group(1)
+                if op.startswith("v_") and not op.startswith("v_cmp") and dst_regs(nxt) & regs:
+                    hit = (nxt, ws)
+                    break
+                if op == "s_nop":
+                    arg = nxt.split(None, 1)[1].split("//")[0].strip() if len(nxt.split(None, 1)) > 1 else "0"
+                    ws += int(arg, 0) + 1
+                else:
+                    ws += 1
+                if op == "s_endpgm":
+                    break
+                if op.startswith("s_branch") or op.startswith("s_cbranch"):
+                    t = _branch_target(nxt, addr_line, label_line, func_addr)
+                    if t is not None:
+                        work.append((t, ws))
+                    if op.startswith("s_branch"):
+                        break
+                j = _next_instr(lines, j + 1)
+        if hit is not None:
             found += 1
-            print(f"{path}:{i + 1}: {fn[:90]}\n    {l.strip()}\n    {nxt.strip()}   <- overwrites store data, 0 wait states")
+            print(f"{path}:{i + 1}: {fn[:90]}\n    {l.strip()}\n    {hit[0].strip()}   <- overwrites store data, "
+                  f"{hit[1]} wait state(s)")
     return found
 
 

@@ -1377,6 +1377,16 @@ extern "C" size_t tcx_unet_workspace_size(const tcx_unet* net, int Bt, int H, in
 namespace tcx {
 namespace {
 
+// Fault injection for the sampler's error paths (tcx_debug_fail_eval): the k-th U-Net evaluation
+// after arming returns TCX_EINVAL before launching anything (one shot).
+int g_fail_eval = 0;
+int injected_failure() {
+    if (g_fail_eval <= 0) return TCX_OK;
+    if (--g_fail_eval > 0) return TCX_OK;
+    set_error("tcx_unet_eval: injected failure (tcx_debug_fail_eval)");
+    return TCX_EINVAL;
+}
+
 // One (possibly chunked) U-Net evaluation + sampler step.  e_base: element offset of x[0] within
 // the whole sampling batch (the Philox noise counter of element i is e_base + i, so a batch
 // evaluated in pieces — chunks or concurrent lanes — draws the same noise as in one piece).
@@ -1385,6 +1395,7 @@ int unet_eval_impl(const tcx_unet* net, const float* x, float* x2, const float* 
                    const float* scal, const float* z, uint64_t seed, uint64_t step, float* x_inout, float* eps_out,
                    void* ws, size_t ws_bytes, hipStream_t st, size_t e_base, CondTab ct = {}) {
     TCX_TRY(validate(net, B, H, W));
+    TCX_TRY(injected_failure());
     TCX_REQUIRE(x && t && y_cat && y_cont && ws, "tcx_unet_eval: null pointer");
     TCX_REQUIRE(mode >= 0 && mode <= 5, "tcx_unet_eval: bad mode");
     TCX_REQUIRE(mode == 0 || scal, "tcx_unet_eval: sampler modes need the step table row");
@@ -1418,16 +1429,20 @@ int unet_eval_impl(const tcx_unet* net, const float* x, float* x2, const float* 
     return TCX_OK;
 }
 
-// The sampler's conditioning tables (k_cond_maps), one stream-ordered allocation per sampling call:
-// tmaps [n_t][time_ch] for the step table's t values, cmaps [B + 1][cond_ch] (row B: null token).
-// TCX_COND_HOIST=0 keeps the per-evaluation k_cond (A/B).
+// The sampler's conditioning tables (k_cond_maps + k_bias_table), carved from the CALLER's workspace
+// (tcx_sde_workspace_size / tcx_ode_workspace_size size them; the library never allocates): tmaps
+// [n_t][time_ch] for the step table's t values, cmaps [B + 1][cond_ch] (row B: null token), then the
+// per-(step, image) first-conv bias rows [n_t][B + 1][base_ch].  They replace the reference's
+// per-call _make_maps (sde_score_model.py:227-241).  TCX_COND_HOIST=0 keeps the per-evaluation k_cond
+// (A/B; the tables are then left unused).
+size_t cond_tab_floats(const tcx_unet* net, int B, int n_t) {
+    return (size_t)n_t * net->time_ch + (size_t)(B + 1) * net->cond_ch + (size_t)n_t * (B + 1) * net->base_ch;
+}
+size_t cond_tab_bytes(const tcx_unet* net, int B, int n_t) { return align_up(cond_tab_floats(net, B, n_t) * 4, 256); }
+
 struct CondMaps {
     float* buf = nullptr;
-    hipStream_t st = nullptr;
     int time_ch = 0, cond_ch = 0, C0 = 0, B = 0, n_t = 0;
-    ~CondMaps() {
-        if (buf) (void)hipFreeAsync(buf, st);
-    }
     float* tmaps() const { return buf; }
     float* cmaps() const { return buf + (size_t)n_t * time_ch; }
     float* bias() const { return cmaps() + (size_t)(B + 1) * cond_ch; }
@@ -1438,18 +1453,17 @@ struct CondMaps {
     }
 };
 
+// tab: cond_tab_bytes(net, B, n_t) bytes of the caller's workspace, 256-B aligned
 int make_cond_maps(const tcx_unet* net, const float* scal_table, int n_t, const int64_t* y_cat, const float* y_cont,
-                   int B, hipStream_t st, CondMaps& cm) {
+                   int B, hipStream_t st, void* tab, CondMaps& cm) {
     static const bool on = [] {
         const char* e = getenv("TCX_COND_HOIST");
         return !(e && e[0] == '0');
     }();
     if (!on) return TCX_OK;
-    cm.st = st; cm.time_ch = net->time_ch; cm.cond_ch = net->cond_ch; cm.C0 = net->base_ch; cm.B = B; cm.n_t = n_t;
+    cm.time_ch = net->time_ch; cm.cond_ch = net->cond_ch; cm.C0 = net->base_ch; cm.B = B; cm.n_t = n_t;
     const size_t nbias = (size_t)n_t * (B + 1) * net->base_ch;
-    const size_t n = (size_t)n_t * net->time_ch + (size_t)(B + 1) * net->cond_ch + nbias;
-    TCX_REQUIRE(hipMallocAsync(reinterpret_cast<void**>(&cm.buf), n * sizeof(float), st) == hipSuccess,
-                "tcx_sample: conditioning table allocation");
+    cm.buf = reinterpret_cast<float*>(tab);
     CondArgs a{};
     a.time_w1t = net->time_w1t; a.time_b1 = net->time_b1; a.time_w2t = net->time_w2t; a.time_b2 = net->time_b2;
     a.ttm_wt = net->ttm_wt; a.ttm_b = net->ttm_b; a.tcm_wt = net->tcm_wt; a.tcm_b = net->tcm_b;
@@ -1466,6 +1480,35 @@ int make_cond_maps(const tcx_unet* net, const float* scal_table, int n_t, const 
     return check_launch("k_bias_table");
 }
 
+// Joins sampling lanes 1..L-1 back into the caller's stream on EVERY exit of a sampler: on success
+// through join() (errors reported), on an error return from the destructor (best effort), so no lane
+// work is left unordered against the caller's later use or release of the workspace.
+struct LaneJoin {
+    LaneSync* ls = nullptr;
+    int L = 0;
+    hipStream_t st = nullptr;
+    int join() {
+        LaneSync* s = ls;
+        ls = nullptr;
+        if (!s) return TCX_OK;
+        int rc = TCX_OK;
+        for (int l = 1; l < L; ++l) {
+            if (hipEventRecord(s->ev[l], s->s[l]) != hipSuccess || hipStreamWaitEvent(st, s->ev[l], 0) != hipSuccess) {
+                set_error("tcx_sample: joining lane %d to the caller's stream failed", l);
+                rc = TCX_EHIP;
+            }
+        }
+        return rc;
+    }
+    ~LaneJoin() {
+        if (ls) {
+            const std::string keep = tcx_last_error();  // the error being returned stays the reported one
+            (void)join();
+            set_error("%s", keep.c_str());
+        }
+    }
+};
+
 }  // namespace
 }  // namespace tcx
 
@@ -1477,29 +1520,74 @@ extern "C" int tcx_unet_eval(const tcx_unet* net, const float* x, float* x2, con
                           x_inout, eps_out, ws, ws_bytes, (hipStream_t)stream, 0);
 }
 
+// Workspace of the samplers (one caller allocation; the library allocates nothing): the U-Net
+// evaluations' workspace for the (CFG-doubled) rows under the current lane setting, then the
+// conditioning tables of the call's n_steps + 1 step-table rows (and for the PF-ODE the drift d and
+// the Euler point x_e between them).
+namespace tcx {
+namespace {
+size_t sde_ws_parts(const tcx_unet* net, int B, int H, int W, int n_steps, float guidance, size_t* unet_part) {
+    const size_t u = align_up(tcx_unet_workspace_size(net, guidance > 0.f ? 2 * B : B, H, W), 256);
+    if (unet_part) *unet_part = u;
+    return u + cond_tab_bytes(net, B, n_steps + 1) + 256;
+}
+size_t ode_ws_parts(const tcx_unet* net, int B, int H, int W, int n_steps, float guidance, size_t* unet_part,
+                    size_t* img_part) {
+    const size_t u = align_up(tcx_unet_workspace_size(net, guidance > 0.f ? 2 * B : B, H, W), 256);
+    const size_t im = align_up((size_t)B * H * W * sizeof(float), 256);
+    if (unet_part) *unet_part = u;
+    if (img_part) *img_part = im;
+    return u + 2 * im + cond_tab_bytes(net, B, n_steps + 1) + 256;
+}
+}  // namespace
+}  // namespace tcx
+
+extern "C" size_t tcx_sde_workspace_size(const tcx_unet* net, int B, int H, int W, int n_steps, float guidance) {
+    if (!net || B <= 0 || n_steps < 0) return 0;
+    return sde_ws_parts(net, B, H, W, n_steps, guidance, nullptr);
+}
+
+extern "C" size_t tcx_ode_workspace_size(const tcx_unet* net, int B, int H, int W, int n_steps, float guidance) {
+    if (!net || B <= 0 || n_steps < 0) return 0;
+    return ode_ws_parts(net, B, H, W, n_steps, guidance, nullptr, nullptr);
+}
+
+extern "C" int tcx_debug_fail_eval(int k) {
+    g_fail_eval = k < 0 ? 0 : k;
+    return TCX_OK;
+}
+
 extern "C" int tcx_sde_sample_shard(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
                                     int H, int W, int n_steps, float guidance, const float* scal_table,
                                     const float* noise, uint64_t seed, int flags, uint64_t e_base, void* ws,
                                     size_t ws_bytes, void* stream) {
-    TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_sde_sample: bad args");
+    TCX_REQUIRE(x && scal_table && n_steps >= 0 && ws, "tcx_sde_sample: bad args");
     TCX_REQUIRE((flags & ~TCX_SAMPLE_X0_HAT) == 0, "tcx_sde_sample: unknown flags %d", flags);
     TCX_TRY(validate(net, B, H, W));
     const int fmode = (flags & TCX_SAMPLE_X0_HAT) ? 5 : 2;
     const size_t img = (size_t)B * H * W;
+    size_t ubytes = 0;
+    const size_t need = sde_ws_parts(net, B, H, W, n_steps, guidance, &ubytes);
+    if (ws_bytes < need) {
+        set_error("tcx_sde_sample: workspace too small (%zu < %zu, tcx_sde_workspace_size)", ws_bytes, need);
+        return TCX_EWS;
+    }
+    char* wbase = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
+    hipStream_t st = (hipStream_t)stream;
     CondMaps cmap;
-    TCX_TRY(make_cond_maps(net, scal_table, n_steps + 1, y_cat, y_cont, B, (hipStream_t)stream, cmap));
+    TCX_TRY(make_cond_maps(net, scal_table, n_steps + 1, y_cat, y_cont, B, st, wbase + ubytes, cmap));
     const int L = std::min(lanes_setting(), B);
     const int rows = guidance > 0.f ? 2 * B : B;
     LaneSync* ls = L > 1 ? lane_sync() : nullptr;
-    if (ls && ws_bytes >= (size_t)L * lane_ws_bytes(net, rows, H, W, L) + 256) {
+    if (ls && ubytes >= (size_t)L * lane_ws_bytes(net, rows, H, W, L)) {
         const size_t HW = (size_t)H * W;
         const size_t lws = lane_ws_bytes(net, rows, H, W, L);
-        char* wbase = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
-        hipStream_t st = (hipStream_t)stream;
         auto lst = [&](int l) { return l == 0 ? st : ls->s[l]; };
         TCX_REQUIRE(hipEventRecord(ls->ev[4], st) == hipSuccess, "tcx_sde_sample: event record");
+        LaneJoin lj;
         for (int l = 1; l < L; ++l)
             TCX_REQUIRE(hipStreamWaitEvent(ls->s[l], ls->ev[4], 0) == hipSuccess, "tcx_sde_sample: stream wait");
+        lj.ls = ls; lj.L = L; lj.st = st;
         for (int i = 0; i <= n_steps; ++i) {
             const float* row = scal_table + (size_t)i * TCX_SCAL;
             for (int l = 0; l < L; ++l) {
@@ -1517,23 +1605,18 @@ extern "C" int tcx_sde_sample_shard(const tcx_unet* net, float* x, const int64_t
                 }
             }
         }
-        for (int l = 1; l < L; ++l) {
-            TCX_REQUIRE(hipEventRecord(ls->ev[l], ls->s[l]) == hipSuccess, "tcx_sde_sample: event record");
-            TCX_REQUIRE(hipStreamWaitEvent(st, ls->ev[l], 0) == hipSuccess, "tcx_sde_sample: stream wait");
-        }
-        return TCX_OK;
+        return lj.join();
     }
-    hipStream_t st = (hipStream_t)stream;
     for (int i = 0; i < n_steps; ++i) {
         const float* row = scal_table + (size_t)i * TCX_SCAL;
         TCX_TRY(unet_eval_impl(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, 1, row,
-                               noise ? noise + (size_t)i * img : nullptr, seed, (uint64_t)i, x, nullptr, ws, ws_bytes,
+                               noise ? noise + (size_t)i * img : nullptr, seed, (uint64_t)i, x, nullptr, wbase, ubytes,
                                st, e_base, cmap.at(i, 0)));
     }
     // final projection -> image written over x
     const float* row = scal_table + (size_t)n_steps * TCX_SCAL;
     return unet_eval_impl(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, fmode, row, nullptr, seed, 0,
-                          nullptr, x, ws, ws_bytes, st, e_base, cmap.at(n_steps, 0));
+                          nullptr, x, wbase, ubytes, st, e_base, cmap.at(n_steps, 0));
 }
 
 extern "C" int tcx_sde_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
@@ -1553,32 +1636,36 @@ extern "C" int tcx_sde_sample(const tcx_unet* net, float* x, const int64_t* y_ca
 extern "C" int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B,
                                  int H, int W, int n_steps, float guidance, const float* scal_table, int flags, void* ws,
                                  size_t ws_bytes, void* stream) {
-    TCX_REQUIRE(x && scal_table && n_steps >= 0, "tcx_ode_sample: bad args");
+    TCX_REQUIRE(x && scal_table && n_steps >= 0 && ws, "tcx_ode_sample: bad args");
     TCX_REQUIRE((flags & ~TCX_SAMPLE_X0_HAT) == 0, "tcx_ode_sample: unknown flags %d", flags);
     TCX_TRY(validate(net, B, H, W));
     const int fmode = (flags & TCX_SAMPLE_X0_HAT) ? 5 : 2;
+    size_t ubytes = 0, ibytes = 0;
+    const size_t need = ode_ws_parts(net, B, H, W, n_steps, guidance, &ubytes, &ibytes);
+    if (ws_bytes < need) {
+        set_error("tcx_ode_sample: workspace too small (%zu < %zu, tcx_ode_workspace_size)", ws_bytes, need);
+        return TCX_EWS;
+    }
+    char* wbase = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
+    hipStream_t st = (hipStream_t)stream;
+    // [U-Net workspace][d][x_e][conditioning tables]
+    float* d = reinterpret_cast<float*>(wbase + ubytes);
+    float* xe = reinterpret_cast<float*>(wbase + ubytes + ibytes);
     CondMaps cmap;  // stage 2 of step i evaluates at t_{i+1}: table row i + 1
-    TCX_TRY(make_cond_maps(net, scal_table, n_steps + 1, y_cat, y_cont, B, (hipStream_t)stream, cmap));
-    // Scratch for d and x_e lives at the end of the workspace.
-    const size_t img = (size_t)B * H * W;
-    const size_t need = tcx_unet_workspace_size(net, guidance > 0.f ? 2 * B : B, H, W);
-    TCX_REQUIRE(ws_bytes >= need + 2 * img * sizeof(float) + 512, "tcx_ode_sample: workspace too small");
-    char* tail = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>((char*)ws + need), 256));
-    float* d = reinterpret_cast<float*>(tail);
-    float* xe = d + align_up(img, 64);
+    TCX_TRY(make_cond_maps(net, scal_table, n_steps + 1, y_cat, y_cont, B, st, wbase + ubytes + 2 * ibytes, cmap));
     // concurrent lanes (tcx_set_sample_lanes): image groups on their own streams, d / x_e sliced
     const int L = std::min(lanes_setting(), B);
     const int rows = guidance > 0.f ? 2 * B : B;
     LaneSync* ls = L > 1 ? lane_sync() : nullptr;
-    if (ls && need >= (size_t)L * lane_ws_bytes(net, rows, H, W, L) + 256) {
+    if (ls && ubytes >= (size_t)L * lane_ws_bytes(net, rows, H, W, L)) {
         const size_t HW = (size_t)H * W;
         const size_t lws = lane_ws_bytes(net, rows, H, W, L);
-        char* wbase = reinterpret_cast<char*>(align_up(reinterpret_cast<uintptr_t>(ws), 256));
-        hipStream_t st = (hipStream_t)stream;
         auto lst = [&](int l) { return l == 0 ? st : ls->s[l]; };
         TCX_REQUIRE(hipEventRecord(ls->ev[4], st) == hipSuccess, "tcx_ode_sample: event record");
+        LaneJoin lj;
         for (int l = 1; l < L; ++l)
             TCX_REQUIRE(hipStreamWaitEvent(ls->s[l], ls->ev[4], 0) == hipSuccess, "tcx_ode_sample: stream wait");
+        lj.ls = ls; lj.L = L; lj.st = st;
         for (int i = 0; i <= n_steps; ++i) {
             const float* row = scal_table + (size_t)i * TCX_SCAL;
             for (int l = 0; l < L; ++l) {
@@ -1598,24 +1685,19 @@ extern "C" int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y
                 }
             }
         }
-        for (int l = 1; l < L; ++l) {
-            TCX_REQUIRE(hipEventRecord(ls->ev[l], ls->s[l]) == hipSuccess, "tcx_ode_sample: event record");
-            TCX_REQUIRE(hipStreamWaitEvent(st, ls->ev[l], 0) == hipSuccess, "tcx_ode_sample: stream wait");
-        }
-        return TCX_OK;
+        return lj.join();
     }
-    hipStream_t st = (hipStream_t)stream;
     for (int i = 0; i < n_steps; ++i) {
         const float* row = scal_table + (size_t)i * TCX_SCAL;
-        TCX_TRY(unet_eval_impl(net, x, xe, row, 0, y_cat, y_cont, B, H, W, guidance, 3, row, nullptr, 0, 0, x, d, ws,
-                               need, st, 0, cmap.at(i, 0)));
+        TCX_TRY(unet_eval_impl(net, x, xe, row, 0, y_cat, y_cont, B, H, W, guidance, 3, row, nullptr, 0, 0, x, d, wbase,
+                               ubytes, st, 0, cmap.at(i, 0)));
         const float* row_n = row + TCX_SCAL;  // t_{i+1}
         TCX_TRY(unet_eval_impl(net, xe, nullptr, row_n, 0, y_cat, y_cont, B, H, W, guidance, 4, row, nullptr, 0, 0, x,
-                               d, ws, need, st, 0, cmap.at(i + 1, 0)));
+                               d, wbase, ubytes, st, 0, cmap.at(i + 1, 0)));
     }
     const float* row = scal_table + (size_t)n_steps * TCX_SCAL;
     return unet_eval_impl(net, x, nullptr, row, 0, y_cat, y_cont, B, H, W, guidance, fmode, row, nullptr, 0, 0, nullptr,
-                          x, ws, need, st, 0, cmap.at(n_steps, 0));
+                          x, wbase, ubytes, st, 0, cmap.at(n_steps, 0));
 }
 
 extern "C" int tcx_ode_sample(const tcx_unet* net, float* x, const int64_t* y_cat, const float* y_cont, int B, int H,

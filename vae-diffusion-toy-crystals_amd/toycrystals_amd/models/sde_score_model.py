@@ -273,8 +273,11 @@ class _UNetPack:
             launch()
         self.net.precision = 0
 
-    def workspace(self, Bt: int, H: int, W: int, extra: int = 0) -> Tuple[torch.Tensor, int]:
-        need = int(lib().tcx_unet_workspace_size(ctypes.byref(self.net), Bt, H, W)) + extra
+    def workspace(self, Bt: int, H: int, W: int, extra: int = 0, need: Optional[int] = None) -> Tuple[torch.Tensor, int]:
+        """The caller-owned workspace of a libtcx call (grown, never shrunk): `need` bytes when the
+        call has its own size query (tcx_sde/ode_workspace_size), else one U-Net evaluation's."""
+        if need is None:
+            need = int(lib().tcx_unet_workspace_size(ctypes.byref(self.net), Bt, H, W)) + extra
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self.ws, self.ws.numel()
@@ -592,7 +595,8 @@ def sample_reverse_sde_euler_maruyama(model: CondUNetTiny, sde: VPSDE, y_cat: to
             raise ValueError(f"noise must be [n_steps+1, B, 1, H, W], got {tuple(noise.shape)}")
         zs = noise[1:]
     g = float(guidance_scale) if guidance_scale > 0.0 else 0.0
-    ws, nbytes = pk.workspace(2 * B if g > 0 else B, H, W)
+    ws, nbytes = pk.workspace(2 * B if g > 0 else B, H, W,
+                              need=int(L.tcx_sde_workspace_size(ctypes.byref(pk.net), B, H, W, int(n_steps), g)))
     flags = TCX_SAMPLE_X0_HAT if return_x0_hat else 0
 
     def launch():
@@ -627,8 +631,8 @@ def sample_probability_flow_ode(model: CondUNetTiny, sde: VPSDE, y_cat: torch.Te
     if x_init is None and seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
     g = float(guidance_scale) if guidance_scale > 0.0 else 0.0
-    img_bytes = B * H * W * 4
-    ws, nbytes = pk.workspace(2 * B if g > 0 else B, H, W, extra=2 * img_bytes + 1024)
+    ws, nbytes = pk.workspace(2 * B if g > 0 else B, H, W,
+                              need=int(L.tcx_ode_workspace_size(ctypes.byref(pk.net), B, H, W, int(n_steps), g)))
 
     def launch():
         if x_init is not None:
