@@ -185,12 +185,15 @@ def rand_tabs(B, C, seed):
     (2, 192, 192, 32, True, False),  # down2_1 (32^2)
     (2, 96, 96, 32, True, False),    # up2_1
     (2, 192, 192, 16, True, False),  # mid_1 (16^2 rows)
+    (2, 32, 96, 64, True, False),    # one chunk pair (the 16x16x32 form's untransformed last even chunk)
+    (1, 384, 96, 32, True, False),   # the widest source the prologue tables hold
     (1, 96, 96, 128, True, False),   # config 5's 128^2 rows
     (2, 64, 96, 32, False, False),   # zero padding: the padded ring is 0 AFTER the transform
     (2, 96, 96, 64, True, True),     # concat: source 1 h2, source 2 fp32 + tables
 ])
 def test_conv_h2_gn_silu_prologue_vs_oracle(B, Ci, Co, H, circ, two):
-    """k_conv3g's GroupNorm+SiLU prologue: conv(silu(x*sc + sh)) against the fp64 oracle of the
+    """The GroupNorm+SiLU prologue (k_conv3m's 16x16x32 form at 16/32/64-px rows, k_conv3g at 128,
+    k_conv3l for the mixed concat): conv(silu(x*sc + sh)) against the fp64 oracle of the
     same (SiLU in fp64), at the fp32 gate and within 2x the fp32-MFMA conv of the pre-normalised
     input (the fp32 path applies the tables in a separate pass)."""
     x = rng.standard_normal((B, Ci, H, H)) * 2.0

@@ -827,11 +827,14 @@ bool conv3l_enabled() {
     return on;
 }
 
+bool conv3m_takes(const ConvParams& p);
+
 // called by launch_conv3g once conv3g_applies() holds (fragment-ordered weights, Cin % 32 == 0,
 // Cin <= 384, cout_pad % 96 == 0, whole-row tiles)
 bool conv3l_takes(const ConvParams& p) {
     if (!conv3l_enabled() || p.bf || !p.circular || p.M % L_TP != 0 || p.HoWo % L_TP != 0) return false;
     if (p.W == 32 || p.W == 64) return true;
+    if (conv3m_takes(p)) return true;  // 16-px rows: the 16x16x32 forms, incl. the GroupNorm prologue
     // 16-px rows: the LDS-DMA kernel for h2 sources (mid.net.0: 2 % faster than k_conv3g); its
     // GroupNorm prologue form is 9 % slower than k_conv3g's there (profiles/r02_zt_*), so that stays
     return p.W == 16 && p.sc1 == nullptr && !(p.C2 > 0 && p.sc2 != nullptr);

@@ -54,8 +54,17 @@ constexpr int M_PAIR = 12288;          // bytes of B fragments per tap pair (2 t
 constexpr int M_BN = 96;               // output channels per tile
 
 __host__ __device__ constexpr int m_npx(int W) { return (M_TP / W + 2) * (W + 2); }
-template <int W>
-constexpr size_t conv3m_lds_bytes() { return (size_t)2 * ((m_npx(W) + 15) / 16) * 16 * 64 + 2 * (size_t)M_PAIR; }
+// PRO 1: + the image's GroupNorm tables [scale | shift][Cin <= 384] after the ring
+template <int W, int PRO = 0>
+constexpr size_t conv3m_lds_bytes() {
+    return (size_t)2 * ((m_npx(W) + 15) / 16) * 16 * 64 + 2 * (size_t)M_PAIR + (PRO ? 2 * 384 * sizeof(float) : 0);
+}
+// PRO 1 transform units per thread: the 2 NPX 8-channel halo units of a chunk over 256 threads
+__host__ __device__ constexpr int m_tu(int W) { return (2 * m_npx(W) + 255) / 256; }
+// PRO 1 transform lane map (found by search over the ds_read_b128 16-lane groups and the ds_write_b128
+// 8-lane groups at 16/32/64-px rows, tools/emu/conv3mg_lanemap.py: <= 1.29 / 1.18 average ways, 2
+// worst): lane l takes slot 32 wv + 128 i + 2 perm[l >> 2] + (l & 1), 8-channel group (l >> 1) & 1
+constexpr unsigned long long M_TPERM = 0x46dfb9a83e52701cull;  // nibble h = perm[h]
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -70,12 +79,45 @@ __device__ __forceinline__ void m_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int
 __device__ unsigned long long* g_m_stamps = nullptr;
 __device__ int g_m_stamps_n = 0;
 
+// PRO 1: task of MFMA gap G (0..35) of a half-pair that carries a transform unit: 0 load (two
+// ds_read_b128 + the scale / shift of values 0-1), 1..8 value code - 1 (GroupNorm affine + SiLU),
+// 9..12 the h2 split of channel pair code - 9, 13 the write-back (two ds_write_b128) and the range
+// flag, 14..16 the scale / shift of value pair code - 13 (two ds_read_b64, read two gaps before their
+// first value); -1 none.  The load leads the first value by 3 MFMAs (its LDS latency).
+constexpr int m_tcode(int G) {
+    return G == 0 ? 0 : G == 3 ? 1 : G == 4 ? 14 : G == 5 ? 2 : G == 7 ? 9 : G == 9 ? 3 : G == 10 ? 15 : G == 11 ? 4
+         : G == 13 ? 10 : G == 15 ? 5 : G == 16 ? 16 : G == 17 ? 6 : G == 19 ? 11 : G == 21 ? 7 : G == 23 ? 8
+         : G == 25 ? 12 : G == 27 ? 13 : -1;
+}
+template <typename F, int... Is>
+__device__ __forceinline__ void m_static_for(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+
+// A/B build variants of the prologue form (tools/build_variant.sh; 0 = the product)
+#ifndef TCX_M_VAR
+#define TCX_M_VAR 0
+#endif
+#ifndef TCX_M_AGPR
+#define TCX_M_AGPR 1
+#endif
+
 constexpr int M_WAIT_VM0 = 0x0F70;    // s_waitcnt vmcnt(0)
 constexpr int M_WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
 
 // FAST: no activation and an fp32 output (every U-Net conv k_conv3m serves: a GroupNorm follows), so
-// the epilogue is straight-line code; otherwise the activation / h2 output are run-time branches
-template <int W, bool FAST>
+// the epilogue is straight-line code; otherwise the activation / h2 output are run-time branches.
+// PRO 1: the source is the previous conv's fp32 output and the halo is staged as
+// h2(silu(x * scale[b][c] + shift[b][c])) — the GroupNorm + SiLU of the _ConvBlock feeding this conv
+// (sde_score_model.py:103-107), never written to memory.  The raw fp32 chunk (16 channels = 64 B per
+// pixel, the size of its h2 slot) is DMA'd into the slot image as for an h2 source, in one shot at
+// the mid of pair 4 (even chunk, buffer 0) / 8 (odd, buffer 1), waited for at the mid of pair 6 / 1,
+// and rewritten IN PLACE by all four waves during the next four half-pairs (6.H2, 7.H1, 7.H2, 8.H1 /
+// 1.H2, 2.H1, 2.H2, 3.H1): one 8-channel unit per thread and half-pair, its two ds_read_b128, eight
+// values, four channel-pair splits and two ds_write_b128 spread one task per MFMA gap over the half's
+// 36 MFMAs.  It is published by the same barriers as an h2 chunk (mids 8 / 3), so the MFMA pipeline,
+// the weight ring and the epilogue are k_conv3m's.
+template <int W, bool FAST, int PRO>
 __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     constexpr int W2 = W + 2;
     constexpr int NPX = m_npx(W);
@@ -83,7 +125,11 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     constexpr int NIH = (NI + 1) / 2;    // per halo wave (wave 2: even i, wave 3: odd i)
     constexpr int HB = NI * 16 * 64;
     constexpr int RING = 2 * HB;
+    constexpr int TAB = RING + 2 * M_PAIR;  // PRO 1: [scale | shift][Cin]
+    constexpr int TU = m_tu(W);             // PRO 1: transform units per thread and chunk (3 or 4)
     static_assert(W == 16 || W == 32 || W == 64, "k_conv3m: rows of 16, 32 or 64 pixels");
+    static_assert(NI * 16 >= NPX + 4, "k_conv3m: idle transform lanes use 4 padding slots");
+    static_assert(TU <= 4, "k_conv3m: at most 4 transform half-pairs per chunk");
     auto sw = [](int col) { return (col >> 2) & 1; };
     extern __shared__ __attribute__((aligned(16))) float sm[];
     char* const smc = reinterpret_cast<char*>(sm);
@@ -91,7 +137,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     int lz;
     asm volatile("s_mov_b32 %0, 0" : "=s"(lz));
     char* const smd = smc + lz;
-    mfma_agpr_form();  // accumulators in AGPRs (common.hpp: the SrcC-reuse hazard this kernel hit under the lanes)
+    if constexpr (PRO == 0 && TCX_M_AGPR) mfma_agpr_form();  // accumulators in AGPRs (common.hpp)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -119,12 +165,13 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     const __amdgpu_buffer_rsrc_t rw = mk_rsrc(reinterpret_cast<const float*>(p.wf), p.bytesw);
 
     // ---- halo DMA (waves 2, 3): lane l of instruction i fills slot 16 i + l / 4, physical piece l % 4,
-    // so it reads logical piece (l % 4) ^ sw(col) of that pixel (the swizzle rides on the source address)
+    // so it reads logical piece (l % 4) ^ sw(col) of that pixel (the swizzle rides on the source address).
+    // An h2 record and an fp32 chunk of 16 channels are both 64 B: the same offsets serve PRO 0 and 1
     const int hw = wv & 1;
     const int rowb = p.C1 * 4;
     const int img0 = bs * H;
     const int ls = lane >> 2;
-    auto halo_voff = [&](int i) {
+    auto halo_voff = [&](int i) __attribute__((always_inline)) {
         const int hr0 = (16 * i) / W2;
         const int th = W2 * (hr0 + 1) - 16 * i;
         const int y0 = wrap_idx(r0 + hr0 - 1, H), y1 = wrap_idx(r0 + hr0, H);
@@ -139,7 +186,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         return yo + x * rowb + 16 * ((lane & 3) ^ sw(hcs));
     };
     // third `th` (0..2) of chunk j's halo into buffer buf
-    auto halo_third = [&](int j, int buf, int th) {
+    auto halo_third = [&](int j, int buf, int th) __attribute__((always_inline)) {
         const int ci0 = j * M_KC;
         const bool s1 = ci0 < p.C1;
         const int cc = (s1 ? ci0 : ci0 - p.C1) * 4;
@@ -152,8 +199,12 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
             if (i < NI) m_dma16(rs, smd + buf * HB + i * 1024, halo_voff(i), cc);
         }
     };
+    auto halo_all = [&](int j, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t3 = 0; t3 < 3; ++t3) halo_third(j, buf, t3);
+    };
     // weight pair k (12 KB) -> ring slot k & 1; wave w (0, 1) moves KB [6 w, 6 w + 6)
-    auto pair_issue = [&](int k) {
+    auto pair_issue = [&](int k) __attribute__((always_inline)) {
         const int base = (nblk * 2 * npair + 2 * k) * 6144 + wv * 6144;
         char* const d = smd + RING + (k & 1) * M_PAIR + wv * 6144;
 #pragma unroll
@@ -189,72 +240,215 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
 #pragma unroll
         for (int n = 0; n < 6; ++n) acc[rb][n] = (f32x4){};
     h8 a_h[4], a_l[4], b_h[3], b_l[3];
-    auto rd_a = [&](int q, int rb) {
+    auto rd_a = [&](int q, int rb) __attribute__((always_inline)) {
         a_h[rb] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + aq[q] + rbo(rb)));
         a_l[rb] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(smc + (aq[q] ^ 16) + rbo(rb)));
     };
     // B fragments (hi, lo) of pair k, column block nb, into register slot i
-    auto rd_b = [&](int i, int k, int nb) {
+    auto rd_b = [&](int i, int k, int nb) __attribute__((always_inline)) {
         const char* B = smc + bq + (k & 1) * M_PAIR + (nb >> 1) * 2048 + (nb & 1) * 256;
         b_h[i] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(B));
         b_l[i] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(B + 1024));
     };
-    // the 3 MFMAs (hi.lo, lo.hi, hi.hi) of row block rb and column block nb with B slot i
-    auto mf3 = [&](int rb, int nb, int i) {
-        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h[rb], b_l[i], acc[rb][nb], 0, 0, 0);
-        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_l[rb], b_h[i], acc[rb][nb], 0, 0, 0);
-        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h[rb], b_h[i], acc[rb][nb], 0, 0, 0);
+    // MFMA number k (0..11) of column block nb with B slot i: product k >> 2 (hi.lo, lo.hi, hi.hi) of
+    // row block k & 3 (4 independent accumulators between the dependent products of one block)
+    auto mfk = [&](int k, int nb, int i) __attribute__((always_inline)) {
+        const int rb = k & 3, pr = k >> 2;
+        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pr == 1 ? a_l[rb] : a_h[rb], pr == 0 ? b_l[i] : b_h[i],
+                                                             acc[rb][nb], 0, 0, 0);
     };
-    // the 12 MFMAs of column block nb over the 4 row blocks (4 independent accumulators between the
-    // dependent products of one block: rb-inner)
-    auto mf_col = [&](int nb, int i) {
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-            acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h[rb], b_l[i], acc[rb][nb], 0, 0, 0);
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-            acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_l[rb], b_h[i], acc[rb][nb], 0, 0, 0);
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-            acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h[rb], b_h[i], acc[rb][nb], 0, 0, 0);
+
+    // ---- PRO 1 transform (in-place fp32 -> h2 of the GroupNorm + SiLU value).  Registers are the
+    // limit (128 VGPRs beside the 96 accumulator AGPRs): the unit's LDS offset is recomputed per unit
+    // and its scale / shift pairs are read from the LDS tables two values ahead of use
+    const int t_so = 2 * (int)((M_TPERM >> (4 * (lane >> 2))) & 15ull) + (lane & 1);
+    const int t_g = (lane >> 1) & 1;
+    const float* const Tw = reinterpret_cast<const float*>(smc + TAB);
+    int tdst = 0;        // LDS byte offset (buffer 0) of the current unit's first piece
+    bool tlive = false;  // the unit is a real halo slot (idle lanes rewrite a padding slot)
+    int tj = 0;          // chunk being transformed
+    float ux[8];
+    f32x2 tsc[2], tsh[2];  // scale / shift of two values, double-buffered by value pair
+    unsigned uh[4], ul[4];
+    float um = 0.f;
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    auto t_addr = [&](int i) __attribute__((always_inline)) {
+        const int sl0 = 128 * i + 32 * wv + t_so;
+        tlive = sl0 < NPX;
+        const int sl = tlive ? sl0 : NPX + (lane & 3);
+        tdst = sl * 64 + 16 * ((2 * t_g) ^ sw(sl % W2));
+    };
+    auto t_tab = [&](int q) __attribute__((always_inline)) {  // channels 2 q, 2 q + 1 of the lane's group
+        const float* t = Tw + tj * M_KC + 8 * t_g + 2 * q;
+        tsc[q & 1] = *reinterpret_cast<const f32x2*>(t);
+        tsh[q & 1] = *reinterpret_cast<const f32x2*>(t + p.C1);
+    };
+    auto t_load = [&](int i, int buf) __attribute__((always_inline)) {
+        t_addr(i);
+        const float4 x0 = *reinterpret_cast<const float4*>(smc + buf * HB + tdst);
+        const float4 x1 = *reinterpret_cast<const float4*>(smc + buf * HB + (tdst ^ 16));
+        ux[0] = x0.x; ux[1] = x0.y; ux[2] = x0.z; ux[3] = x0.w; ux[4] = x1.x; ux[5] = x1.y; ux[6] = x1.z; ux[7] = x1.w;
+        um = 0.f;
+        t_tab(0);
+    };
+    auto t_val = [&](int k) __attribute__((always_inline)) {
+        const int q = k >> 1, e = k & 1;
+        ux[k] = silu_hw(fmaf(ux[k], tsc[q & 1][e], tsh[q & 1][e]));
+    };
+    auto t_pair = [&](int q) __attribute__((always_inline)) {
+        const f32x2 v = {ux[2 * q], ux[2 * q + 1]};
+        const f16x2 h = __builtin_convertvector(v, f16x2);
+        const f32x2 r = v - __builtin_convertvector(h, f32x2);
+        const f16x2 l = __builtin_convertvector(r, f16x2);
+        uh[q] = __builtin_bit_cast(unsigned, h);
+        ul[q] = __builtin_bit_cast(unsigned, l);
+        um = fmaxf(um, fmaxf(fabsf(v[0]), fabsf(v[1])));
+    };
+    auto t_store = [&](int buf, bool live) __attribute__((always_inline)) {
+        *reinterpret_cast<uint4*>(smc + buf * HB + tdst) = make_uint4(uh[0], uh[1], uh[2], uh[3]);
+        *reinterpret_cast<uint4*>(smc + buf * HB + (tdst ^ 16)) = make_uint4(ul[0], ul[1], ul[2], ul[3]);
+        h2_flag(p.ovf, !(um < kH2Max) && live && tlive);
+    };
+    // one task (m_tcode) of a transform unit
+    auto t_task = [&](auto Cc, int U, int buf, bool live) __attribute__((always_inline)) {
+        constexpr int code = decltype(Cc)::value;
+        if constexpr (code == 0) t_load(U, buf);
+        else if constexpr (code <= 8) t_val(code - 1);
+        else if constexpr (code <= 12) t_pair(code - 9);
+        else if constexpr (code == 13) t_store(buf, live);
+        else t_tab(code - 13);  // 14..16: tables of value pair 1..3
     };
 
     // ---- prologue: pairs 0, 1 and halo chunk 0 in LDS; the first third of chunk 1 issued
+    // (PRO 1: chunk 0 raw + the image's tables, then chunk 1 raw in full while chunk 0 is transformed)
     if (wv < 2) {
         pair_issue(0);
         pair_issue(1);
     } else {
-#pragma unroll
-        for (int t3 = 0; t3 < 3; ++t3) halo_third(0, 0, t3);
+        halo_all(0, 0);
+    }
+    if constexpr (PRO == 1) {
+        float* const Twr = reinterpret_cast<float*>(smc + TAB);
+        for (int c = tid; c < p.C1; c += 64 * M_NW) {
+            Twr[c] = p.sc1[(size_t)b * p.C1 + c];
+            Twr[p.C1 + c] = p.sh1[(size_t)b * p.C1 + c];
+        }
     }
     __builtin_amdgcn_s_waitcnt(M_WAIT_VM0);
     __builtin_amdgcn_s_waitcnt(M_WAIT_LGKM0);
     __builtin_amdgcn_s_barrier();
     if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
-    if (wv >= 2 && cpt > 1) halo_third(1, 1, 0);
+    if constexpr (PRO == 1) {
+        if (wv >= 2) halo_all(1, 1);  // cpt >= 2
+        tj = 0;
+#pragma unroll
+        for (int i = 0; i < TU; ++i) {
+            t_load(i, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q < 3) t_tab(q + 1);
+                t_val(2 * q);
+                t_val(2 * q + 1);
+                t_pair(q);
+            }
+            t_store(0, true);
+        }
+        __builtin_amdgcn_s_waitcnt(M_WAIT_LGKM0);
+        __builtin_amdgcn_s_barrier();
+    } else {
+        if (wv >= 2 && cpt > 1) halo_third(1, 1, 0);
+    }
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) rd_a(0, rb);
 #pragma unroll
     for (int i = 0; i < 3; ++i) rd_b(i, 0, i);
 
-    auto pair_iter = [&](int pp, auto Q) {
+    // the 12 MFMAs of column block nb (B slot i) as gaps G0 .. G0 + 11 of a half-pair, each followed
+    // by its transform task when the half carries unit U (U < 0: none) of buffer BUF, chunk live `tl`
+    auto mf_col = [&](int nb, int i, auto G0c, auto Uc, auto BUFc, bool tl) __attribute__((always_inline)) {
+        constexpr int G0 = decltype(G0c)::value, U = decltype(Uc)::value, BUF = decltype(BUFc)::value;
+        m_static_for([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            mfk(k, nb, i);
+            if constexpr (U >= 0 && TCX_M_VAR != 9) {
+                constexpr int code = m_tcode(G0 + k);
+                if constexpr (code >= 0) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    t_task(std::integral_constant<int, code>{}, U, BUF, tl);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }, std::make_integer_sequence<int, 12>{});
+    };
+    // the 3 MFMAs of row block rb, column block nb (B slot i) as gaps G0 .. G0 + 2
+    auto mf3 = [&](int rb, int nb, int i, auto G0c, auto Uc, auto BUFc, bool tl) __attribute__((always_inline)) {
+        constexpr int G0 = decltype(G0c)::value, U = decltype(Uc)::value, BUF = decltype(BUFc)::value;
+        m_static_for([&](auto K) {
+            constexpr int pr = decltype(K)::value;
+            mfk(4 * pr + rb, nb, i);
+            if constexpr (U >= 0 && TCX_M_VAR != 9) {
+                constexpr int code = m_tcode(G0 + pr);
+                if constexpr (code >= 0) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    t_task(std::integral_constant<int, code>{}, U, BUF, tl);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }, std::make_integer_sequence<int, 3>{});
+    };
+
+    auto pair_iter = [&](int pp, auto Q) __attribute__((always_inline)) {
         constexpr int q = decltype(Q)::value;
         constexpr int qn = q == 8 ? 0 : q + 1;
         const int k = 9 * pp + q;
+        // PRO 1 transform units of this pair's two halves: odd chunk 2 pp + 1 (buffer 1) in 1.H2, 2.H1,
+        // 2.H2, 3.H1; even chunk 2 pp + 2 (buffer 0) in 6.H2, 7.H1, 7.H2, 8.H1 (the first TU of them)
+        constexpr int U1 = PRO != 1 ? -1 : (q == 2 ? 1 : q == 3 ? 3 : q == 7 ? 1 : q == 8 ? 3 : -1);
+        constexpr int U2 = PRO != 1 ? -1 : (q == 1 ? 0 : q == 2 ? 2 : q == 6 ? 0 : q == 7 ? 2 : -1);
+        constexpr int UH1 = U1 < TU ? U1 : -1, UH2 = U2 < TU ? U2 : -1;
+        constexpr int BUF = q <= 4 ? 1 : 0;
+        const bool tl = BUF == 1 ? true : 2 * pp + 2 < cpt;  // the even chunk after the last is not staged
+        using Uh1 = std::integral_constant<int, UH1>;
+        using Uh2 = std::integral_constant<int, UH2>;
+        using Bc = std::integral_constant<int, BUF>;
+        if constexpr (UH1 >= 0 || UH2 >= 0) tj = BUF == 1 ? 2 * pp + 1 : 2 * pp + 2;  // chunk being transformed
         // H1: column blocks 0-2 (B slots 0-2); each slot, once its 12 MFMAs have issued, takes block 3 + i
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            mf_col(i, i);
-            __builtin_amdgcn_sched_barrier(0);
-            rd_b(i, k, 3 + i);
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        mf_col(0, 0, std::integral_constant<int, 0>{}, Uh1{}, Bc{}, tl);
+        __builtin_amdgcn_sched_barrier(0);
+        rd_b(0, k, 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mf_col(1, 1, std::integral_constant<int, 12>{}, Uh1{}, Bc{}, tl);
+        __builtin_amdgcn_sched_barrier(0);
+        rd_b(1, k, 4);
+        __builtin_amdgcn_sched_barrier(0);
+        mf_col(2, 2, std::integral_constant<int, 24>{}, Uh1{}, Bc{}, tl);
+        __builtin_amdgcn_sched_barrier(0);
+        rd_b(2, k, 5);
+        __builtin_amdgcn_sched_barrier(0);
         // mid: every wave's ring reads of pair k done; pair k+1 (weights) / a halo chunk published
+        // (PRO 1: the raw chunk landed at mids 1 / 6, the transformed one published at 3 / 8)
         __builtin_amdgcn_s_waitcnt(M_WAIT_LGKM0);
-        if (wv < 2 || q == 3 || q == 8) __builtin_amdgcn_s_waitcnt(M_WAIT_VM0);
+        constexpr bool halo_wait = PRO == 1 ? (q == 1 || q == 6) : (q == 3 || q == 8);
+        if (wv < 2 || halo_wait) __builtin_amdgcn_s_waitcnt(M_WAIT_VM0);
         __builtin_amdgcn_s_barrier();
         if (wv < 2) {
             if (k + 2 < npair) pair_issue(k + 2);
+        } else if constexpr (PRO == 1) {
+            if constexpr (TCX_M_VAR == 1) {   // in halves: thirds 0-1 at the mid of pair 4 / 8, third 2 at 5 / 0
+                if constexpr (q == 4) {
+                    if (2 * pp + 2 < cpt) { halo_third(2 * pp + 2, 0, 0); halo_third(2 * pp + 2, 0, 1); }
+                } else if constexpr (q == 5) {
+                    if (2 * pp + 2 < cpt) halo_third(2 * pp + 2, 0, 2);
+                } else if constexpr (q == 8) {
+                    if (2 * pp + 3 < cpt) { halo_third(2 * pp + 3, 1, 0); halo_third(2 * pp + 3, 1, 1); }
+                } else if constexpr (q == 0) {
+                    if (2 * pp + 1 < cpt && pp > 0) halo_third(2 * pp + 1, 1, 2);
+                }
+            } else if constexpr (q == 4) {     // chunk 2 pp + 2 -> buffer 0 (chunk 2 pp was last read by pair 4)
+                if (2 * pp + 2 < cpt) halo_all(2 * pp + 2, 0);
+            } else if constexpr (q == 8) {     // chunk 2 pp + 3 -> buffer 1 (chunk 2 pp + 1 last read by pair 8)
+                if (2 * pp + 3 < cpt) halo_all(2 * pp + 3, 1);
+            }
         } else {
             if constexpr (q >= 4 && q <= 6) {  // chunk 2 pp + 2 -> buffer 0 (chunk 2 pp was last read by pair 4)
                 if (2 * pp + 2 < cpt) halo_third(2 * pp + 2, 0, q - 4);
@@ -268,20 +462,21 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         // H2: column blocks 3-5; slots 0, 1 then take B(k+1) blocks 0, 1; block 5 runs row block by row
         // block so that A(k+1) of each row block is read right after its last use of A(k), then slot 2
         // takes B(k+1) block 2
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            mf_col(3 + i, i);
-            __builtin_amdgcn_sched_barrier(0);
-            rd_b(i, k + 1, i);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) {
-            mf3(rb, 5, 2);
+        mf_col(3, 0, std::integral_constant<int, 0>{}, Uh2{}, Bc{}, tl);
+        __builtin_amdgcn_sched_barrier(0);
+        rd_b(0, k + 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mf_col(4, 1, std::integral_constant<int, 12>{}, Uh2{}, Bc{}, tl);
+        __builtin_amdgcn_sched_barrier(0);
+        rd_b(1, k + 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        m_static_for([&](auto RB) {
+            constexpr int rb = decltype(RB)::value;
+            mf3(rb, 5, 2, std::integral_constant<int, 24 + 3 * rb>{}, Uh2{}, Bc{}, tl);
             __builtin_amdgcn_sched_barrier(0);
             rd_a(qn, rb);
             __builtin_amdgcn_sched_barrier(0);
-        }
+        }, std::make_integer_sequence<int, 4>{});
         rd_b(2, k + 1, 2);
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -403,20 +598,22 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
 
 template <int W>
 int launch3m(const ConvParams& p, hipStream_t st) {
-    static bool attr[2] = {};
+    static bool attr[3] = {};
+    const bool pro = p.sc1 != nullptr;
     const bool fast = p.act == 0 && !p.out_h2;
-    const int ai = (int)fast;
-    void (*const k)(ConvParams) = fast ? &k_conv3m<W, true> : &k_conv3m<W, false>;
+    const int ai = pro ? 2 : (int)fast;
+    void (*const k)(ConvParams) = pro ? &k_conv3m<W, true, 1> : fast ? &k_conv3m<W, true, 0> : &k_conv3m<W, false, 0>;
+    const size_t lds = pro ? conv3m_lds_bytes<W, 1>() : conv3m_lds_bytes<W, 0>();
     if (!attr[ai]) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)conv3m_lds_bytes<W>()) != hipSuccess) {
-            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", conv3m_lds_bytes<W>());
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+            hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", lds);
             return TCX_EHIP;
         }
         attr[ai] = true;
     }
     const int grid = (p.M / M_TP) * p.n_nblk;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * M_NW), conv3m_lds_bytes<W>(), st, p);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * M_NW), lds, st, p);
     return check_launch("tcx_conv2d_h2(3x3 16x16x32)");
 }
 
@@ -430,10 +627,22 @@ int launch3m(const ConvParams& p, hipStream_t st) {
 // deterministic (profiles/r04_m2_*) and the headline runs 79.9-80.1 -> 82.6-82.7 images/s.
 
 
-// called by launch_conv3l for the h2-source (PRO 0) form: k_conv3lg's conditions plus the fast
-// epilogue's (dense NHWC fp32 / h2 output, no per-batch bias or residual, 32-bit offsets)
+// TCX_CONV3MG=0 keeps the GroupNorm-prologue convs on k_conv3lg / k_conv3g (A/B measurements)
+bool conv3mg_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("TCX_CONV3MG");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// called by launch_conv3l: k_conv3lg's conditions plus the fast epilogue's (dense NHWC fp32 / h2 output,
+// no per-batch bias or residual, 32-bit offsets); h2 sources (PRO 0), or ONE fp32 source with its
+// GroupNorm+SiLU tables and an fp32 output (PRO 1)
 bool conv3m_takes(const ConvParams& p) {
-    return !p.bf && p.circular && p.sc1 == nullptr && !(p.C2 > 0 && p.sc2 != nullptr) &&
+    const bool pro = p.sc1 != nullptr;
+    if (pro && (!conv3mg_enabled() || p.C2 != 0 || p.act != 0 || p.out_h2 || p.sh1 == nullptr)) return false;
+    return !p.bf && p.circular && !(p.C2 > 0 && p.sc2 != nullptr) &&
            (p.W == 16 || p.W == 32 || p.W == 64) && p.M % M_TP == 0 && p.HoWo % M_TP == 0 && p.Cin % 32 == 0 &&
            p.Cin <= 384 && p.Cout % M_BN == 0 && p.osy == 1 && p.osx == 1 && p.bias_b == nullptr &&
            p.resid == nullptr && (long long)p.M * p.Cout < (1ll << 29) && p.wscale != nullptr;
