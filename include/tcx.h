@@ -454,27 +454,6 @@ int tcx_gemm_ws(int M, int N, int K, float alpha, const float* A, long long sa_m
                 long long sb_hi, long long sb_lo, long long sc_hi, long long sc_lo, void* ws,
                 size_t ws_bytes, void* stream);
 
-/* f16x3 GEMM of the training Linears (csrc/gemm_x3.hip): C[M][N] (row stride ldc) =
- * act(alpha sum_k A(m,k) B(n,k) + beta C + bias[n] + resid[m][n]) with A in "h2 rows" form (f16 hi / lo
- * records [M][K/8][8 hi | 8 lo], row m scaled by the exact power of two 1 / inva[m]) and B either
- * h2 rows [N][K] with invb[N] (invb != NULL) or fp32 B(n,k) = B[n sb_n + k sb_k] (sb_k == 1, or sb_n ==
- * 1 with N % 4 == 0) split on the fly with the power of two of *amax_b (max |B| as float bits).  Three
- * f16 MFMA products per pair, fp32 accumulation.  Replaces the forward x W^T, dgrad dy W and wgrad
- * dy^T x GEMMs of DiffusionPriorFiLM's fc1 / fc2 / cond (diffusion_prior.py:39-55).  K % 8 == 0.
- * tcx_gemm_x3_workspace: split-K scratch bytes (0: none).  act 0/1/2/3 = none, relu, sigmoid, silu.
- * tcx_h2_rows: h2 rows of x [R][K] (row stride ldx) with per-row scales; tcx_h2_cols: h2 rows of
- * x^T for x [R][C] (R % 8 == 0) with per-column scales.  tcx_absmax_multi: max |x_i| of up to 32
- * tensors (n_i % 4 == 0) into bits[i] (zeroed first), one launch. */
-int tcx_h2_rows(const float* x, int R, int K, long long ldx, void* out, float* inv, void* stream);
-int tcx_h2_cols(const float* x, int R, int C, long long ldx, void* out, float* inv, void* stream);
-int tcx_absmax_multi(const float* const* xs, const size_t* ns, int count, unsigned* bits, void* stream);
-int tcx_gemm_x3_ok(int M, int N, int K, const float* B, long long sb_k, long long sb_n, int b_h2);
-size_t tcx_gemm_x3_workspace(int M, int N, int K);
-int tcx_gemm_x3(int M, int N, int K, float alpha, const void* A, const float* inva, const void* B,
-                long long sb_k, long long sb_n, const float* invb, const unsigned* amax_b, float beta,
-                float* C, long long ldc, const float* bias, const float* resid, long long ld_resid, int act,
-                void* ws, size_t ws_bytes, void* stream);
-
 /* Conv2d weight gradient dw[Cout][C1+C2][ks][ks] (= beta*dw + ...) from the NHWC input
  * [x1 | x2] [Bt][H][W][C1+C2] and the output gradient dy [Bt][Ho][Wo][Cout] (circular or zero
  * padding).  Also the ConvTranspose2d weight gradient (input/output roles swapped).  Backward of

@@ -81,11 +81,12 @@ __device__ __forceinline__ void block_amax_publish(float m, unsigned* amax) {
 // SiLU with the hardware exp2 / reciprocal (a few ulp; used in staged prologues)
 
 // Call first thing in an MFMA kernel: an AGPR reference keeps hipcc from proving the kernel AGPR-free,
-// so it selects the AGPR form of the MFMAs (accumulators in AGPRs, fragments in VGPRs).  In the
-// all-VGPR form the allocator may move an accumulator (MFMA D != C) and reuse its old SrcC register
-// for a following ds_read / load; an MFMA queued behind other waves' MFMAs on the matrix pipe can read
-// SrcC after that data has landed: wrong sums whenever other kernels share the CU (k_conv3m under the
-// sampling lanes, r04_n; tools/mfma_war_check.py finds the pattern in the .s).
+// so it selects the AGPR form of the MFMAs (accumulators in AGPRs, fragments in VGPRs).  Round 4 added
+// it to k_conv3m while chasing wrong sums under co-run (r04_n), suspecting the all-VGPR form's reuse of
+// a moved accumulator's old SrcC register as a load destination; the cause was the store-data hazard
+// (conv_common.hpp store_b128_guarded).  k_conv3m runs the all-VGPR form again since round 5 (equal
+// speed, co-run / lane tests green without it, profiles/r05_c_*); the skinny prior GEMMs keep it.
+// tools/mfma_war_check.py lists the SrcC-reuse sites of a .s.
 __device__ __forceinline__ void mfma_agpr_form() { asm volatile("" ::: "a0"); }
 
 __device__ __forceinline__ int wrap_idx(int i, int n) {

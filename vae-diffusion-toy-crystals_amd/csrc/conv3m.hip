@@ -79,28 +79,31 @@ __device__ __forceinline__ void m_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int
 __device__ unsigned long long* g_m_stamps = nullptr;
 __device__ int g_m_stamps_n = 0;
 
-// PRO 1: task of MFMA gap G (0..35) of a half-pair that carries a transform unit: 0 load (two
-// ds_read_b128 + the scale / shift of values 0-1), 1..8 value code - 1 (GroupNorm affine + SiLU),
-// 9..12 the h2 split of channel pair code - 9, 13 the write-back (two ds_write_b128) and the range
-// flag, 14..16 the scale / shift of value pair code - 13 (two ds_read_b64, read two gaps before their
-// first value); -1 none.  The load leads the first value by 3 MFMAs (its LDS latency).
-constexpr int m_tcode(int G) {
-    return G == 0 ? 0 : G == 3 ? 1 : G == 4 ? 14 : G == 5 ? 2 : G == 7 ? 9 : G == 9 ? 3 : G == 10 ? 15 : G == 11 ? 4
-         : G == 13 ? 10 : G == 15 ? 5 : G == 16 ? 16 : G == 17 ? 6 : G == 19 ? 11 : G == 21 ? 7 : G == 23 ? 8
-         : G == 25 ? 12 : G == 27 ? 13 : -1;
-}
+// PRO 1: the transform unit's tasks over the 36 MFMA gaps of a half-pair, as (gap, task) in issue
+// order: task 0 load (two ds_read_b128 + the scale / shift of values 0-1), 1..8 value task - 1 part A
+// (y = x sc + sh, e = exp2(-y log2 e)), 9..16 part B (y rcp(1 + e)), 17..20 the h2 split of channel
+// pair task - 17, 21 the write-back (two ds_write_b128) and the range flag, 22..24 the scale / shift
+// of value pair task - 21 (two ds_read_b64; the pair buffer they refill is free by then).
+struct MTask {
+    int gap, task;
+};
+// Two parts of a value back to back, one value per other gap.  Measured per layer against the
+// alternatives (tools/gpu/r05f.sh, profiles/r05_f_conv.txt: up1_1 496 / 493 / 532 us, h2-source form
+// 409): an exp2 pair then its reciprocals two gaps later (equal), a whole value pair per gap (bursts,
+// 7 % slower), and each value's parts spread over separate gaps (r05_e: 5 % slower).  The transform's
+// VALU (two quarter-rate transcendentals per value, 1.3-1.55 halo values per output pixel) is what the
+// form costs over the h2-source one: without the transform tasks (a diagnostic build, wrong results)
+// it runs at the h2-source form's speed (r05_c).
+constexpr MTask kMSched[] = {{0, 0},   {3, 1},   {3, 9},   {4, 22},  {5, 2},   {5, 10},  {7, 17},
+                             {9, 3},   {9, 11},  {10, 23}, {11, 4},  {11, 12}, {13, 18}, {15, 5},
+                             {15, 13}, {16, 24}, {17, 6},  {17, 14}, {19, 19}, {21, 7},  {21, 15},
+                             {23, 8},  {23, 16}, {25, 20}, {27, 21}};
+constexpr const MTask* m_sched() { return kMSched; }
+constexpr int M_NTASK = 25;
 template <typename F, int... Is>
 __device__ __forceinline__ void m_static_for(F&& f, std::integer_sequence<int, Is...>) {
     (f(std::integral_constant<int, Is>{}), ...);
 }
-
-// A/B build variants of the prologue form (tools/build_variant.sh; 0 = the product)
-#ifndef TCX_M_VAR
-#define TCX_M_VAR 0
-#endif
-#ifndef TCX_M_AGPR
-#define TCX_M_AGPR 1
-#endif
 
 constexpr int M_WAIT_VM0 = 0x0F70;    // s_waitcnt vmcnt(0)
 constexpr int M_WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0)
@@ -137,7 +140,8 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     int lz;
     asm volatile("s_mov_b32 %0, 0" : "=s"(lz));
     char* const smd = smc + lz;
-    if constexpr (PRO == 0 && TCX_M_AGPR) mfma_agpr_form();  // accumulators in AGPRs (common.hpp)
+    // accumulators in VGPRs (hipcc's all-VGPR MFMA form; the AGPR form of round 4, common.hpp
+    // mfma_agpr_form, measured equal and is not needed: r05_c, with the co-run and lane tests green)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -170,8 +174,11 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     const int hw = wv & 1;
     const int rowb = p.C1 * 4;
     const int img0 = bs * H;
-    const int ls = lane >> 2;
     auto halo_voff = [&](int i) __attribute__((always_inline)) {
+        // PRO 1 at 64-px rows: recomputed at every issue (an opaque copy of the lane index keeps hipcc from
+        // hoisting all 13 offsets out of the tap loop, where they spilled with the transform's registers)
+        int ls = lane >> 2;
+        if constexpr (PRO == 1) asm volatile("v_mov_b32 %0, %1" : "=v"(ls) : "v"(lane >> 2));
         const int hr0 = (16 * i) / W2;
         const int th = W2 * (hr0 + 1) - 16 * i;
         const int y0 = wrap_idx(r0 + hr0 - 1, H), y1 = wrap_idx(r0 + hr0, H);
@@ -283,17 +290,40 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         tsc[q & 1] = *reinterpret_cast<const f32x2*>(t);
         tsh[q & 1] = *reinterpret_cast<const f32x2*>(t + p.C1);
     };
+    // the unit's LDS reads / writes as inline asm: the compiler counts every C++ LDS read after an
+    // LDS-DMA issue as a possible alias of the DMA and waits for vmcnt(0) first (it stalled the weight
+    // waves on the pair they had just issued, one L2 round trip per transform half); the halo buffer a
+    // unit rewrites is never a DMA target while it is transformed (the raw chunk landed at the previous
+    // mid), so the reads need only lgkmcnt, which t_val 0's explicit wait provides
+    const int lds_base = (int)(size_t)((__attribute__((address_space(3))) char*)smc);
+    auto lds_rd16 = [&](int a) __attribute__((always_inline)) {
+        f32x4 v;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+        return v;
+    };
+    auto lds_wr16 = [&](int a, u32x4 v) __attribute__((always_inline)) {
+        asm volatile("ds_write_b128 %0, %1" : : "v"(a), "v"(v) : "memory");
+    };
     auto t_load = [&](int i, int buf) __attribute__((always_inline)) {
         t_addr(i);
-        const float4 x0 = *reinterpret_cast<const float4*>(smc + buf * HB + tdst);
-        const float4 x1 = *reinterpret_cast<const float4*>(smc + buf * HB + (tdst ^ 16));
-        ux[0] = x0.x; ux[1] = x0.y; ux[2] = x0.z; ux[3] = x0.w; ux[4] = x1.x; ux[5] = x1.y; ux[6] = x1.z; ux[7] = x1.w;
+        const int lb = lds_base + buf * HB;
+        const f32x4 x0 = lds_rd16(lb + tdst);
+        const f32x4 x1 = lds_rd16(lb + (tdst ^ 16));
+        ux[0] = x0[0]; ux[1] = x0[1]; ux[2] = x0[2]; ux[3] = x0[3]; ux[4] = x1[0]; ux[5] = x1[1]; ux[6] = x1[2]; ux[7] = x1[3];
         um = 0.f;
         t_tab(0);
     };
-    auto t_val = [&](int k) __attribute__((always_inline)) {
+    float ue[2];  // exp2 of value k between its parts A and B
+    auto t_valA = [&](int k) __attribute__((always_inline)) {
+        if (k == 0) __builtin_amdgcn_s_waitcnt(M_WAIT_LGKM0);  // the unit's asm reads (t_load)
         const int q = k >> 1, e = k & 1;
-        ux[k] = silu_hw(fmaf(ux[k], tsc[q & 1][e], tsh[q & 1][e]));
+        ux[k] = fmaf(ux[k], tsc[q & 1][e], tsh[q & 1][e]);
+        ue[k & 1] = __builtin_amdgcn_exp2f(-1.4426950408889634f * ux[k]);
+    };
+    auto t_valB = [&](int k) __attribute__((always_inline)) { ux[k] = ux[k] * __builtin_amdgcn_rcpf(1.0f + ue[k & 1]); };
+    auto t_val = [&](int k) __attribute__((always_inline)) {
+        t_valA(k);
+        t_valB(k);
     };
     auto t_pair = [&](int q) __attribute__((always_inline)) {
         const f32x2 v = {ux[2 * q], ux[2 * q + 1]};
@@ -305,18 +335,38 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         um = fmaxf(um, fmaxf(fabsf(v[0]), fabsf(v[1])));
     };
     auto t_store = [&](int buf, bool live) __attribute__((always_inline)) {
-        *reinterpret_cast<uint4*>(smc + buf * HB + tdst) = make_uint4(uh[0], uh[1], uh[2], uh[3]);
-        *reinterpret_cast<uint4*>(smc + buf * HB + (tdst ^ 16)) = make_uint4(ul[0], ul[1], ul[2], ul[3]);
+        const int lb = lds_base + buf * HB;
+        lds_wr16(lb + tdst, (u32x4){uh[0], uh[1], uh[2], uh[3]});
+        lds_wr16(lb + (tdst ^ 16), (u32x4){ul[0], ul[1], ul[2], ul[3]});
         h2_flag(p.ovf, !(um < kH2Max) && live && tlive);
     };
     // one task (m_tcode) of a transform unit
     auto t_task = [&](auto Cc, int U, int buf, bool live) __attribute__((always_inline)) {
         constexpr int code = decltype(Cc)::value;
         if constexpr (code == 0) t_load(U, buf);
-        else if constexpr (code <= 8) t_val(code - 1);
-        else if constexpr (code <= 12) t_pair(code - 9);
-        else if constexpr (code == 13) t_store(buf, live);
-        else t_tab(code - 13);  // 14..16: tables of value pair 1..3
+        else if constexpr (code <= 8) t_valA(code - 1);
+        else if constexpr (code <= 16) t_valB(code - 9);
+        else if constexpr (code <= 20) t_pair(code - 17);
+        else if constexpr (code == 21) t_store(buf, live);
+        else t_tab(code - 21);  // 22..24: tables of value pair 1..3
+    };
+    // the tasks scheduled into MFMA gap G (m_sched order), fenced by sched barriers
+    auto t_gap = [&](auto Gc, int U, int buf, bool live) __attribute__((always_inline)) {
+        constexpr int G = decltype(Gc)::value;
+        constexpr bool any = [] {
+            for (int e = 0; e < M_NTASK; ++e)
+                if (m_sched()[e].gap == G) return true;
+            return false;
+        }();
+        if constexpr (any) {
+            __builtin_amdgcn_sched_barrier(0);
+            m_static_for([&](auto E) {
+                constexpr int e = decltype(E)::value;
+                if constexpr (m_sched()[e].gap == G)
+                    t_task(std::integral_constant<int, m_sched()[e].task>{}, U, buf, live);
+            }, std::make_integer_sequence<int, M_NTASK>{});
+            __builtin_amdgcn_sched_barrier(0);
+        }
     };
 
     // ---- prologue: pairs 0, 1 and halo chunk 0 in LDS; the first third of chunk 1 issued
@@ -370,14 +420,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         m_static_for([&](auto K) {
             constexpr int k = decltype(K)::value;
             mfk(k, nb, i);
-            if constexpr (U >= 0 && TCX_M_VAR != 9) {
-                constexpr int code = m_tcode(G0 + k);
-                if constexpr (code >= 0) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    t_task(std::integral_constant<int, code>{}, U, BUF, tl);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
+            if constexpr (U >= 0) t_gap(std::integral_constant<int, G0 + k>{}, U, BUF, tl);
         }, std::make_integer_sequence<int, 12>{});
     };
     // the 3 MFMAs of row block rb, column block nb (B slot i) as gaps G0 .. G0 + 2
@@ -386,14 +429,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         m_static_for([&](auto K) {
             constexpr int pr = decltype(K)::value;
             mfk(4 * pr + rb, nb, i);
-            if constexpr (U >= 0 && TCX_M_VAR != 9) {
-                constexpr int code = m_tcode(G0 + pr);
-                if constexpr (code >= 0) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    t_task(std::integral_constant<int, code>{}, U, BUF, tl);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
+            if constexpr (U >= 0) t_gap(std::integral_constant<int, G0 + pr>{}, U, BUF, tl);
         }, std::make_integer_sequence<int, 3>{});
     };
 
@@ -434,17 +470,8 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         if (wv < 2) {
             if (k + 2 < npair) pair_issue(k + 2);
         } else if constexpr (PRO == 1) {
-            if constexpr (TCX_M_VAR == 1) {   // in halves: thirds 0-1 at the mid of pair 4 / 8, third 2 at 5 / 0
-                if constexpr (q == 4) {
-                    if (2 * pp + 2 < cpt) { halo_third(2 * pp + 2, 0, 0); halo_third(2 * pp + 2, 0, 1); }
-                } else if constexpr (q == 5) {
-                    if (2 * pp + 2 < cpt) halo_third(2 * pp + 2, 0, 2);
-                } else if constexpr (q == 8) {
-                    if (2 * pp + 3 < cpt) { halo_third(2 * pp + 3, 1, 0); halo_third(2 * pp + 3, 1, 1); }
-                } else if constexpr (q == 0) {
-                    if (2 * pp + 1 < cpt && pp > 0) halo_third(2 * pp + 1, 1, 2);
-                }
-            } else if constexpr (q == 4) {     // chunk 2 pp + 2 -> buffer 0 (chunk 2 pp was last read by pair 4)
+            // (the raw chunk in two parts over mids 4-5 / 8-0 measured no faster: r05_c)
+            if constexpr (q == 4) {     // chunk 2 pp + 2 -> buffer 0 (chunk 2 pp was last read by pair 4)
                 if (2 * pp + 2 < cpt) halo_all(2 * pp + 2, 0);
             } else if constexpr (q == 8) {     // chunk 2 pp + 3 -> buffer 1 (chunk 2 pp + 1 last read by pair 8)
                 if (2 * pp + 3 < cpt) halo_all(2 * pp + 3, 1);
@@ -622,10 +649,9 @@ int launch3m(const ConvParams& p, hipStream_t st) {
 // Default for the h2-source 3x3 convs it covers (round 4).  It had been opt-in: with other kernels
 // sharing its CUs a few 16x16 blocks per launch got one wrong channel.  The cause was the store-data
 // hazard of its quad epilogue (a 16-B store's first data VGPR rewritten across an if/else join with no
-// wait state, conv_common.hpp store_b128_guarded), not the MFMA / ds_read order: with the pad and
-// without the MFMA-dependency waits that had only made it rarer, the co-run and sampler probes are
-// deterministic (profiles/r04_m2_*) and the headline runs 79.9-80.1 -> 82.6-82.7 images/s.
-
+// wait state, conv_common.hpp store_b128_guarded), not the MFMA / ds_read order: with the pad, the
+// co-run and sampler probes are deterministic (profiles/r04_m2_*), and since round 5 also without the
+// AGPR accumulator form (tests/test_gpu_headline.py co-run repeats, profiles/r05_c_*).
 
 // TCX_CONV3MG=0 keeps the GroupNorm-prologue convs on k_conv3lg / k_conv3g (A/B measurements)
 bool conv3mg_enabled() {

@@ -150,13 +150,6 @@ _SIGS = {
     "tcx_gemm_workspace": (c_size, [c_int, c_int, c_int, c_int]),
     "tcx_gemm_ws": (c_int, [c_int, c_int, c_int, c_float, c_fp, c_ll, c_ll, c_fp, c_ll, c_ll, c_float, c_fp, c_ll,
                             c_ll, c_fp, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_fp, c_size, c_fp]),
-    "tcx_h2_rows": (c_int, [c_fp, c_int, c_int, c_ll, c_fp, c_fp, c_fp]),
-    "tcx_h2_cols": (c_int, [c_fp, c_int, c_int, c_ll, c_fp, c_fp, c_fp]),
-    "tcx_absmax_multi": (c_int, [c_fp, c_fp, c_int, c_fp, c_fp]),
-    "tcx_gemm_x3_ok": (c_int, [c_int, c_int, c_int, c_fp, c_ll, c_ll, c_int]),
-    "tcx_gemm_x3_workspace": (c_size, [c_int, c_int, c_int]),
-    "tcx_gemm_x3": (c_int, [c_int, c_int, c_int, c_float, c_fp, c_fp, c_fp, c_ll, c_ll, c_fp, c_fp, c_float, c_fp,
-                            c_ll, c_fp, c_fp, c_ll, c_int, c_fp, c_size, c_fp]),
     "tcx_conv_wgrad_workspace": (c_size, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "tcx_conv_wgrad": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_int, c_int, c_int, c_int, c_int,
                                c_float, c_fp, c_fp, c_size, c_fp]),

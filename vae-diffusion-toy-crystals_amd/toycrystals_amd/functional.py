@@ -536,73 +536,22 @@ class AttentionFn(torch.autograd.Function):
 
 
 # ---------------------------------------------------------------- linear / activations / embedding
-def absmax_words(ts) -> torch.Tensor:
-    """max |t| of each tensor (<= 32) as float bits, one int32 word per tensor, in one launch
-    (tcx_absmax_multi): the power-of-two scales of the f16x3 GEMM's weight operands"""
-    ts = [t.detach() for t in ts]
-    dev = ts[0].device
-    words = torch.empty(len(ts), dtype=torch.int32, device=dev)
-    ptrs = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
-    ns = (ctypes.c_size_t * len(ts))(*[t.numel() for t in ts])
-    check(lib().tcx_absmax_multi(ptrs, ns, len(ts), ptr(words), _st(ts[0])), "tcx_absmax_multi")
-    return words
-
-
-def h2_rows(x: torch.Tensor):
-    """f16 hi / lo records of x [R][K] with per-row power-of-two scales (tcx_h2_rows): (records, inv)"""
-    R, K = x.shape
-    out = torch.empty(R * K * 4, dtype=torch.uint8, device=x.device)
-    inv = _empty((R,), x)
-    check(lib().tcx_h2_rows(ptr(x), R, K, K, ptr(out), ptr(inv), _st(x)), "tcx_h2_rows")
-    return out, inv
-
-
-def h2_cols(x: torch.Tensor):
-    """records of x^T for x [R][C] with per-column scales (tcx_h2_cols): (records [C][R], inv [C])"""
-    R, C = x.shape
-    out = torch.empty(R * C * 4, dtype=torch.uint8, device=x.device)
-    inv = _empty((C,), x)
-    check(lib().tcx_h2_cols(ptr(x), R, C, C, ptr(out), ptr(inv), _st(x)), "tcx_h2_cols")
-    return out, inv
-
-
-def gemm_x3(M, N, K, A, inva, B, sb_k, sb_n, invb, amax_b, C, bias=None, resid=None, act=0):
-    """C[M][N] (contiguous) = act(sum_k A(m,k) B(n,k) + bias + resid) on the f16x3 GEMM (tcx_gemm_x3):
-    A h2 rows [M][K] with inva; B h2 rows [N][K] with invb, or fp32 strided with its max-|B| word"""
-    L = lib()
-    nb = int(L.tcx_gemm_x3_workspace(M, N, K))
-    ws = _ws(C.device, nb) if nb else None
-    check(L.tcx_gemm_x3(M, N, K, 1.0, ptr(A), ptr(inva), ptr(B), sb_k, sb_n, ptr(invb), ptr(amax_b), 0.0, ptr(C), N,
-                        ptr(bias), ptr(resid), N, act, ptr(ws) if ws is not None else None, nb, _st(C)), "tcx_gemm_x3")
-
-
-def _x3_fp32_b(M, N, K, w, sb_k, sb_n) -> bool:
-    return K % 8 == 0 and lib().tcx_gemm_x3_ok(M, N, K, ptr(w), sb_k, sb_n, 0) == 1
-
-
 class LinearFn(torch.autograd.Function):
-    """y = x W^T + b (+ resid), x [M][K] (row stride K), W [N][K].  With amax_w (the max-|W| word of
-    absmax_words) the three GEMMs run on f16x3 MFMA (csrc/gemm_x3.hip) where their shapes allow:
-    forward on h2 rows of x and W split on the fly, dgrad on h2 rows of dy and W, wgrad on the h2 rows
-    of dy^T and x^T; fp32 MFMA otherwise."""
+    """y = x W^T + b (+ resid), x [M][K] (row stride K), W [N][K], on the fp32-MFMA GEMM (tcx_gemm_ws;
+    an f16x3 GEMM for these shapes measured slower per prior step and was removed)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, resid=None, amax_w=None):
+    def forward(ctx, x, w, b, resid=None):
         x, w, b, resid = _c(x), _c(w), _c(b), _c(resid)
         M, K = x.shape
         N = w.shape[0]
         y = _empty((M, N), x)
-        if amax_w is not None and _x3_fp32_b(M, N, K, w, 1, K):
-            hx, ix = h2_rows(x)
-            gemm_x3(M, N, K, hx, ix, w, 1, K, None, amax_w, y, bias=b, resid=resid)
-        else:
-            beta = 0.0
-            if resid is not None:
-                check(lib().tcx_copy2d(ptr(resid), N, ptr(y), N, M, N, 0.0, _st(x)), "copy2d")
-                beta = 1.0
-            gemm(M, N, K, x, K, 1, w, 1, K, y, N, 1, beta=beta, bias=b)
+        beta = 0.0
+        if resid is not None:
+            check(lib().tcx_copy2d(ptr(resid), N, ptr(y), N, M, N, 0.0, _st(x)), "copy2d")
+            beta = 1.0
+        gemm(M, N, K, x, K, 1, w, 1, K, y, N, 1, beta=beta, bias=b)
         ctx.save_for_backward(x, w)
-        ctx.amax_w = amax_w
         ctx.has = (b is not None, resid is not None)
         return y
 
@@ -612,32 +561,22 @@ class LinearFn(torch.autograd.Function):
         dy = dy.contiguous()
         M, K = x.shape
         N = w.shape[0]
-        x3 = ctx.amax_w is not None
         dx = dw = db = dr = None
         if ctx.needs_input_grad[0]:
             dx = _empty((M, K), dy)
-            if x3 and _x3_fp32_b(M, K, N, w, K, 1):
-                hdy, idy = h2_rows(dy)
-                gemm_x3(M, K, N, hdy, idy, w, K, 1, None, ctx.amax_w, dx)
-            else:
-                gemm(M, K, N, dy, N, 1, w, K, 1, dx, K, 1)
+            gemm(M, K, N, dy, N, 1, w, K, 1, dx, K, 1)
         if ctx.needs_input_grad[1]:
             dw = _empty((N, K), dy)
-            if x3 and M % 8 == 0 and lib().tcx_gemm_x3_ok(N, K, M, None, 0, 0, 1) == 1:
-                hdt, idt = h2_cols(dy)
-                hxt, ixt = h2_cols(x)
-                gemm_x3(N, K, M, hdt, idt, hxt, 0, 0, ixt, None, dw)
-            else:
-                gemm(N, K, M, dy, 1, N, x, K, 1, dw, K, 1)
+            gemm(N, K, M, dy, 1, N, x, K, 1, dw, K, 1)
         if ctx.has[0] and ctx.needs_input_grad[2]:
             db = _colsum_total(dy, M, N)
         if ctx.has[1] and ctx.needs_input_grad[3]:
             dr = dy
-        return dx, dw, db, dr, None
+        return dx, dw, db, dr
 
 
-def linear(x, m: torch.nn.Linear, resid=None, amax_w=None):
-    return LinearFn.apply(x, m.weight, m.bias, resid, amax_w)
+def linear(x, m: torch.nn.Linear, resid=None):
+    return LinearFn.apply(x, m.weight, m.bias, resid)
 
 
 class ActFn(torch.autograd.Function):

@@ -213,8 +213,7 @@ class DiffusionPriorFiLM(nn.Module):
         y_feat = TF.linear(TF.act(TF.linear(TF.cat_cols(ycf, ycont), self.y_fuse[0]), TF.ACT_SILU), self.y_fuse[2])
         cond = TF.cat_cols(t_feat, y_feat)
         h = TF.linear(z_t.to(torch.float32), self.in_proj)
-        # fp32-MFMA GEMMs: the f16x3 GEMM of csrc/gemm_x3.hip (TF.linear(..., amax_w=...)) is parity-green
-        # but measured slower on this step
+        # fp32-MFMA GEMMs (an f16x3 GEMM measured slower on this step and was removed: DESIGN.md §3k)
         for blk in self.blocks:
             gb = TF.linear(cond, blk.cond)  # [gamma | beta] = cond(cond).chunk(2)
             hn = TF.LayerNormFiLMFn.apply(h, blk.norm.weight, blk.norm.bias, gb, blk.norm.eps)
