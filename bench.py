@@ -302,6 +302,7 @@ def main() -> int:
     conv_avg_ms = ms.value / max(1, n.value)
     conv_avg_flop = fl.value / max(1, n.value)
     achieved = conv_avg_flop / (conv_avg_ms * 1e-3) / 1e12 if n.value else 0.0
+    traffic = TRAFFIC_BYTES_PER_CONV_LAUNCH.get(args.precision) if S == 64 else None
     result = {
         "metric": "denoised images/sec (300-step reverse-SDE, CFG=1.5) at 1/2/4/8 MI355X",
         "value": round(value, 4),
@@ -324,8 +325,10 @@ def main() -> int:
         "path_tflops": round(value / world * FWD_PER_IMG * GFLOP_PER_IMG_FWD / 1e3, 3) if S == 64 else None,
         "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": round(peak, 1),
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                     "traffic": TRAFFIC_BYTES_PER_CONV_LAUNCH.get(args.precision) if S == 64 else None,
-                     "traffic_unit": "HBM bytes per conv launch", "traffic_source": TRAFFIC_SOURCE,
+                     "traffic": traffic,
+                     "traffic_unit": "HBM bytes per conv launch",
+                     "traffic_source": TRAFFIC_SOURCE if traffic is not None else
+                     "not measured for this configuration (PMC passes exist for the 64x64 f16x3 headline only)",
                      "peak_basis": peak_basis,
                      "measured_on": "one-lane roofline pass (same K sampling passes on one stream, HIP events per conv launch)",
                      "avg_launch_ms": round(conv_avg_ms, 5), "avg_launch_gflop": round(conv_avg_flop / 1e9, 4),

@@ -176,6 +176,17 @@ int tcx_gn_apply_tab_bf16(const float* x, void* y, int Bt, int HW, int C, const 
 int tcx_upsample2x_bf16(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
                         const float* shift, void* stream);
 int tcx_attention_split_bf16(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream);
+/* 2-byte bf16 ("b2", csrc/h2.hpp): config 5's tensors at 256^2 are plain NHWC bf16 (round to nearest
+ * even) — the hi halves of the bf16 records, which are all a bf16 product reads.  tcx_conv2d_h2_pro with
+ * bf16 = 2 reads b2 sources and writes a b2 output for out_h2 = 1 (k_conv3lb, k_conv4s2g, k_lin1x1 shapes
+ * only, no prologue); tcx_gn_apply_tab_b2 normalises an fp32 source into b2 (in_b2 = 0) or a b2 tensor in
+ * place (in_b2 = 1, x == y); tcx_upsample2x_b2 / tcx_attention_split_b2 write b2 (the attention reads b2
+ * qkv).  The U-Net evaluator uses them at precision 2 and 256^2 (sde_score_model.py:170-266). */
+int tcx_gn_apply_tab_b2(const void* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift,
+                        int silu, int in_b2, void* stream);
+int tcx_upsample2x_b2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
+                      void* stream);
+int tcx_attention_split_b2(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream);
 
 /* tcx_conv2d_h2 with the fragment-ordered weights (wfrag, or NULL) and a GroupNorm+SiLU prologue per
  * source: a source whose pro_scale/pro_shift

@@ -1,10 +1,10 @@
-# Round 4 final verification: determinism (alone + co-run), the whole GPU suite, the bench line, kernel trace
+# Final verification: determinism (alone + co-run), the whole GPU suite, the bench line, kernel trace
 # of the one-lane pass, HBM traffic PMC passes at the roofline's configuration (one lane: Bt = 256 per
 # launch), training steps.
 set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp
-T=${1:-r04_fin}
+T=${1:-r05_fin}
 timeout -k 10 200 python -u tools/determinism_probe.py > gpurun_out/${T}_det.log 2>&1 && \
 timeout -k 10 200 python -u tools/determinism_probe.py --corun > gpurun_out/${T}_corun.log 2>&1 && \
 grep -q "^deterministic" gpurun_out/${T}_det.log && grep -q "^deterministic" gpurun_out/${T}_corun.log && \

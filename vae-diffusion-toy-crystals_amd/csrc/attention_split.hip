@@ -33,15 +33,15 @@ _Pragma("unroll") \
             const int i = tid + 512 * u; \
             const int j = i / KPL, pc = i - (i / KPL) * KPL; \
             if (KT * KPL % 512 == 0 || i < KT * KPL) \
-                kreg[u] = *reinterpret_cast<const f4*>(base + (size_t)(k0 + j) * rs + (size_t)(C + h * D) * 4 + \
-                                                       (BF ? 2 * pc : pc) * 16); \
+                kreg[u] = *reinterpret_cast<const f4*>(base + (size_t)(k0 + j) * rs + (size_t)(C + h * D) * ESZ + \
+                                                       (B2 ? pc : BF ? 2 * pc : pc) * 16); \
         } \
 _Pragma("unroll") \
         for (int u = 0; u < VI; ++u) { \
             const int i = tid + 512 * u; \
             if (i < (KT / 2) * G) { \
                 const int g = i / (KT / 2), jp = i - g * (KT / 2);  /* key pair (2 jp, 2 jp + 1), dim group g */ \
-                const char* src = base + (size_t)(k0 + 2 * jp) * rs + (size_t)(2 * C + h * D) * 4 + g * 32; \
+                const char* src = base + (size_t)(k0 + 2 * jp) * rs + (size_t)(2 * C + h * D) * ESZ + g * 8 * ESZ; \
                 vreg[u][0] = *reinterpret_cast<const u4*>(src); \
                 if (!BF) vreg[u][1] = *reinterpret_cast<const u4*>(src + 16); \
                 vreg[u][2] = *reinterpret_cast<const u4*>(src + rs); \
@@ -87,10 +87,13 @@ _Pragma("unroll") \
 // never loaded), + 16 B pad (both strides an odd number of 16-B units: conflict-free b128 row reads)
 __host__ __device__ constexpr int attn_ksb(int D, bool BF) { return (BF ? D * 2 : D * 4) + 16; }
 
-// BF: bf16 records (h2.hpp), one v_mfma_f32_32x32x16_bf16 (hi x hi) per product, P in bf16
-template <int D, bool BF>
+// FMT 0: h2 records; 1 (BF): bf16 records (h2.hpp), one v_mfma_f32_32x32x16_bf16 (hi x hi) per product,
+// P in bf16; 2 (BF, B2): the same on 2-byte bf16 qkv and output (h2.hpp "b2": the records' hi halves)
+template <int D, int FMT>
 __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict__ qkv, char* __restrict__ out, int N,
                                                          int C, float scale) {
+    constexpr bool BF = FMT >= 1, B2 = FMT == 2;
+    constexpr int ESZ = B2 ? 2 : 4;  // bytes per element of qkv / out
     static_assert(D % 16 == 0 && D <= 64, "split attention: head dim multiple of 16, <= 64");
     constexpr int KT = 128;            // keys per staged tile
     constexpr int NST = KT / 32;       // 32-key subtiles
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     constexpr int STAGE = KT * KSB + 2 * DP * VSW * 4;
     const int b = blockIdx.z, h = blockIdx.y;
     const int tid = threadIdx.x;
-    const size_t rs = 12 * (size_t)C;  // bytes per token row of qkv (3C channels, 4 B each)
+    const size_t rs = 3 * ESZ * (size_t)C;  // bytes per token row of qkv (3C channels)
     const char* base = qkv + (size_t)b * N * rs;
     const int lane = tid & 63, w = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
@@ -113,11 +116,11 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     const float scale2 = scale * 1.4426950408889634f;  // log2(e) / sqrt(D)
     h8 qh[DS], ql[DS];
     {
-        const char* qr = base + (size_t)q * rs + (size_t)h * D * 4;
+        const char* qr = base + (size_t)q * rs + (size_t)h * D * ESZ;
 #pragma unroll
         for (int s = 0; s < DS; ++s) {
-            qh[s] = *reinterpret_cast<const h8*>(qr + (2 * s + lh) * 32);
-            ql[s] = *reinterpret_cast<const h8*>(qr + (2 * s + lh) * 32 + 16);
+            qh[s] = *reinterpret_cast<const h8*>(qr + (2 * s + lh) * 8 * ESZ);
+            if constexpr (!BF) ql[s] = *reinterpret_cast<const h8*>(qr + (2 * s + lh) * 32 + 16);
         }
     }
     auto Kb = [&](int st) { return smem + st * STAGE; };
@@ -277,26 +280,27 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
             if (d < D) {
                 const float4 v = make_float4(oacc[t][4 * i] * inv, oacc[t][4 * i + 1] * inv, oacc[t][4 * i + 2] * inv,
                                              oacc[t][4 * i + 3] * inv);
-                store4_h2x(out, ((size_t)b * N + q) * C * 4, (h * D + d) >> 2, v, BF);
+                if constexpr (B2) store4_b2(out, ((size_t)b * N + q) * C, (h * D + d) >> 2, v);
+                else store4_h2x(out, ((size_t)b * N + q) * C * 4, (h * D + d) >> 2, v, BF);
             }
         }
 }
 
-template <int D, bool BF>
+template <int D, int FMT>
 int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
     const float scale = (float)(1.0 / std::sqrt((double)D));
     constexpr int DP = (D + 31) / 32 * 32;
-    constexpr size_t shm = 2 * ((size_t)128 * attn_ksb(D, BF) + 2 * (size_t)DP * (128 / 2 + 4) * 4);
+    constexpr size_t shm = 2 * ((size_t)128 * attn_ksb(D, FMT >= 1) + 2 * (size_t)DP * (128 / 2 + 4) * 4);
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D, BF>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D, FMT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) {
             set_error("tcx_attention_split: cannot enable %zu B of dynamic LDS", shm);
             return TCX_EHIP;
         }
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_attention_split<D, BF>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
+    hipLaunchKernelGGL((k_attention_split<D, FMT>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
                        (char*)out, N, C, scale);
     return check_launch("tcx_attention_split");
 }
@@ -317,8 +321,9 @@ int attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads,
     if (Bt == 0) return TCX_OK;
 #define TCX_ATT_D(D_)                                                                        \
     case D_:                                                                                 \
-        return bf ? launch_split<D_, true>(qkv, out, Bt, N, C, heads, st)                   \
-                  : launch_split<D_, false>(qkv, out, Bt, N, C, heads, st);
+        return bf == 2 ? launch_split<D_, 2>(qkv, out, Bt, N, C, heads, st)                 \
+             : bf ? launch_split<D_, 1>(qkv, out, Bt, N, C, heads, st)                      \
+                  : launch_split<D_, 0>(qkv, out, Bt, N, C, heads, st);
     switch (C / heads) {
         TCX_ATT_D(16)
         TCX_ATT_D(32)
@@ -338,4 +343,8 @@ extern "C" int tcx_attention_split(const void* qkv, void* out, int Bt, int N, in
 
 extern "C" int tcx_attention_split_bf16(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream) {
     return attention_split(qkv, out, Bt, N, C, heads, 1, (hipStream_t)stream);
+}
+
+extern "C" int tcx_attention_split_b2(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream) {
+    return attention_split(qkv, out, Bt, N, C, heads, 2, (hipStream_t)stream);
 }

@@ -629,9 +629,12 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
     p.gn = gn_stats;
     p.nsplit = cdiv(p.HoWo, BM);
     if (gn_stats) TCX_REQUIRE(p.HoWo % BM == 0, "tcx_conv2d_h2: fused GN stats need Ho*Wo %% 128 == 0");
+    TCX_REQUIRE(bf16 >= 0 && bf16 <= 2, "tcx_conv2d_h2: bf16 must be 0 (f16x3), 1 (bf16 records) or 2 (2-byte bf16)");
     const size_t bsrc = bmod > 0 ? (size_t)bmod : (size_t)Bt;
     const size_t lim = (size_t)1 << 31;
-    const size_t b1 = bsrc * H * W * C1 * 4, b2 = bsrc * H * W * C2 * 4, bw = (size_t)cout_pad * kpad * 4;
+    const size_t esz = bf16 == 2 ? 2 : 4;  // bytes per source element (the prologue's fp32 sources: 4)
+    const size_t b1 = bsrc * H * W * C1 * (pro_scale1 ? 4 : esz), b2 = bsrc * H * W * C2 * (pro_scale2 ? 4 : esz),
+                 bw = (size_t)cout_pad * kpad * 4;
     TCX_REQUIRE(b1 < lim && b2 < lim && bw < lim, "tcx_conv2d_h2: operands must be < 2 GiB (32-bit buffer offsets)");
     p.bytes1 = (unsigned)b1; p.bytes2 = (unsigned)b2; p.bytesw = (unsigned)bw;
     p.wscale = wscale; p.out_h2 = out_h2; p.ovf = ovf;
@@ -639,7 +642,17 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
                 "tcx_conv2d_h2: prologue tables come in scale/shift pairs per source");
     p.sc1 = pro_scale1; p.sh1 = pro_shift1; p.sc2 = pro_scale2; p.sh2 = pro_shift2;
     p.wf = wfrag;
-    p.bf = bf16 != 0;  // k_conv3p / k_conv3h have no bf16 form: those shapes take the im2col kernel
+    p.bf = bf16;  // k_conv3p / k_conv3h have no bf16 form: those shapes take the im2col kernel
+    if (bf16 == 2) {
+        // 2-byte bf16 tensors (config 5 at 256^2): only the LDS-DMA kernels read them
+        TCX_REQUIRE(!pro_scale1 && !pro_scale2, "tcx_conv2d_h2: 2-byte bf16 sources take no prologue");
+        ConvParams q = p;
+        q.n_nblk = cout_pad / 96;
+        const bool ok = (conv3g_applies(p, cout_pad) && conv3lb_takes(q)) || conv4s2g_applies(p, cout_pad) ||
+                        lin1x1_applies(p, cout_pad);
+        TCX_REQUIRE(ok, "tcx_conv2d_h2: 2-byte bf16 operands need k_conv3lb (3x3, rows of 64/128/256 px), "
+                        "k_conv4s2g (4x4/s2) or k_lin1x1 (1x1) shapes");
+    }
     if (conv3g_applies(p, cout_pad)) return launch_conv3g(p, cout_pad, (hipStream_t)stream);
     TCX_REQUIRE(!pro_scale1 && !pro_scale2,
                 "tcx_conv2d_h2: the GroupNorm+SiLU prologue needs k_conv3g: the fragment-ordered weights "

@@ -91,7 +91,10 @@ __global__ __launch_bounds__(64 * B_NW, 2) void k_conv3lb(ConvParams p) {
     // piece l & 1, which holds logical piece (l & 1) ^ sw(col) = the hi 16 B of 8-channel group g at
     // byte 32 g of the chunk's record
     const int hw = wv & 1;
-    const int rowb = p.C1 * 4;
+    // b2 sources (p.bf == 2, h2.hpp): the 2-byte bf16 rows hold exactly the hi pieces, so every byte
+    // offset (pixel stride, piece, chunk) is half the record's
+    const int esz = p.bf == 2 ? 2 : 4;
+    const int rowb = p.C1 * esz;
     const int img0 = bs * H;
     const int ls = lane >> 1;
     auto halo_voff = [&](int i) {
@@ -106,12 +109,12 @@ __global__ __launch_bounds__(64 * B_NW, 2) void k_conv3lb(ConvParams p) {
         if (sl >= NPX) hc = (NPX - 1) % W2;  // padding slots read a valid pixel
         const int x = hc == 0 ? W - 1 : (hc == W + 1 ? 0 : hc - 1);
         const int yo = (sl >= NPX) ? (img0 + wrap_idx(r0 + (NPX - 1) / W2 - 1, H)) * W * rowb : (nx ? yo1 : yo0);
-        return yo + x * rowb + 32 * ((lane & 1) ^ sw(hcs));
+        return yo + x * rowb + 8 * esz * ((lane & 1) ^ sw(hcs));
     };
     auto halo_issue = [&](int j, int buf, int q0, int q1) {
         const int ci0 = j * B_KC;
         const bool s1 = ci0 < p.C1;
-        const int cc = (s1 ? ci0 : ci0 - p.C1) * 4;
+        const int cc = (s1 ? ci0 : ci0 - p.C1) * esz;
         const __amdgpu_buffer_rsrc_t rs = s1 ? r1 : r2;
 #pragma unroll
         for (int q = 0; q < NIH; ++q) {

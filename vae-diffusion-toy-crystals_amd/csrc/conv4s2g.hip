@@ -35,8 +35,13 @@ constexpr int Q_TP = 128;                       // output pixels per tile
 constexpr int Q_PAIR = 2 * 3 * 2 * 1024;        // B fragments of two k-steps (12 KB)
 __host__ __device__ constexpr int q_rs(int Wo) { return 2 * Wo + 4; }  // both parities (Wo + 1 each) + 2 pad
 __host__ __device__ constexpr int q_npx(int Wo) { return (2 * (Q_TP / Wo) + 2) * q_rs(Wo); }
-__host__ __device__ constexpr int q_ni(int Wo) { return (q_npx(Wo) + 31) / 32; }  // 1-KB DMA per chunk
-constexpr size_t conv4s2g_lds_bytes(int Wo) { return (size_t)2 * q_ni(Wo) * 1024 + 2 * (size_t)Q_PAIR; }
+// SLIM (2-byte bf16 sources, h2.hpp "b2"): a slot is the 16-B hi piece of the 8-channel chunk only, 64
+// slots per 1-KB DMA instruction, consecutive and unswizzled (a ds_read_b128 lane group reads 16
+// consecutive 16-B slots of one parity row: every bank once); config 5's ds1 (Wo = 128) fits only so
+__host__ __device__ constexpr int q_ni(int Wo, bool SLIM = false) { return (q_npx(Wo) + (SLIM ? 63 : 31)) / (SLIM ? 64 : 32); }
+constexpr size_t conv4s2g_lds_bytes(int Wo, bool SLIM = false) {
+    return (size_t)2 * q_ni(Wo, SLIM) * 1024 + 2 * (size_t)Q_PAIR;
+}
 constexpr int Q_WAIT_VM0 = 0x0F70;
 constexpr int Q_WAIT_LGKM0 = 0xC07F;
 
@@ -44,13 +49,14 @@ __device__ __forceinline__ void q_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
 
-template <int Wo, bool BF>
+template <int Wo, bool BF, bool SLIM = false>
 __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
+    static_assert(!SLIM || BF, "the slim slot holds the bf16 hi piece only");
     constexpr int NT = 3;
     constexpr int TR = Q_TP / Wo;        // output rows per tile
     constexpr int RS = q_rs(Wo);         // halo slots per halo row (both column parities + 2 pad)
     constexpr int NPX = q_npx(Wo);
-    constexpr int NI = q_ni(Wo);
+    constexpr int NI = q_ni(Wo, SLIM);
     constexpr int NIH = (NI + 1) / 2;    // halo DMA instructions per halo wave
     constexpr int HB = NI * 1024;
     constexpr int RING = 2 * HB;
@@ -82,23 +88,26 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
     // ---- halo DMA (waves 2-3: instruction i = 2 q + (wv & 1)); lane l -> slot 32 i + l / 2, physical
     // piece l & 1, logical piece (l & 1) ^ swz(slot); slots past the halo re-read its last pixel
     const int hw = wv & 1;
-    const int rowb = p.C1 * 4;
+    // b2 sources (BF, p.bf == 2, h2.hpp): the 8-channel chunk is ONE 16-B hi piece at byte 16 j of the
+    // pixel's 2-byte row; both DMA lanes of a slot read it (the lo slot half is never read by BF)
+    const bool b2 = BF && p.bf == 2;
+    const int rowb = p.C1 * (b2 ? 2 : 4);
     auto halo_voff = [&](int i) {
-        int s = 32 * i + (lane >> 1);
+        int s = SLIM ? 64 * i + lane : 32 * i + (lane >> 1);
         s = s < NPX ? s : NPX - 1;
         const int hr = s / RS, hc = s - (s / RS) * RS;
-        const int swz = (hr & 1) ^ ((hc >> 3) & 1);
+        const int swz = SLIM ? 0 : (hr & 1) ^ ((hc >> 3) & 1);
         const int par = hc >= Wo + 1 ? 1 : 0;
         const int cc = min(hc - par * (Wo + 1), Wo);  // the 2 pad slots re-read column Wo
         const int y = wrap_idx(2 * r0 - 1 + hr, H), x = wrap_idx(2 * cc + par - 1, W);
-        return ((bs * H + y) * W + x) * rowb + 16 * ((lane & 1) ^ swz);
+        return ((bs * H + y) * W + x) * rowb + (b2 ? 0 : 16 * ((lane & 1) ^ swz));
     };
     auto halo_issue = [&](int j, int buf, int q0, int q1) {
 #pragma unroll
         for (int q = 0; q < NIH; ++q) {
             if (q < q0 || q >= q1) continue;
             const int i = 2 * q + hw;
-            if (i < NI) q_dma16(r1, smd + buf * HB + i * 1024, halo_voff(i), 32 * j);
+            if (i < NI) q_dma16(r1, smd + buf * HB + i * 1024, halo_voff(i), (b2 ? 16 : 32) * j);
         }
     };
     // ---- weight pairs (waves 0-1): pair k = k-steps 2k, 2k + 1 -> ring slot k & 1; wave w moves KB [6 w, 6 w + 6)
@@ -126,8 +135,8 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
     auto rd_a = [&](int set, int kc, int hb) {  // k-step kc = 2 dy + p of the chunk in halo buffer hb
         const int s = abase + (kc >> 1) * RS + (kc & 1);
         const int sw = ((kc >> 1) & 1) ^ ((kc & 1) ? asw1 : asw0);
-        const char* A = smc + hb * HB + s * 32;
-        a_h[set] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(A + 16 * sw));
+        const char* A = smc + hb * HB + s * (SLIM ? 16 : 32);
+        a_h[set] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(A + (SLIM ? 0 : 16 * sw)));
         if constexpr (!BF) a_l[set] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(A + 16 * (sw ^ 1)));
     };
     const int bl = lane * 16;
@@ -254,19 +263,37 @@ __global__ void k_pack_frag4(const char* __restrict__ wh, char* __restrict__ wf,
 
 template <int Wo>
 int launch_q(const ConvParams& p, hipStream_t st) {
-    constexpr size_t shm = conv4s2g_lds_bytes(Wo);
-    static bool attr[2] = {false, false};
-    auto kc = p.bf ? &k_conv4s2g<Wo, true> : &k_conv4s2g<Wo, false>;
-    if (!attr[p.bf ? 1 : 0]) {
+    const int ai = p.bf == 2 ? 2 : p.bf ? 1 : 0;  // b2 sources take the slim slots
+    const size_t shm = conv4s2g_lds_bytes(Wo, ai == 2);
+    static bool attr[3] = {false, false, false};
+    auto kc = ai == 2 ? &k_conv4s2g<Wo, true, true> : ai == 1 ? &k_conv4s2g<Wo, true> : &k_conv4s2g<Wo, false>;
+    if (!attr[ai]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)shm) != hipSuccess) {
             set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", shm);
             return TCX_EHIP;
         }
-        attr[p.bf ? 1 : 0] = true;
+        attr[ai] = true;
     }
     hipLaunchKernelGGL(kc, dim3((p.M / Q_TP) * p.n_nblk), dim3(256), shm, st, p);
     return check_launch("tcx_conv2d_h2(4x4/s2 lds-dma)");
+}
+// Wo = 128 (config 5's ds1): the slim b2 form only (the 32-B slots would not leave two workgroups per CU)
+int launch_q128(const ConvParams& p, hipStream_t st) {
+    constexpr size_t shm = conv4s2g_lds_bytes(128, true);
+    static_assert(shm <= 80 * 1024, "two workgroups per CU");
+    static bool attr = false;
+    auto kc = &k_conv4s2g<128, true, true>;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)shm) != hipSuccess) {
+            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", shm);
+            return TCX_EHIP;
+        }
+        attr = true;
+    }
+    hipLaunchKernelGGL(kc, dim3((p.M / Q_TP) * p.n_nblk), dim3(256), shm, st, p);
+    return check_launch("tcx_conv2d_h2(4x4/s2 lds-dma, Wo 128)");
 }
 
 }  // namespace
@@ -274,7 +301,8 @@ int launch_q(const ConvParams& p, hipStream_t st) {
 // Host dispatch (conv.hip): the fragment-ordered 4x4 weights exist and the shape is the U-Net's
 bool conv4s2g_applies(const ConvParams& p, int cout_pad) {
     return p.wf != nullptr && p.ks == 4 && p.stride == 2 && p.pad_y == 1 && p.pad_x == 1 && p.circular &&
-           p.Hi == p.H && p.Wi == p.W && (p.Wo == 16 || p.Wo == 32 || p.Wo == 64) && p.H == 2 * p.Ho &&
+           p.Hi == p.H && p.Wi == p.W && (p.Wo == 16 || p.Wo == 32 || p.Wo == 64 || (p.Wo == 128 && p.bf == 2)) &&
+           p.H == 2 * p.Ho &&
            p.W == 2 * p.Wo && p.HoWo % Q_TP == 0 && cout_pad % 96 == 0 && p.Cin % 8 == 0 && p.C2 == 0 &&
            p.x2 == nullptr && p.kpad == 16 * p.Cin && p.osy == 1 && p.osx == 1 && p.sc1 == nullptr;
 }
@@ -286,7 +314,8 @@ int launch_conv4s2g(ConvParams& p, int cout_pad, hipStream_t st) {
     int rc;
     if (p.Wo == 32) rc = launch_q<32>(p, st);
     else if (p.Wo == 16) rc = launch_q<16>(p, st);
-    else rc = launch_q<64>(p, st);
+    else if (p.Wo == 64) rc = launch_q<64>(p, st);
+    else rc = launch_q128(p, st);
     prof_end(st, 2.0 * (double)p.M * p.Cout * 16 * p.Cin);
     return rc;
 }

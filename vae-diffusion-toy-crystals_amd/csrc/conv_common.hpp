@@ -51,6 +51,8 @@ bool conv3g_applies(const ConvParams& p, int cout_pad);
 // can take the GroupNorm+SiLU prologue of tcx_conv2d_h2_pro)
 bool conv3g_covers(int H, int W, int Cin, int cout_pad, bool bf = false);
 int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st);
+// bf16 LDS-DMA 3x3 kernel (conv3lb.hip): config 5's rows of 64 / 128 / 256 px.
+bool conv3lb_takes(const ConvParams& p);
 // 1x1 split GEMM (lin1x1.hip): the attention block's qkv / proj convs.
 bool lin1x1_applies(const ConvParams& p, int cout_pad);
 int launch_lin1x1(ConvParams& p, int cout_pad, hipStream_t st);
@@ -186,7 +188,8 @@ __device__ __forceinline__ void conv_epi_store_cols(const ConvParams& p, f32x16 
     // accumulator row r of a lane is output pixel pix0 + (r & 3) + 8 (r >> 2): a per-lane byte
     // offset (VGPR) plus a wave-uniform row offset (SGPR soffset)
     const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, (unsigned)((long long)p.M * p.Cout * 4));
-    const int rowb = p.Cout * 4;
+    const bool b2 = p.out_h2 && p.bf == 2;  // 2-byte bf16 output (h2.hpp "b2")
+    const int rowb = p.Cout * (b2 ? 2 : 4);
     const f32x2 wsc2 = {wsc, wsc};
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -198,8 +201,9 @@ __device__ __forceinline__ void conv_epi_store_cols(const ConvParams& p, f32x16 
             // fp32: the element; h2: the lane's dword of its 8-channel group record (even lane the
             // hi pair, odd lane the lo pair)
             const bool odd = (li & 1) != 0;
-            const int vo = p.out_h2 ? pix0 * rowb + (co & ~7) * 4 + (odd ? 16 : 0) + 2 * ((co & 7) & ~1)
-                                    : (pix0 * p.Cout + co) * 4;
+            const int vo = b2 ? (pix0 * p.Cout + co) * 2
+                              : p.out_h2 ? pix0 * rowb + (co & ~7) * 4 + (odd ? 16 : 0) + 2 * ((co & 7) & ~1)
+                                         : (pix0 * p.Cout + co) * 4;
             f32x2 add[8];
             if (p.resid) {  // attention proj only: the 16 residuals of this block before its stores
 #pragma unroll
@@ -224,7 +228,9 @@ __device__ __forceinline__ void conv_epi_store_cols(const ConvParams& p, f32x16 
                     else if (p.act == 3) v = silu_f(v);
                     v2[e] = v;
                     const int so = ((r & 3) + 8 * (r >> 2)) * rowb;
-                    if (p.out_h2) {
+                    if (b2) {
+                        __builtin_amdgcn_raw_buffer_store_b16(bf16_bits((__bf16)v), ry, vo, so, 0);
+                    } else if (p.out_h2) {
                         // lane pairs (2j, 2j+1) of an 8-channel group swap halves
                         const unsigned sp = split1x(v, bf);
                         const unsigned oth = (unsigned)__shfl_xor((int)(odd ? (sp & 0xffffu) : (sp >> 16)), 1);
@@ -271,7 +277,8 @@ __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 
 #pragma unroll
     for (int n = 0; n < NT; ++n) bco[n] = p.bias ? p.bias[n0 + n * 32 + li] : 0.f;
     const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, (unsigned)((long long)p.M * p.Cout * 4));
-    const int rowb = p.Cout * 4;
+    const bool b2 = p.out_h2 && p.bf == 2;  // 2-byte bf16 output (h2.hpp "b2"): one 8-B store per lane and group
+    const int rowb = p.Cout * (b2 ? 2 : 4);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
         const int wv = wv0 + rt;
@@ -300,10 +307,13 @@ __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 
                 }
                 quad_transpose4(v, qi);
                 const int so = 8 * j * rowb;
-                if (p.out_h2) {
+                typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
+                if (b2) {
+                    const u32x2_ w2 = {pack2_bf(v[0], v[1]), pack2_bf(v[2], v[3])};
+                    __builtin_amdgcn_raw_buffer_store_b64(w2, ry, (pixq * p.Cout + c4) * 2, so, 0);
+                } else if (p.out_h2) {
                     const unsigned a0 = split1x(v[0], bf), a1 = split1x(v[1], bf), a2 = split1x(v[2], bf),
                                    a3 = split1x(v[3], bf);
-                    typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
                     const u32x2_ hi = {(a0 & 0xffffu) | (a1 << 16), (a2 & 0xffffu) | (a3 << 16)};
                     const u32x2_ lo = {(a0 >> 16) | (a1 & 0xffff0000u), (a2 >> 16) | (a3 & 0xffff0000u)};
                     __builtin_amdgcn_raw_buffer_store_b64(hi, ry, voh, so, 0);
@@ -397,7 +407,9 @@ __device__ __forceinline__ void conv_epi_store_general(const ConvParams& p, f32x
             if (p.act == 1) v = fmaxf(v, 0.f);
             else if (p.act == 2) v = 1.f / (1.f + expf(-v));
             else if (p.act == 3) v = silu_f(v);
-            if (p.out_h2) {
+            if (p.out_h2 && p.bf == 2) {  // 2-byte bf16 output (h2.hpp "b2")
+                if (ok[r]) *reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(p.y) + oidx[r] * 2) = bf16_bits((__bf16)v);
+            } else if (p.out_h2) {
                 // h2 record of the pixel: lane pairs (2j, 2j+1) of an 8-channel group swap halves so
                 // the even lane stores the hi pair and the odd lane the lo pair (one dword each)
                 const unsigned sp = split1x(v, bf);

@@ -74,6 +74,20 @@ __device__ __forceinline__ void store4_h2x(char* base, size_t pix, int q, const 
     *reinterpret_cast<uint2*>(g + 16) = lo;
 }
 
+// "b2": config 5's 2-byte bf16 tensors (bf = 2 in the conv / writer flags): plain NHWC bf16 (round to
+// nearest even), i.e. only the hi halves of the bf16 records above.  A bf16 product never reads the lo
+// halves, so every record reader's byte offset of a hi piece is halved: pixel p, 8-channel group g at
+// p C 2 + 16 g (records: p C 4 + 32 g).
+__device__ __forceinline__ unsigned pack2_bf(float a, float b) {
+    return (unsigned)bf16_bits((__bf16)a) | ((unsigned)bf16_bits((__bf16)b) << 16);
+}
+// channels [4q, 4q+4) of the pixel whose b2 row starts at element `pix_elem` (= pixel * C)
+__device__ __forceinline__ void store4_b2(char* base, size_t pix_elem, int q, const float4 v) {
+    *reinterpret_cast<uint2*>(base + (pix_elem + 4 * (size_t)q) * 2) = make_uint2(pack2_bf(v.x, v.y), pack2_bf(v.z, v.w));
+}
+__device__ __forceinline__ float bf_lo(unsigned w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+
 __device__ __forceinline__ bool h2_bad(float v) { return !(fabsf(v) < kH2Max); }
 
 // Store channels [4q, 4q+4) of one pixel whose h2 record starts at byte `pix` (= pixel * C * 4).

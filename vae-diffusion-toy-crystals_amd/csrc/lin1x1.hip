@@ -52,10 +52,15 @@ __global__ __launch_bounds__(256, 2) void k_lin1x1(ConvParams p) {
     // DMA plan: A instructions 4 wv .. 4 wv + 3 (8 rows each), B instructions 3 wv .. 3 wv + 2
     const int lr = lane >> 3, lp = lane & 7;
     int aoff[4], boff[3];
+    // b2 source (BF, p.bf == 2, h2.hpp): a 32-channel chunk is 64 B of hi halves; lane lp of a row
+    // fills physical piece lp with logical piece L = lp ^ swizzle, whose hi data (L even) sits at 16 (L / 2)
+    // (an odd L, a lo piece, is never read by BF: it gets the same bytes)
+    const bool b2 = BF && p.bf == 2;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int r = 8 * (4 * wv + q) + lr;
-        aoff[q] = (m0 + r) * p.Cin * 4 + 16 * (lp ^ ((r >> 1) & 7));
+        const int L = lp ^ ((r >> 1) & 7);
+        aoff[q] = b2 ? (m0 + r) * p.Cin * 2 + 16 * (L >> 1) : (m0 + r) * p.Cin * 4 + 16 * L;
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -65,7 +70,7 @@ __global__ __launch_bounds__(256, 2) void k_lin1x1(ConvParams p) {
     auto issue = [&](int c, int buf) {
         char* const d = smd + buf * X_STAGE;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x_dma16(ra, d + (4 * wv + q) * 1024, aoff[q], c * 128);
+        for (int q = 0; q < 4; ++q) x_dma16(ra, d + (4 * wv + q) * 1024, aoff[q], c * (b2 ? 64 : 128));
 #pragma unroll
         for (int q = 0; q < 3; ++q) x_dma16(rw, d + X_ABYTES + (3 * wv + q) * 1024, boff[q], c * 128);
     };

@@ -339,9 +339,13 @@ __global__ __launch_bounds__(256) void k_upsample2x_g8(const float* __restrict__
                 split4x(make_float4(o[0], o[1], o[2], o[3]), hi[h], lo[h], bf != 0);
             }
             const size_t pix = ((size_t)b * 2 * H + oy) * 2 * W + ox;
-            char* gp = y + pix * C * 4 + 32 * (size_t)g;
-            *reinterpret_cast<uint4*>(gp) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
-            *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo[0].x, lo[0].y, lo[1].x, lo[1].y);
+            if (bf == 2) {  // 2-byte bf16 (h2.hpp "b2"): the hi halves only
+                *reinterpret_cast<uint4*>(y + (pix * C + 8 * (size_t)g) * 2) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
+            } else {
+                char* gp = y + pix * C * 4 + 32 * (size_t)g;
+                *reinterpret_cast<uint4*>(gp) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
+                *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo[0].x, lo[0].y, lo[1].x, lo[1].y);
+            }
         }
     }
     h2_flag(ovf, bad && !bf);
@@ -433,7 +437,11 @@ __global__ __launch_bounds__(256, 2) void k_upsample2x_band(const float* __restr
             }
             split4x(make_float4(o[0], o[1], o[2], o[3]), hi[h], lo[h], bf != 0);
         }
-        if constexpr (G8) {
+        if (bf == 2) {  // 2-byte bf16 (h2.hpp "b2"): the hi halves only
+            char* gp = y + (pix * C + (size_t)CW * q) * 2;
+            if constexpr (G8) *reinterpret_cast<uint4*>(gp) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
+            else *reinterpret_cast<uint2*>(gp) = hi[0];
+        } else if constexpr (G8) {
             char* gp = y + pix * C * 4 + 32 * (size_t)q;
             *reinterpret_cast<uint4*>(gp) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
             *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo[0].x, lo[0].y, lo[1].x, lo[1].y);
@@ -533,11 +541,89 @@ __global__ __launch_bounds__(256, 2) void k_upsample2x_bandseg(const float* __re
             }
             split4x(make_float4(o[0], o[1], o[2], o[3]), hi[h], lo[h], bf != 0);
         }
-        char* gp = y + pix * C * 4 + 32 * (size_t)q;
-        *reinterpret_cast<uint4*>(gp) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
-        *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo[0].x, lo[0].y, lo[1].x, lo[1].y);
+        if (bf == 2) {  // 2-byte bf16 (h2.hpp "b2"): the hi halves only
+            *reinterpret_cast<uint4*>(y + (pix * C + 8 * (size_t)q) * 2) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
+        } else {
+            char* gp = y + pix * C * 4 + 32 * (size_t)q;
+            *reinterpret_cast<uint4*>(gp) = make_uint4(hi[0].x, hi[0].y, hi[1].x, hi[1].y);
+            *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo[0].x, lo[0].y, lo[1].x, lo[1].y);
+        }
     }
     h2_flag(ovf, bad && !bf);
+}
+
+// GroupNorm (+ SiLU) apply from tables into 2-byte bf16 (h2.hpp "b2", config 5): one thread per (pixel,
+// 8-channel group), the source fp32 (32 B) or itself b2 (16 B, in place: the conv wrote its pre-norm
+// output as bf16), the result 16 B of bf16.  Loads of a batch of GU groups before any store, the next
+// batch's loads before this batch's stores (k_gn_apply_tab_h2's order).
+template <bool IN_B2>
+__global__ __launch_bounds__(256) void k_gn_apply_b2(const char* x, char* y, int HW, int C,
+                                                     const float* __restrict__ tsc, const float* __restrict__ tsh,
+                                                     int silu, int ppb) {
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    float* sc = lsm;
+    float* sh = lsm + ((C + 3) & ~3);
+    const int b = blockIdx.y;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        sc[c] = tsc[(size_t)b * C + c];
+        sh[c] = tsh[(size_t)b * C + c];
+    }
+    __syncthreads();
+    const int p0 = blockIdx.x * ppb;
+    const int p1 = min(HW, p0 + ppb);
+    const size_t base = ((size_t)b * HW + p0) * C;  // element index of the block's first value
+    const int C8 = C / 8;
+    const int n8 = (p1 - p0) * C8;
+    constexpr int GU = 4;
+    uint4 n0[GU], n1[GU];
+    auto ld = [&](int at, int k) {
+        const size_t e = base + (size_t)(at + 256 * k) * 8;
+        if constexpr (IN_B2) {
+            n0[k] = *reinterpret_cast<const uint4*>(x + e * 2);
+        } else {
+            n0[k] = *reinterpret_cast<const uint4*>(x + e * 4);
+            n1[k] = *reinterpret_cast<const uint4*>(x + e * 4 + 16);
+        }
+    };
+    auto work = [&](int at, const uint4& a, const uint4& c) {
+        float v[8];
+        if constexpr (IN_B2) {
+            v[0] = bf_lo(a.x); v[1] = bf_hi(a.x); v[2] = bf_lo(a.y); v[3] = bf_hi(a.y);
+            v[4] = bf_lo(a.z); v[5] = bf_hi(a.z); v[6] = bf_lo(a.w); v[7] = bf_hi(a.w);
+        } else {
+            v[0] = __uint_as_float(a.x); v[1] = __uint_as_float(a.y); v[2] = __uint_as_float(a.z); v[3] = __uint_as_float(a.w);
+            v[4] = __uint_as_float(c.x); v[5] = __uint_as_float(c.y); v[6] = __uint_as_float(c.z); v[7] = __uint_as_float(c.w);
+        }
+        const int c0 = (at % C8) * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            v[e] = fmaf(v[e], sc[c0 + e], sh[c0 + e]);
+            if (silu) v[e] = silu_hw(v[e]);
+        }
+        *reinterpret_cast<uint4*>(y + (base + (size_t)at * 8) * 2) =
+            make_uint4(pack2_bf(v[0], v[1]), pack2_bf(v[2], v[3]), pack2_bf(v[4], v[5]), pack2_bf(v[6], v[7]));
+    };
+    int i = threadIdx.x;
+    if (i + (GU - 1) * 256 < n8)
+#pragma unroll
+        for (int k = 0; k < GU; ++k) ld(i, k);
+    for (; i + (GU - 1) * 256 < n8; i += GU * 256) {
+        uint4 u0[GU], u1[GU];
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+            u0[k] = n0[k];
+            u1[k] = n1[k];
+        }
+        if (i + GU * 256 + (GU - 1) * 256 < n8)
+#pragma unroll
+            for (int k = 0; k < GU; ++k) ld(i + GU * 256, k);
+#pragma unroll
+        for (int k = 0; k < GU; ++k) work(i + 256 * k, u0[k], u1[k]);
+    }
+    for (; i < n8; i += 256) {
+        ld(i, 0);
+        work(i, n0[0], n1[0]);
+    }
 }
 
 // LayerNorm over rows of width Wd (+ optional FiLM h*(1+gamma)+beta), one wave per row.
@@ -922,9 +1008,28 @@ int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float*
     const int ppb = std::max(1, 32768 / C);
     const dim3 grid(cdiv(HW, ppb), Bt);
     const size_t shm = (size_t)2 * ((C + 3) & ~3) * sizeof(float);
+    if (bf == 2) {  // fp32 source -> 2-byte bf16 (x == y is not allowed: different sizes)
+        TCX_REQUIRE((const void*)x != y, "tcx_gn_apply_tab_h2: an fp32 -> 2-byte apply cannot run in place");
+        hipLaunchKernelGGL(k_gn_apply_b2<false>, grid, dim3(256), shm, st, (const char*)x, (char*)y, HW, C, scale, shift,
+                           silu, ppb);
+        return check_launch("tcx_gn_apply_tab_h2(b2)");
+    }
     hipLaunchKernelGGL(k_gn_apply_tab_h2, grid, dim3(256), shm, st, x, (char*)y, HW, C, scale, shift, silu, ppb, ovf,
                        bf);
     return check_launch("tcx_gn_apply_tab_h2");
+}
+
+// GroupNorm (+ SiLU) of a 2-byte bf16 tensor in place (config 5: the pre-norm conv outputs are bf16)
+int gn_apply_b2_inplace(void* x, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
+                        hipStream_t st) {
+    TCX_REQUIRE(x && scale && shift && C % 8 == 0 && aligned16(x), "tcx_gn_apply_b2: bad args");
+    if (Bt == 0) return TCX_OK;
+    const int ppb = std::max(1, 32768 / C);
+    const dim3 grid(cdiv(HW, ppb), Bt);
+    const size_t shm = (size_t)2 * ((C + 3) & ~3) * sizeof(float);
+    hipLaunchKernelGGL(k_gn_apply_b2<true>, grid, dim3(256), shm, st, (const char*)x, (char*)x, HW, C, scale, shift,
+                       silu, ppb);
+    return check_launch("tcx_gn_apply_b2");
 }
 }  // namespace tcx
 
@@ -946,6 +1051,20 @@ extern "C" int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int 
 extern "C" int tcx_gn_apply_tab_bf16(const float* x, void* y, int Bt, int HW, int C, const float* scale,
                                      const float* shift, int silu, void* stream) {
     return gn_apply_tab_h2(x, y, Bt, HW, C, scale, shift, silu, nullptr, 1, (hipStream_t)stream);
+}
+
+extern "C" int tcx_gn_apply_tab_b2(const void* x, void* y, int Bt, int HW, int C, const float* scale,
+                                   const float* shift, int silu, int in_b2, void* stream) {
+    if (in_b2) {
+        TCX_REQUIRE(x == y, "tcx_gn_apply_tab_b2: a 2-byte source is normalised in place");
+        return gn_apply_b2_inplace(y, Bt, HW, C, scale, shift, silu, (hipStream_t)stream);
+    }
+    return gn_apply_tab_h2(static_cast<const float*>(x), y, Bt, HW, C, scale, shift, silu, nullptr, 2, (hipStream_t)stream);
+}
+
+extern "C" int tcx_upsample2x_b2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
+                                 const float* shift, void* stream) {
+    return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, nullptr, 2, (hipStream_t)stream);
 }
 
 extern "C" int tcx_f32_to_h2(const float* x, void* y, size_t n, unsigned* ovf, void* stream) {

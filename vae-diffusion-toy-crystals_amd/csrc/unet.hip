@@ -23,6 +23,8 @@ int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const fl
                   unsigned* ovf, int bf, hipStream_t st);
 int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
                     unsigned* ovf, int bf, hipStream_t st);
+int gn_apply_b2_inplace(void* x, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
+                        hipStream_t st);
 int attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads, int bf, hipStream_t st);
 }
 
@@ -540,7 +542,17 @@ __global__ __launch_bounds__(256) void k_head(const float* __restrict__ h, int H
 // same order as k_head8 (bit-identical).
 constexpr int HR_PASS = 8;
 constexpr int HPR = 32 * HR_PASS;
-template <int Q>
+// B2: the source is 2-byte bf16 (config 5: up1_1's pre-norm output, h2.hpp "b2"): 8 B per 4 channels
+template <bool B2>
+__device__ __forceinline__ float4 head_ld4(const float* h, size_t e) {
+    if constexpr (B2) {
+        const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(h) + e * 2);
+        return make_float4(bf_lo(u.x), bf_hi(u.x), bf_lo(u.y), bf_hi(u.y));
+    } else {
+        return *reinterpret_cast<const float4*>(h + e);
+    }
+}
+template <int Q, bool B2 = false>
 __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int HW, const float* __restrict__ tsc,
                                                 const float* __restrict__ tsh, const float* __restrict__ w_out,
                                                 float* __restrict__ r) {
@@ -553,11 +565,11 @@ __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int
     const int c0 = sub * CL;
     float4 v[Q], vn[Q];  // passes 0 and 1 in flight before the constants are loaded
     {
-        const float* src = h + (size_t)(p0 + pl) * C + c0;
+        const size_t src = (size_t)(p0 + pl) * C + c0;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            v[q] = *reinterpret_cast<const float4*>(src + 4 * q);
-            vn[q] = *reinterpret_cast<const float4*>(src + 32 * C + 4 * q);
+            v[q] = head_ld4<B2>(h, src + 4 * q);
+            vn[q] = head_ld4<B2>(h, src + 32 * C + 4 * q);
         }
     }
     float wr[CL][9], scl[CL], shf[CL];
@@ -572,9 +584,9 @@ __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int
         const int pg = p0 + pass * 32 + pl;
         float4 vnn[Q];  // two passes ahead
         if (pass + 2 < HR_PASS) {
-            const float* src = h + (size_t)(pg + 64) * C + c0;
+            const size_t src = (size_t)(pg + 64) * C + c0;
 #pragma unroll
-            for (int q = 0; q < Q; ++q) vnn[q] = *reinterpret_cast<const float4*>(src + 4 * q);
+            for (int q = 0; q < Q; ++q) vnn[q] = head_ld4<B2>(h, src + 4 * q);
         }
         float acc[9];
 #pragma unroll
@@ -697,9 +709,13 @@ __global__ __launch_bounds__(256) void k_conv_first_rec(const float* __restrict_
         if (!bf)
             bad = bad || h2_bad(o0.x) || h2_bad(o0.y) || h2_bad(o0.z) || h2_bad(o0.w) || h2_bad(o1.x) ||
                   h2_bad(o1.y) || h2_bad(o1.z) || h2_bad(o1.w);
-        char* gp = dst + (size_t)pl * C0 * 4 + 32 * g;
-        *reinterpret_cast<uint4*>(gp) = make_uint4(hi0.x, hi0.y, hi1.x, hi1.y);
-        *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo0.x, lo0.y, lo1.x, lo1.y);
+        if (bf == 2) {  // 2-byte bf16 (h2.hpp "b2"): the hi halves only
+            *reinterpret_cast<uint4*>(y + (((size_t)b * HW + p) * C0 + 8 * g) * 2) = make_uint4(hi0.x, hi0.y, hi1.x, hi1.y);
+        } else {
+            char* gp = dst + (size_t)pl * C0 * 4 + 32 * g;
+            *reinterpret_cast<uint4*>(gp) = make_uint4(hi0.x, hi0.y, hi1.x, hi1.y);
+            *reinterpret_cast<uint4*>(gp + 16) = make_uint4(lo0.x, lo0.y, lo1.x, lo1.y);
+        }
     }
     h2_flag(ovf, bad);
 }
@@ -965,12 +981,13 @@ struct H2Ctx {
     bool on;
     unsigned* ovf;
     bool bf;  // precision 2: bf16 records, one bf16 MFMA per product (no range limit, no flag)
+    int fmt;  // conv / writer format flag: 0 h2, 1 bf16 records, 2 two-byte bf16 ("b2", h2.hpp: config 5)
 };
 
 int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2, int Bt, int bmod, int H, int W,
             int stride, int pad, const float* bias_b, const float* resid, float* y, double* gn, int* nsplit,
             hipStream_t st, const float* sc1 = nullptr, const float* sh1 = nullptr, const float* sc2 = nullptr,
-            const float* sh2 = nullptr, H2Ctx h2 = {false, nullptr, false}, int out_h2 = 0) {
+            const float* sh2 = nullptr, H2Ctx h2 = {false, nullptr, false, 0}, int out_h2 = 0) {
     const int Ho = (H + 2 * pad - cv.ks) / stride + 1, Wo = (W + 2 * pad - cv.ks) / stride + 1;
     const int HoWo = Ho * Wo;
     const bool fused = gn && HoWo % 128 == 0;
@@ -979,7 +996,7 @@ int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2
         TCX_REQUIRE(cv.wh && cv.wscale, "tcx_unet: split path needs packed h2 weights");
         TCX_TRY(tcx_conv2d_h2_pro(x1, x2, Bt, bmod, H, W, C1, C2, cv.wh, cv.whf, cv.wscale, cv.b, bias_b, resid, y, out_h2,
                                   cv.cout, cv.cout_pad, cv.kpad, cv.ks, stride, pad, 1, 0, fused ? gn : nullptr, sc1,
-                                  sh1, sc2, sh2, h2.bf ? 1 : 0, h2.ovf, st));
+                                  sh1, sc2, sh2, h2.fmt, h2.ovf, st));
     } else {
         TCX_TRY(tcx_conv2d(x1, x2, Bt, bmod, H, W, C1, C2, cv.w, cv.b, bias_b, resid, y, cv.cout, cv.cout_pad,
                            cv.kpad, cv.ks, stride, pad, 1, 0, 0, fused ? gn : nullptr, sc1, sh1, sc2, sh2, st));
@@ -1088,10 +1105,24 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // finalize the table of norm i, or normalise `y` in place when no prologue can consume it
     // split path: every conv source is h2 (h2.hpp) — GroupNorm applies feeding a conv write h2
     // in place, convs feeding only convs (ds1, ds2, us2, us1) write h2, the rest stay fp32
-    const H2Ctx h2{net->precision >= 1, net->h2_ovf, net->precision == 2};
+    // Config 5 (bf16 at 256^2): every conv there runs on an LDS-DMA kernel that reads 2-byte bf16 (k_conv3lb
+    // at 256 / 128 / 64-px rows, k_conv4s2g's slim slots at Wo 128 / 64, k_lin1x1, the split attention), so
+    // the tensors are 2-byte bf16 ("b2", h2.hpp) instead of 4-byte records whose lo halves a bf16 product never
+    // reads, and the pre-GroupNorm conv outputs are bf16 too (the GroupNorm statistics are taken on the fp32
+    // values in the conv epilogue; the apply pass normalises the stored bf16 in place, 2 B read + 2 B written
+    // per element).  fp32 stays where a consumer needs it: the attention input / residual (mid_1) and up2_1's
+    // output (the upsample applies its GroupNorm from fp32).  TCX_BF_B2=0 keeps the 4-byte records (A/B).
+    static const bool b2_on = [] {
+        const char* e = getenv("TCX_BF_B2");
+        return !(e && e[0] == '0');
+    }();
+    const int fmt = net->precision == 2 ? ((b2_on && W == 256 && H % 4 == 0 && C == 96) ? 2 : 1) : 0;
+    const H2Ctx h2{net->precision >= 1, net->h2_ovf, net->precision == 2, fmt};
+    const int pre_b2 = fmt == 2 ? 1 : 0;  // out_h2 of a conv whose output only a GroupNorm apply reads
     auto norm = [&](int i, float* y, int HW, int Cn, bool to_h2 = true) -> int {
         TCX_TRY(gn_tab(net, P, i, HW, Cn, gn, ns, st));
         if (pro[i]) return TCX_OK;
+        if (h2.on && to_h2 && fmt == 2) return gn_apply_b2_inplace(y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, st);
         if (h2.on && to_h2) return gn_apply_tab_h2(y, y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, h2.ovf, h2.bf, st);
         return tcx_gn_apply_tab(y, y, Bt, HW, Cn, P.sc(i), P.sh(i), 1, st);
     };
@@ -1124,7 +1155,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                     const size_t shr = ((size_t)12 * C + (size_t)nrow * W) * sizeof(float);
                     hipLaunchKernelGGL(k_conv_first_rec, dim3(H * W / FR_PX, Bt), dim3(256), shr, st, x, B, H, W, C,
                                        c0.w, c0.kpad, P.bias0, (char*)P.a64, ct, B, cfg, P.sc(0), P.sh(0), h2.ovf,
-                                       h2.bf ? 1 : 0);
+                                       fmt);
                 } else {
                     hipLaunchKernelGGL(k_conv_first<2>, dim3(H * W / FIRST_PX, Bt), dim3(256), shm, st, x, B, H, W,
                                        C, c0.w, c0.kpad, P.bias0, P.a64, nullptr, ct, B, cfg, P.sc(0), P.sh(0),
@@ -1152,24 +1183,24 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     }
     if (!first_fused) TCX_TRY(norm(0, P.a64, P.P0, C));
     TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.h1, gn, &ns, st,
-                    SC(0), SH(0), nullptr, nullptr, h2));
+                    SC(0), SH(0), nullptr, nullptr, h2, pre_b2));
     TCX_TRY(norm(1, P.h1, P.P0, C));  // h1 stays raw; its two consumers apply table 1
     // ds1: 4x4/s2 circular on silu(gn(h1))
     TCX_TRY(conv_gn(net->ds1, P.h1, nullptr, C, 0, Bt, 0, H, W, 2, 1, nullptr, nullptr, P.a32, nullptr, &ns, st,
                     SC(1), SH(1), nullptr, nullptr, h2, 1));
     // down2
     TCX_TRY(conv_gn(net->down2_0, P.a32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st,
-                    nullptr, nullptr, nullptr, nullptr, h2));
+                    nullptr, nullptr, nullptr, nullptr, h2, pre_b2));
     TCX_TRY(norm(2, P.b32, P.P1, C2));
     TCX_TRY(conv_gn(net->down2_1, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.h2, gn, &ns, st,
-                    SC(2), SH(2), nullptr, nullptr, h2));
+                    SC(2), SH(2), nullptr, nullptr, h2, pre_b2));
     TCX_TRY(norm(3, P.h2, P.P1, C2));  // h2 raw; consumers apply table 3
     // ds2
     TCX_TRY(conv_gn(net->ds2, P.h2, nullptr, C2, 0, Bt, 0, H1, W1, 2, 1, nullptr, nullptr, P.a16, nullptr, &ns, st,
                     SC(3), SH(3), nullptr, nullptr, h2, 1));
     // mid
     TCX_TRY(conv_gn(net->mid_0, P.a16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, nullptr, nullptr, P.b16, gn, &ns, st,
-                    nullptr, nullptr, nullptr, nullptr, h2));
+                    nullptr, nullptr, nullptr, nullptr, h2, pre_b2));
     TCX_TRY(norm(4, P.b16, P.P2, C2));
     TCX_TRY(conv_gn(net->mid_1, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, nullptr, nullptr, P.a16, gn, &ns, st,
                     SC(4), SH(4), nullptr, nullptr, h2));
@@ -1181,7 +1212,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         const int ns_a = std::max(1, P.P2 / 256);
         TCX_TRY(tcx_gn_partials(P.a16, Bt, P.P2, C2, ns_a, gn, st));
         TCX_TRY(gn_tab(net, P, 6, P.P2, C2, gn, ns_a, st));
-        if (h2.on) TCX_TRY(gn_apply_tab_h2(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, h2.ovf, h2.bf, st));
+        if (h2.on) TCX_TRY(gn_apply_tab_h2(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, h2.ovf, fmt, st));
         else TCX_TRY(tcx_gn_apply_tab(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, st));
         const tcx_conv& q = net->qkv;
         int dummy = 0;
@@ -1193,7 +1224,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         TCX_TRY(conv_gn(q, P.b16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 0, nullptr, nullptr, P.qkv, nullptr, &dummy, st,
                         nullptr, nullptr, nullptr, nullptr, h2, split_attn ? 1 : 0));
         TCX_REQUIRE(split_attn || !h2.bf, "tcx_unet: bf16 precision needs the split attention (N %% 256 == 0)");
-        if (split_attn) TCX_TRY(attention_split(P.qkv, P.b16, Bt, P.P2, C2, net->heads, h2.bf, st));
+        if (split_attn) TCX_TRY(attention_split(P.qkv, P.b16, Bt, P.P2, C2, net->heads, fmt, st));
         else if (h2.on) TCX_TRY(tcx_attention_h2(P.qkv, P.b16, Bt, P.P2, C2, net->heads, h2.ovf, st));
         else TCX_TRY(tcx_attention(P.qkv, P.b16, Bt, P.P2, C2, net->heads, st));
         const tcx_conv& pr = net->proj;
@@ -1203,13 +1234,13 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // us2: bilinear x2 (edge-clamped) into the free b32 buffer, then the circular 3x3 conv -> a32.
     // (The upsample-on-load conv variant re-reads 4 source taps per im2col element and measured
     // slower than this separate 250 MB pass.)
-    if (h2.on) TCX_TRY(upsample2x_h2(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, h2.ovf, h2.bf, st));
+    if (h2.on) TCX_TRY(upsample2x_h2(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, h2.ovf, fmt, st));
     else TCX_TRY(tcx_upsample2x(P.a16, P.b32, Bt, H2, W2, C2, nullptr, nullptr, st));
     TCX_TRY(conv_gn(net->us2, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, nullptr, &ns, st,
                     nullptr, nullptr, nullptr, nullptr, h2, 1));
     // up2 on cat[a32, silu(gn(h2))]
     TCX_TRY(conv_gn(net->up2_0, P.a32, P.h2, C2, C2, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st,
-                    nullptr, nullptr, SC(3), SH(3), h2));
+                    nullptr, nullptr, SC(3), SH(3), h2, pre_b2));
     TCX_TRY(norm(7, P.b32, P.P1, C));
     TCX_TRY(conv_gn(net->up2_1, P.b32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, gn, &ns, st,
                     SC(7), SH(7), nullptr, nullptr, h2));
@@ -1219,20 +1250,20 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // (r03_o, one lane, alternating: 72.7 vs 72.3 images/s against the separate apply pass)
     if (h2.on && upsample_fused_ok(H1, W1, C)) {
         TCX_TRY(gn_tab(net, P, 8, P.P1, C, gn, ns, st));
-        TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, P.sc(8), P.sh(8), h2.ovf, h2.bf, st));
+        TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, P.sc(8), P.sh(8), h2.ovf, fmt, st));
     } else {
         TCX_TRY(norm(8, P.a32, P.P1, C, false));
-        if (h2.on) TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, h2.ovf, h2.bf, st));
+        if (h2.on) TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, h2.ovf, fmt, st));
         else TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, st));
     }
     TCX_TRY(conv_gn(net->us1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, nullptr, &ns, st,
                     nullptr, nullptr, nullptr, nullptr, h2, 1));
     // up1 on cat[a64, silu(gn(h1))]
     TCX_TRY(conv_gn(net->up1_0, P.a64, P.h1, C, C, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.b64, gn, &ns, st, nullptr,
-                    nullptr, SC(1), SH(1), h2));
+                    nullptr, SC(1), SH(1), h2, pre_b2));
     TCX_TRY(norm(9, P.b64, P.P0, C));
     TCX_TRY(conv_gn(net->up1_1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, gn, &ns, st,
-                    SC(9), SH(9), nullptr, nullptr, h2));
+                    SC(9), SH(9), nullptr, nullptr, h2, pre_b2));  // b2: the head reads it as bf16
     // head: GN(up1.net.4)+SiLU fused with the out conv's channel reduction
     {
         TCX_TRY(gn_tab(net, P, 10, P.P0, C, gn, ns, st));
@@ -1240,7 +1271,9 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         // register-weight head (r03_ag: 124 -> 118 us at 64^2); k_head8 for other widths / shapes
         if (P.P0 % HPR == 0 && (C == 96 || C == 64 || C == 32)) {
             const dim3 gr(Bt * P.P0 / HPR);
-            if (C == 96) hipLaunchKernelGGL(k_head8r<3>, gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
+            if (C == 96 && fmt == 2)
+                hipLaunchKernelGGL((k_head8r<3, true>), gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
+            else if (C == 96) hipLaunchKernelGGL(k_head8r<3>, gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
             else if (C == 64) hipLaunchKernelGGL(k_head8r<2>, gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
             else hipLaunchKernelGGL(k_head8r<1>, gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
             TCX_TRY(check_launch("k_head8r"));
