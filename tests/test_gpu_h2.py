@@ -479,3 +479,45 @@ def test_conv_h2_16x16_kernel_bmod_act_out_h2_gn(H, Ci, Co):
     r = ref.reshape(4, Co, -1)
     np.testing.assert_allclose(s[..., 0], r.sum(-1), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(s[..., 1], (r * r).sum(-1), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,C1,Co,H,out_h2", [
+    (2, 96, 96, 64, False),   # up1_0's shape (64^2 rows, 96 + 96 -> 96), fp32 output + GroupNorm partials
+    (2, 96, 96, 32, False),   # 32^2 rows
+    (1, 192, 96, 32, False),  # up2_0's shape (192 + 192 -> 96)
+    (2, 96, 96, 64, True),    # h2 output
+])
+def test_quad_epilogue_equals_column_epilogue(B, C1, Co, H, out_h2):
+    """k_conv3lg (the concat with a GroupNorm+SiLU prologue on source 2) stores through the quad-transposed
+    epilogue (conv_epi_store_quad) without a residual and through the column epilogue
+    (conv_epi_store_cols) with one.  A zero residual makes the two compute the same values: the outputs
+    must be bit-equal, and the GroupNorm partials (summed per value in the quad form, as packed pairs in
+    the column form: a different fp32 order) equal to fp32 rounding of the 128-pixel sums."""
+    x1 = rng.standard_normal((B, C1, H, H))
+    x2 = rng.standard_normal((B, C1, H, H)) * 1.5
+    w = rng.standard_normal((Co, 2 * C1, 3, 3)) / np.sqrt(2 * C1 * 9)
+    b = rng.standard_normal(Co)
+    tabs = [dev(t) for t in rand_tabs(B, C1, 5)]
+    wh, ws, cpad, kpad = pack_h2(w)
+    wf = pack_frag(wh, cpad, kpad, 2 * C1)
+    x1d = to_h2(dev(nhwc(x1)))
+    x2d = dev(nhwc(x2))
+    zero = torch.zeros((B, H, H, Co), device="cuda")
+    bd = dev(b)
+    outs = []
+    for resid in (None, zero):
+        y = torch.full((B, H, H, Co), float("nan"), device="cuda")
+        gnd = None if out_h2 else torch.zeros((B, H * H // 128, Co, 2), dtype=torch.float64, device="cuda")
+        ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+        chk(L().tcx_conv2d_h2_pro(x1d.data_ptr(), x2d.data_ptr(), B, 0, H, H, C1, C1, wh.data_ptr(), wf.data_ptr(),
+                                  ws.data_ptr(), bd.data_ptr(), None, resid.data_ptr() if resid is not None else None,
+                                  y.data_ptr(), int(out_h2), Co, cpad, kpad, 3, 1, 1, 1, 0,
+                                  gnd.data_ptr() if gnd is not None else None, None, None, tabs[0].data_ptr(),
+                                  tabs[1].data_ptr(), 0, ovf.data_ptr(), st()))
+        torch.cuda.synchronize()
+        outs.append((y.cpu().numpy().view(np.uint32), None if gnd is None else gnd.cpu().numpy()))
+    (ya, ga), (yb, gb) = outs
+    assert np.array_equal(ya, yb), int(np.count_nonzero(ya != yb))
+    if ga is not None:
+        # 128 fp32 values per partial: the two orders agree to a few fp32 ulps of the sum of |values|
+        np.testing.assert_allclose(ga, gb, rtol=1e-5, atol=1e-4)

@@ -807,6 +807,119 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
     h2_flag(ovf, bad && !bf);
 }
 
+// The attention block's input side in one pass per image (round 5; sde_score_model.py:130-157 with the
+// mid block's last GroupNorm+SiLU): x = silu(GN_mid(a)) is written back in place as the fp32 residual,
+// the attn.norm statistics of x are summed (fp64) while x is still in registers, the attn.norm tables
+// are formed in the workgroup (gn_tables_from_csum, as tcx_gn_finalize), and GN_attn(x) is written as
+// h2 / bf16 records for the qkv conv.  Replaces k_gn_apply_tab + k_gn_partials + k_gn_finalize +
+// k_gn_apply_tab_h2 (4 launches, x read 3 times).  One workgroup of 1024 threads per image: thread
+// (row, group) holds the 8 channels of group tid % C8 at pixels row, row + R, ... (R = 1024 / C8 rows,
+// at most AP_NP pixels each).
+constexpr int AP_NP = 8;
+__global__ __launch_bounds__(1024) void k_attn_prep(float* __restrict__ a, char* __restrict__ y, int HW, int C,
+                                                    const float* __restrict__ tsc, const float* __restrict__ tsh,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    int groups, float eps, unsigned* ovf, int bf) {
+    extern __shared__ __attribute__((aligned(16))) double ap[];  // lsum[R][C] | csum[C][2] | gstat[groups][2]
+    const int C8 = C / 8, R = 1024 / C8;
+    double* lsum = ap;
+    double* csum = lsum + (size_t)R * C;
+    double* gstat = csum + 2 * C;
+    float* sc = reinterpret_cast<float*>(gstat + 2 * groups);
+    float* sh = sc + C;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int g8 = tid % C8, row = tid / C8;
+    const bool act = row < R;
+    const int c0 = 8 * g8;
+    float* ab = a + (size_t)b * HW * C;
+    float4 v0[AP_NP], v1[AP_NP];
+#pragma unroll
+    for (int k = 0; k < AP_NP; ++k) {
+        const int p = row + R * k;
+        if (act && p < HW) {
+            v0[k] = *reinterpret_cast<const float4*>(ab + (size_t)p * C + c0);
+            v1[k] = *reinterpret_cast<const float4*>(ab + (size_t)p * C + c0 + 4);
+        }
+    }
+    double s[8], ss[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = ss[e] = 0.0;
+    if (act) {
+        float scl[8], shf[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            scl[e] = tsc[(size_t)b * C + c0 + e];
+            shf[e] = tsh[(size_t)b * C + c0 + e];
+        }
+#pragma unroll
+        for (int k = 0; k < AP_NP; ++k) {
+            const int p = row + R * k;
+            if (p < HW) {
+                float4& u = v0[k];
+                float4& w = v1[k];
+                u.x = silu_f(fmaf(u.x, scl[0], shf[0])); u.y = silu_f(fmaf(u.y, scl[1], shf[1]));
+                u.z = silu_f(fmaf(u.z, scl[2], shf[2])); u.w = silu_f(fmaf(u.w, scl[3], shf[3]));
+                w.x = silu_f(fmaf(w.x, scl[4], shf[4])); w.y = silu_f(fmaf(w.y, scl[5], shf[5]));
+                w.z = silu_f(fmaf(w.z, scl[6], shf[6])); w.w = silu_f(fmaf(w.w, scl[7], shf[7]));
+                *reinterpret_cast<float4*>(ab + (size_t)p * C + c0) = u;
+                *reinterpret_cast<float4*>(ab + (size_t)p * C + c0 + 4) = w;
+                const float e8[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    s[e] += (double)e8[e];
+                    ss[e] += (double)e8[e] * (double)e8[e];
+                }
+            }
+        }
+    }
+    // channel totals: the R rows of each channel summed in row order, sums then squares
+    for (int pass = 0; pass < 2; ++pass) {
+        if (act) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) lsum[(size_t)row * C + c0 + e] = pass ? ss[e] : s[e];
+        }
+        __syncthreads();
+        for (int c = tid; c < C; c += 1024) {
+            double t = 0.0;
+            for (int r = 0; r < R; ++r) t += lsum[(size_t)r * C + c];
+            csum[2 * c + pass] = t;
+        }
+        __syncthreads();
+    }
+    gn_tables_from_csum(C, groups, HW, gamma, beta, eps, sc, sh, gstat, csum);
+    bool bad = false;
+    if (act) {
+        float scl[8], shf[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            scl[e] = sc[c0 + e];
+            shf[e] = sh[c0 + e];
+        }
+        char* yb = y + (size_t)b * HW * C * 4;
+#pragma unroll
+        for (int k = 0; k < AP_NP; ++k) {
+            const int p = row + R * k;
+            if (p < HW) {
+                float4 u = v0[k], w = v1[k];
+                u.x = fmaf(u.x, scl[0], shf[0]); u.y = fmaf(u.y, scl[1], shf[1]);
+                u.z = fmaf(u.z, scl[2], shf[2]); u.w = fmaf(u.w, scl[3], shf[3]);
+                w.x = fmaf(w.x, scl[4], shf[4]); w.y = fmaf(w.y, scl[5], shf[5]);
+                w.z = fmaf(w.z, scl[6], shf[6]); w.w = fmaf(w.w, scl[7], shf[7]);
+                uint2 h0, l0, h1, l1;
+                split4x(u, h0, l0, bf != 0);
+                split4x(w, h1, l1, bf != 0);
+                char* g = yb + ((size_t)p * C + c0) * 4;
+                *reinterpret_cast<uint4*>(g) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+                *reinterpret_cast<uint4*>(g + 16) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+                bad = bad || h2_bad(u.x) || h2_bad(u.y) || h2_bad(u.z) || h2_bad(u.w) || h2_bad(w.x) ||
+                      h2_bad(w.y) || h2_bad(w.z) || h2_bad(w.w);
+            }
+        }
+    }
+    h2_flag(ovf, bad && !bf);
+}
+
 // |x| max as the bit pattern of a non-negative float (ordered like the value: an atomicMax on the
 // bits is exact and order-independent).  For the power-of-two operand scaling of the training
 // path's split convs.
@@ -1030,6 +1143,36 @@ int gn_apply_b2_inplace(void* x, int Bt, int HW, int C, const float* scale, cons
     hipLaunchKernelGGL(k_gn_apply_b2<true>, grid, dim3(256), shm, st, (const char*)x, (char*)x, HW, C, scale, shift,
                        silu, ppb);
     return check_launch("tcx_gn_apply_b2");
+}
+
+// k_attn_prep covers the image: the 8-channel groups fit one 1024-thread workgroup and every thread
+// holds at most AP_NP pixels (the 64^2 net's 16^2 x 192 attention input; config 5's 64^2 x 192 does not)
+static size_t attn_prep_lds(int C, int groups) {
+    const int R = 1024 / (C / 8);
+    return ((size_t)R * C + 2 * (size_t)C + 2 * (size_t)groups) * sizeof(double) + 2 * (size_t)C * sizeof(float);
+}
+bool attn_prep_ok(int HW, int C, int groups, int bf) {
+    return bf != 2 && C % 8 == 0 && C / 8 <= 1024 && groups > 0 && C % groups == 0 &&
+           HW <= AP_NP * (1024 / (C / 8)) && attn_prep_lds(C, groups) <= 160 * 1024;
+}
+int attn_prep_h2(float* a, void* y, int Bt, int HW, int C, const float* sc, const float* sh, const float* gamma,
+                 const float* beta, int groups, unsigned* ovf, int bf, hipStream_t st) {
+    TCX_REQUIRE(a && y && sc && sh && aligned16(a) && aligned16(y) && attn_prep_ok(HW, C, groups, bf),
+                "attn_prep_h2: bad args");
+    if (Bt == 0) return TCX_OK;
+    const size_t shm = attn_prep_lds(C, groups);
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attn_prep), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess) {
+            set_error("attn_prep_h2: cannot enable 160 KB of dynamic LDS");
+            return TCX_EHIP;
+        }
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_attn_prep, dim3(Bt), dim3(1024), shm, st, a, (char*)y, HW, C, sc, sh, gamma, beta, groups,
+                       1e-5f, ovf, bf);
+    return check_launch("attn_prep_h2");
 }
 }  // namespace tcx
 

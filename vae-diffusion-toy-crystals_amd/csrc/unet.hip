@@ -19,6 +19,9 @@ namespace tcx {
 bool conv3g_covers(int H, int W, int Cin, int cout_pad, bool bf);  // conv3g.hip
 // h2 / bf16 record writers (norm.hip, attention_split.hip): bf != 0 writes bf16 halves
 bool upsample_fused_ok(int H, int W, int C);  // norm.hip: band / segmented band
+bool attn_prep_ok(int HW, int C, int groups, int bf);  // norm.hip: the attention input pass
+int attn_prep_h2(float* a, void* y, int Bt, int HW, int C, const float* sc, const float* sh, const float* gamma,
+                 const float* beta, int groups, unsigned* ovf, int bf, hipStream_t st);
 int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
                   unsigned* ovf, int bf, hipStream_t st);
 int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
@@ -419,7 +422,8 @@ __global__ __launch_bounds__(256) void k_first_gnsum(const double* __restrict__ 
     const int b = blockIdx.x;
     if (threadIdx.x < 26) {
         double t = 0.0;
-        for (int j = 0; j < nchunk; ++j) t += part[((size_t)b * nchunk + j) * 26 + threadIdx.x];
+        // the CFG halves share x_t: k_first_acf ran over the Bimg distinct images only
+        for (int j = 0; j < nchunk; ++j) t += part[((size_t)(b % Bimg) * nchunk + j) * 26 + threadIdx.x];
         a[threadIdx.x] = t;
     }
     __syncthreads();
@@ -552,6 +556,9 @@ __device__ __forceinline__ float4 head_ld4(const float* h, size_t e) {
         return *reinterpret_cast<const float4*>(h + e);
     }
 }
+// LA: passes whose loads are in flight ahead of the one being computed (round 5: 2 -> 4, the whole pass
+// loop unrolled so the ring is static; 2 passes ahead left the 403 MB read at 3.8 TB/s)
+constexpr int HR_LA = 4;
 template <int Q, bool B2 = false>
 __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int HW, const float* __restrict__ tsc,
                                                 const float* __restrict__ tsh, const float* __restrict__ w_out,
@@ -563,15 +570,12 @@ __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int
     const int tid = threadIdx.x;
     const int sub = tid & 7, pl = tid >> 3;
     const int c0 = sub * CL;
-    float4 v[Q], vn[Q];  // passes 0 and 1 in flight before the constants are loaded
-    {
-        const size_t src = (size_t)(p0 + pl) * C + c0;
+    float4 v[HR_PASS][Q];  // pass k's channels; only HR_LA + 1 passes are live at a time
+    const size_t src0 = (size_t)(p0 + pl) * C + c0;
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            v[q] = head_ld4<B2>(h, src + 4 * q);
-            vn[q] = head_ld4<B2>(h, src + 32 * C + 4 * q);
-        }
-    }
+    for (int k = 0; k < HR_LA && k < HR_PASS; ++k)
+#pragma unroll
+        for (int q = 0; q < Q; ++q) v[k][q] = head_ld4<B2>(h, src0 + (size_t)k * 32 * C + 4 * q);
     float wr[CL][9], scl[CL], shf[CL];
 #pragma unroll
     for (int j = 0; j < CL; ++j) {
@@ -580,20 +584,19 @@ __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int
         scl[j] = tsc[(size_t)b * C + c0 + j];
         shf[j] = tsh[(size_t)b * C + c0 + j];
     }
+#pragma unroll
     for (int pass = 0; pass < HR_PASS; ++pass) {
         const int pg = p0 + pass * 32 + pl;
-        float4 vnn[Q];  // two passes ahead
-        if (pass + 2 < HR_PASS) {
-            const size_t src = (size_t)(pg + 64) * C + c0;
+        if (pass + HR_LA < HR_PASS) {
 #pragma unroll
-            for (int q = 0; q < Q; ++q) vnn[q] = head_ld4<B2>(h, src + 4 * q);
+            for (int q = 0; q < Q; ++q) v[pass + HR_LA][q] = head_ld4<B2>(h, src0 + (size_t)(pass + HR_LA) * 32 * C + 4 * q);
         }
         float acc[9];
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[t] = 0.f;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const float xs[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+            const float xs[4] = {v[pass][q].x, v[pass][q].y, v[pass][q].z, v[pass][q].w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int j = 4 * q + e;
@@ -617,11 +620,6 @@ __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int
             if (sub == t) mine = acc[t];
         dst[(size_t)sub * HW] = mine;  // lane sub writes tap sub; lane 0 also tap 8
         if (sub == 0) dst[(size_t)8 * HW] = acc[8];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            v[q] = vn[q];
-            vn[q] = vnn[q];
-        }
     }
 }
 
@@ -1011,6 +1009,16 @@ int conv_gn(const tcx_conv& cv, const float* x1, const float* x2, int C1, int C2
     return TCX_OK;
 }
 
+// TCX_ATTN_PREP=0: the attention input as four passes (apply, partials, finalize, apply) instead of
+// k_attn_prep (its statistics are summed in another fp64 order: not bit-identical; A/B and parity test)
+bool attn_prep_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("TCX_ATTN_PREP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // TCX_ATTN_SPLIT=0 keeps the split evaluator's attention on fp32 MFMA (A/B measurements)
 bool attn_split_enabled() {
     static const bool on = [] {
@@ -1142,7 +1150,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                 const int chunk = FIRST_ACF_PX;
                 const int nchunk = H * W / chunk;
                 double* acf = gn + (size_t)Bt * C * 2;  // the autocorrelation partials, past the [Bt][1][C][2] sums
-                hipLaunchKernelGGL(k_first_acf, dim3(nchunk, Bt), dim3(256), 0, st, x, B, H, W, chunk, acf);
+                hipLaunchKernelGGL(k_first_acf, dim3(nchunk, std::min(Bt, B)), dim3(256), 0, st, x, B, H, W, chunk, acf);
                 TCX_TRY(check_launch("k_first_acf"));
                 hipLaunchKernelGGL(k_first_gnsum, dim3(Bt), dim3(256), 0, st, acf, nchunk, H * W, C, c0.w, c0.kpad,
                                    P.bias0, ct, B, cfg, gn);
@@ -1206,14 +1214,20 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                     SC(4), SH(4), nullptr, nullptr, h2));
     // the attention block needs the normalised tensor itself (input of attn.norm and residual): fp32
     TCX_TRY(gn_tab(net, P, 5, P.P2, C2, gn, ns, st));
-    TCX_TRY(tcx_gn_apply_tab(P.a16, P.a16, Bt, P.P2, C2, P.sc(5), P.sh(5), 1, st));
     // attention: x_in = a16; b16 = GN(x_in); qkv = 1x1; b16 = attn; a16 = x_in + proj(b16)
     {
-        const int ns_a = std::max(1, P.P2 / 256);
-        TCX_TRY(tcx_gn_partials(P.a16, Bt, P.P2, C2, ns_a, gn, st));
-        TCX_TRY(gn_tab(net, P, 6, P.P2, C2, gn, ns_a, st));
-        if (h2.on) TCX_TRY(gn_apply_tab_h2(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, h2.ovf, fmt, st));
-        else TCX_TRY(tcx_gn_apply_tab(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, st));
+        if (h2.on && attn_prep_enabled() && attn_prep_ok(P.P2, C2, groups_of(C2), fmt)) {
+            // one pass per image: GN5+SiLU in place, attn.norm statistics, tables and h2 records (round 5)
+            TCX_TRY(attn_prep_h2(P.a16, P.b16, Bt, P.P2, C2, P.sc(5), P.sh(5), net->gn_w[6], net->gn_b[6],
+                                 groups_of(C2), h2.ovf, fmt, st));
+        } else {
+            TCX_TRY(tcx_gn_apply_tab(P.a16, P.a16, Bt, P.P2, C2, P.sc(5), P.sh(5), 1, st));
+            const int ns_a = std::max(1, P.P2 / 256);
+            TCX_TRY(tcx_gn_partials(P.a16, Bt, P.P2, C2, ns_a, gn, st));
+            TCX_TRY(gn_tab(net, P, 6, P.P2, C2, gn, ns_a, st));
+            if (h2.on) TCX_TRY(gn_apply_tab_h2(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, h2.ovf, fmt, st));
+            else TCX_TRY(tcx_gn_apply_tab(P.a16, P.b16, Bt, P.P2, C2, P.sc(6), P.sh(6), 0, st));
+        }
         const tcx_conv& q = net->qkv;
         int dummy = 0;
         // split path with N % 256 == 0 and a supported head dim: the qkv conv writes h2 and the
