@@ -576,13 +576,31 @@ __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int
     for (int k = 0; k < HR_LA && k < HR_PASS; ++k)
 #pragma unroll
         for (int q = 0; q < Q; ++q) v[k][q] = head_ld4<B2>(h, src0 + (size_t)k * 32 * C + 4 * q);
+    // the lane's constants as 16-B loads (its 9 CL weights are contiguous in w_out[c][tap], its CL scale /
+    // shift entries in the image's table rows): 9 Q + 2 Q vector loads instead of 11 CL scalar ones, which
+    // were 5x the data loads' instruction count per block
     float wr[CL][9], scl[CL], shf[CL];
+    {
+        float4 wq[9 * Q], sq[Q], hq[Q];
+        const float4* wp = reinterpret_cast<const float4*>(w_out + (size_t)c0 * 9);
 #pragma unroll
-    for (int j = 0; j < CL; ++j) {
+        for (int i = 0; i < 9 * Q; ++i) wq[i] = wp[i];
 #pragma unroll
-        for (int t = 0; t < 9; ++t) wr[j][t] = w_out[(c0 + j) * 9 + t];
-        scl[j] = tsc[(size_t)b * C + c0 + j];
-        shf[j] = tsh[(size_t)b * C + c0 + j];
+        for (int i = 0; i < Q; ++i) {
+            sq[i] = reinterpret_cast<const float4*>(tsc + (size_t)b * C + c0)[i];
+            hq[i] = reinterpret_cast<const float4*>(tsh + (size_t)b * C + c0)[i];
+        }
+#pragma unroll
+        for (int f = 0; f < 36 * Q; ++f) {
+            const float4 v = wq[f >> 2];
+            wr[f / 9][f % 9] = (f & 3) == 0 ? v.x : (f & 3) == 1 ? v.y : (f & 3) == 2 ? v.z : v.w;
+        }
+#pragma unroll
+        for (int j = 0; j < CL; ++j) {
+            const float4 a = sq[j >> 2], c = hq[j >> 2];
+            scl[j] = (j & 3) == 0 ? a.x : (j & 3) == 1 ? a.y : (j & 3) == 2 ? a.z : a.w;
+            shf[j] = (j & 3) == 0 ? c.x : (j & 3) == 1 ? c.y : (j & 3) == 2 ? c.z : c.w;
+        }
     }
 #pragma unroll
     for (int pass = 0; pass < HR_PASS; ++pass) {
@@ -1283,7 +1301,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         TCX_TRY(gn_tab(net, P, 10, P.P0, C, gn, ns, st));
         TCX_REQUIRE(C % 4 == 0, "head: C %% 4");
         // register-weight head (r03_ag: 124 -> 118 us at 64^2); k_head8 for other widths / shapes
-        if (P.P0 % HPR == 0 && (C == 96 || C == 64 || C == 32)) {
+        if (P.P0 % HPR == 0 && (C == 96 || C == 64 || C == 32) && aligned16(net->out_w)) {  // (16-B constant loads)
             const dim3 gr(Bt * P.P0 / HPR);
             if (C == 96 && fmt == 2)
                 hipLaunchKernelGGL((k_head8r<3, true>), gr, dim3(256), 0, st, P.a64, P.P0, P.sc(10), P.sh(10), net->out_w, P.r);
