@@ -53,15 +53,15 @@ F16_PEAK_TFLOPS = 2500.0         # MI355X dense f16/bf16 MFMA peak (no sparsity)
 SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 multiply-add
 # HBM bytes per conv launch (the launches the roofline times), measured by rocprofv3 PMC passes on
 # this sampler in the roofline's own configuration (one lane: Bt = 256 rows per launch, as the timed
-# one-lane pass; tools/gpu/r04r.sh -> tools/pmc_traffic.py, profiles/r04_fin2_pmc_traffic.txt):
+# one-lane pass; tools/gpu/final.sh -> tools/pmc_traffic.py, profiles/r05_fin_pmc_traffic.txt):
 # FETCH_SIZE x 2 (gfx950 reports half of 16-B/lane reads) + WRITE_SIZE, averaged over the conv
 # launches of two sampler steps.  A counter pass cannot run inside this process, so the measured
 # value is carried here with its source; it applies to the f16x3 path it was taken on.
-TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 533.9e6}
+TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 529.8e6}
 TRAFFIC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE in separate passes over bench.py --lanes 1 "
                   "(Bt = 256 per launch, the one-lane pass the roofline times), averaged over the 135 split-path "
-                  "conv launches (k_conv3m 16/32/64 h2, k_conv3lg 32/64 GN+SiLU prologue, k_conv3g 16 prologue, "
-                  "k_conv4s2g, k_lin1x1) of two sampler steps, profiles/r04_fin2_pmc_traffic.txt")
+                  "conv launches (k_conv3m 16/32/64 h2-source and GN+SiLU-prologue forms, k_conv4s2g, k_lin1x1) "
+                  "of two sampler steps, profiles/r05_fin_pmc_traffic.txt")
 
 
 def _cpu_model() -> str:
@@ -281,10 +281,9 @@ def main() -> int:
         args.steps = steps_saved
 
     if args.precision == "f16x3":
-        kname = ("split-path convs: k_conv3m (h2-source 3x3 at 16/32/64-px rows, v_mfma_f32_16x16x32_f16), "
-                 "k_conv3lg (3x3 GN+SiLU prologue at 32/64-px rows; LDS-DMA halo + weight ring), k_conv3g (16-px "
-                 "GN+SiLU prologue), k_conv4s2g (4x4/s2, LDS-DMA), k_lin1x1 (1x1) — f16x3, 3 f16 MFMAs per fp32 "
-                 "MAC; all conv launches of the pass")
+        kname = ("split-path convs: k_conv3m (3x3 at 16/32/64-px rows, v_mfma_f32_16x16x32_f16; h2 sources or the "
+                 "GroupNorm+SiLU prologue form), k_conv4s2g (4x4/s2, LDS-DMA), k_lin1x1 (1x1) — f16x3, 3 f16 "
+                 "MFMAs per fp32 MAC; all conv launches of the pass")
         peak = F16_PEAK_TFLOPS / SPLIT_PRODUCTS
         peak_basis = "2500 TFLOP/s dense f16 MFMA / 3 products per fp32 MAC; achieved in fp32-equivalent FLOPs"
     elif args.precision == "bf16":
