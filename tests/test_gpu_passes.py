@@ -50,37 +50,3 @@ def test_attention_input_pass_vs_four_passes(tmp_path, prec):
     d = float(np.abs(a - b).max()) / scale
     print(f"attention input pass vs four passes ({prec}): max {d:.2e} of scale")
     assert d <= (2e-6 if prec == "f16x3" else 2e-3)
-
-
-UPS_CHILD = r"""
-import sys, numpy as np, torch
-sys.path[:0] = [sys.argv[1], sys.argv[1] + "/tests", sys.argv[1] + "/vae-diffusion-toy-crystals_amd"]
-from test_gpu_ops import L, chk, st
-g = np.random.default_rng(5)
-outs = []
-for (B, H, W, C, tab) in [(2, 32, 32, 96, True), (3, 16, 16, 192, False), (1, 8, 24, 96, True), (2, 6, 5, 8, True)]:
-    x = torch.from_numpy(g.standard_normal((B, H, W, C)).astype(np.float32)).cuda()
-    sc = torch.from_numpy(g.uniform(0.5, 2.0, (B, C)).astype(np.float32)).cuda()
-    sh = torch.from_numpy(g.standard_normal((B, C)).astype(np.float32)).cuda()
-    y = torch.empty((B, 2 * H, 2 * W, C), device="cuda")
-    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
-    chk(L().tcx_upsample2x_h2(x.data_ptr(), y.data_ptr(), B, H, W, C, sc.data_ptr() if tab else None,
-                              sh.data_ptr() if tab else None, ovf.data_ptr(), st()))
-    torch.cuda.synchronize()
-    outs.append(y.cpu().numpy().view(np.uint32).ravel())
-np.save(sys.argv[2], np.concatenate(outs))
-"""
-
-
-def test_upsample_band_heights_are_bit_identical(tmp_path):
-    """the banded upsample with 2-row bands (TCX_UPS_ROWS=2) against the 4-row default: every output is the
-    same 4-tap blend of the same normalised source values, so the h2 records are the same bytes"""
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    got = {}
-    for v in ("2", "4"):
-        path = str(tmp_path / f"u{v}.npy")
-        r = subprocess.run([sys.executable, "-c", UPS_CHILD, root, path], capture_output=True, text=True,
-                           timeout=300, env=dict(os.environ, TCX_UPS_ROWS=v))
-        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        got[v] = np.load(path)
-    assert np.array_equal(got["2"], got["4"])

@@ -1074,13 +1074,10 @@ int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const fl
     if ((size_t)Bt * H * W * C == 0) return TCX_OK;
     if (upsample_band_ok(H, W, C)) {  // the banded LDS form (the 64^2 U-Net's us1 / us2)
         // 4 output rows per band: 48 KB of LDS, 3 workgroups per CU (r03_n: the 8-row bands and 4-channel
-        // items were 3-28 % slower); TCX_UPS_ROWS=2: 2-row bands (36 KB, 4 per CU; A/B)
-        static const int rows = [] {
-            const char* e = getenv("TCX_UPS_ROWS");
-            return e && e[0] == '2' ? 2 : 4;
-        }();
+        // items were 3-28 % slower; r05_n: 2-row bands, 36 KB and 4 per CU, 4-7 % slower)
+        constexpr int rows = 4;
         const size_t shm = (size_t)(rows / 2 + 2) * W * C * sizeof(float);
-        const auto k = rows == 2 ? &k_upsample2x_band<2, true> : &k_upsample2x_band<4, true>;
+        const auto k = &k_upsample2x_band<4, true>;
         static bool attr = false;
         if (!attr) {
             if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,

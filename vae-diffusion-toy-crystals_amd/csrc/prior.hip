@@ -235,7 +235,7 @@ int trunk(const Ctx& c, const tcx_prior& P, const float* z, int B, const float* 
             SkLn ln;
             ln.lw = lw; ln.lb = lb; ln.gy = g1; ln.ld_gy = ld_gy; ln.gt = g2; ln.eps = P.ln_eps;
             ln.yn_h2 = b.hn_h2; ln.ovf = ovf_h2;
-            TCX_TRY(skinny_reduce_ln(b.part, skinny_h2_chunks(F), B, W, e2, ln, c.st));
+            TCX_TRY(skinny_reduce_ln(b.part, skinny_h2_chunks(W, F), B, W, e2, ln, c.st));
         } else {
             TCX_TRY(lin(c, P.fc1[j], 0, b.hn, W, nullptr, 0, true, nullptr, b.a, B, 3));
             TCX_TRY(lin_ln(c, P.fc2[j], b.a, F, h, h_next, B, lw, lb, g1, ld_gy, g2, P.ln_eps, b.hn));

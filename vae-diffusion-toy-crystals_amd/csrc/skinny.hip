@@ -249,6 +249,101 @@ __global__ __launch_bounds__(512) void k_skinny_h2(SkH2Args a) {
     }
 }
 
+// Wide form (round 5): a workgroup is 4 waves, each on CT column tiles (16 CT columns) x its own K slice
+// of 32 NC values, so the activation fragments a wave loads serve CT tiles instead of one.  What bounds a
+// DDIM-sized launch is the count of load instructions reaching the CUs, not the HBM stream
+// (tools/probe/skinny_probe.hip, profiles/r05_o_skinny_probe.txt: without its loads the one-tile form
+// takes 2.6 of its 10.3 us, and at 36 rows the activation fragments are 3x the weights' loads), so
+// sharing them across tiles is the lever.  Always writes partial planes (S = K / (128 NC) chunks: 256
+// workgroups at fc2 of the w1024 prior); the reduce (k_sk_reduce_ln) adds bias, residual and LayerNorm.
+// Used for partial planes only: at fc1 (K = 1,024) the extra reduce launch an h2 epilogue would need costs
+// more than the form saves (r05_o: 8.2 + 5.0 us vs the one-chunk form's 10.3 with its epilogue inside).  Same per-wave MFMA order as k_skinny_h2 (k order within a wave's slice), a
+// fixed wave order in the workgroup and a fixed chunk order in the reduce: deterministic.
+constexpr int SKW_WAVES = 4;
+constexpr int SKW_NC = 2, SKW_CT = 4;
+template <int MT, int NC, int CT>
+__global__ __launch_bounds__(64 * SKW_WAVES) void k_skinny_h2w(SkH2Args a) {
+    __shared__ float red[SKW_WAVES][16 * MT][16 * CT + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int r = lane & 15, q = lane >> 4;
+    const int n0 = blockIdx.x * 16 * CT;
+    const int sidx = blockIdx.y;
+    const int K = a.K, G = K / 8;
+    const int npad = (a.N + 15) / 16 * 16;  // packed weight rows
+    const int kw0 = sidx * SKW_WAVES * 32 * NC + wv * 32 * NC;
+    const int kend = min(K, kw0 + 32 * NC);
+    uint4 wh[CT][NC], wl[CT][NC], xh[NC][MT], xl[NC][MT];
+    float winv[CT];
+#pragma unroll
+    for (int j = 0; j < CT; ++j) {
+        const int n = min(n0 + 16 * j + r, npad - 1);  // rows past the pack re-read its last row (discarded)
+        winv[j] = a.winv[min(n, a.N - 1)];
+        const char* wr = a.w + ((size_t)n * G + q) * 32;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int kc = min(kw0 + 32 * c, K - 32);
+            const char* p = wr + (size_t)(kc / 8) * 32;
+            wh[j][c] = *reinterpret_cast<const uint4*>(p);
+            wl[j][c] = *reinterpret_cast<const uint4*>(p + 16);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int kb = kw0 + 32 * c;
+        const int kc = min(kb, K - 32);
+        const bool live = kb < kend;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const char* p = a.x + ((size_t)min(16 * t + r, a.M - 1) * G + kc / 8 + q) * 32;
+            const char* src = live ? p : reinterpret_cast<const char*>(sk_zero8);
+            xh[c][t] = *reinterpret_cast<const uint4*>(src);
+            xl[c][t] = *reinterpret_cast<const uint4*>(src + 16);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // all loads in flight first (k_skinny)
+    f32x4 acc[CT][MT];
+#pragma unroll
+    for (int j = 0; j < CT; ++j)
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) {
+            const h8 bh = __builtin_bit_cast(h8, wh[j][c]), bl = __builtin_bit_cast(h8, wl[j][c]);
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const h8 ah = __builtin_bit_cast(h8, xh[c][t]), al = __builtin_bit_cast(h8, xl[c][t]);
+                acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[j][t], 0, 0, 0);
+                acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[j][t], 0, 0, 0);
+                acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[j][t], 0, 0, 0);
+            }
+        }
+#pragma unroll
+    for (int j = 0; j < CT; ++j)
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) red[wv][16 * t + 4 * q + e][16 * j + r] = acc[j][t][e] * winv[j];
+    __syncthreads();
+    const int M = a.M, N = a.N;  // N % 8 == 0 (skinny_h2_wide)
+    float* part = a.part + (size_t)sidx * M * N;
+    for (int o = tid; o < M * 2 * CT; o += 64 * SKW_WAVES) {  // (row, 8 columns), two 16-B stores
+        const int m = o / (2 * CT), c0 = 8 * (o - (o / (2 * CT)) * (2 * CT)), n = n0 + c0;
+        if (n >= N) continue;
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            float s = red[0][m][c0 + k];
+#pragma unroll
+            for (int w = 1; w < SKW_WAVES; ++w) s += red[w][m][c0 + k];
+            v[k] = s;
+        }
+        *reinterpret_cast<float4*>(part + (size_t)m * N + n) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(part + (size_t)m * N + n + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+}
+
 typedef void (*SkH2Kernel)(SkH2Args);
 
 SkH2Kernel sk_h2_kernel(int mt, int nc) {
@@ -261,6 +356,25 @@ int nc_for(int K) {
     int nc = 1;
     while (nc < 4 && SK_WAVES * 32 * nc < K) nc *= 2;
     return nc;
+}
+
+// the wide form serves the prior's split-K trunk linear (fc2: N >= 1024 -> >= 16 column groups of 64,
+// K / 256 chunks)
+bool skinny_h2_wide(int N, int K) {
+    static const bool off = getenv("TCX_SKINNY_WIDE") && getenv("TCX_SKINNY_WIDE")[0] == '0';  // A/B
+    return !off && N >= 1024 && N % 8 == 0 && K % (SKW_WAVES * 32 * SKW_NC) == 0;
+}
+
+int launch_h2w(const void* xh, int K, const void* wh, const float* winv, int M, int N, float* part, hipStream_t st) {
+    SkH2Args a{};
+    a.x = static_cast<const char*>(xh); a.w = static_cast<const char*>(wh); a.winv = winv;
+    a.K = K; a.M = M; a.N = N; a.part = part;
+    const int mt = cdiv(M, 16);
+    const dim3 grid(cdiv(N, 16 * SKW_CT), K / (SKW_WAVES * 32 * SKW_NC));
+    auto k = mt == 1 ? k_skinny_h2w<1, SKW_NC, SKW_CT> : mt == 2 ? k_skinny_h2w<2, SKW_NC, SKW_CT>
+           : mt == 3 ? k_skinny_h2w<3, SKW_NC, SKW_CT> : k_skinny_h2w<4, SKW_NC, SKW_CT>;
+    hipLaunchKernelGGL(k, grid, dim3(64 * SKW_WAVES), 0, st, a);
+    return check_launch("skinny linear (f16x3, wide)");
 }
 
 int launch_h2(const void* xh, int K, const void* wh, const float* winv, int M, int N, float* part, const SkEpi* direct,
@@ -561,14 +675,21 @@ bool skinny_h2_ok(int M, int N, int K) {
     return !off && M >= 1 && M <= 64 && N >= 1 && K >= 32 && K % 32 == 0;
 }
 
-int skinny_h2_chunks(int K) { return cdiv(K, SK_WAVES * 32 * nc_for(K)); }
+// partial planes of skinny_h2_partials (the wide form where it applies) / of skinny_h2_linear's split-K
+int skinny_h2_chunks(int N, int K) {
+    return skinny_h2_wide(N, K) ? K / (SKW_WAVES * 32 * SKW_NC) : cdiv(K, SK_WAVES * 32 * nc_for(K));
+}
+int skinny_h2_chunks_linear(int K) { return cdiv(K, SK_WAVES * 32 * nc_for(K)); }
 
-size_t skinny_h2_part_floats(int M, int N, int K) { return (size_t)skinny_h2_chunks(K) * M * N; }
+size_t skinny_h2_part_floats(int M, int N, int K) {
+    return (size_t)std::max(skinny_h2_chunks(N, K), skinny_h2_chunks_linear(K)) * M * N;
+}
 
 int skinny_h2_partials(const void* xh, int K, const void* wh, const float* winv, int M, int N, float* part,
                        hipStream_t st) {
     TCX_REQUIRE(xh && wh && winv && part && skinny_h2_ok(M, N, K) && aligned16(xh) && aligned16(wh),
                 "skinny linear (f16x3): bad args");
+    if (skinny_h2_wide(N, K)) return launch_h2w(xh, K, wh, winv, M, N, part, st);
     return launch_h2(xh, K, wh, winv, M, N, part, nullptr, st);
 }
 
@@ -577,10 +698,10 @@ int skinny_h2_linear(const void* xh, int K, const void* wh, const float* winv, i
     TCX_REQUIRE(xh && wh && winv && skinny_h2_ok(M, N, K) && aligned16(xh) && aligned16(wh) &&
                     (e.y || e.z || e.y_h2) && (!e.y_h2 || (N % 8 == 0 && aligned16(e.y_h2) && (!e.b || aligned16(e.b)))),
                 "skinny linear (f16x3): bad args");
-    if (skinny_h2_chunks(K) == 1) return launch_h2(xh, K, wh, winv, M, N, nullptr, &e, st);
+    if (skinny_h2_chunks_linear(K) == 1) return launch_h2(xh, K, wh, winv, M, N, nullptr, &e, st);
     TCX_REQUIRE(part && !e.y_h2, "skinny linear (f16x3): split-K needs scratch and an fp32 output");
     TCX_TRY(launch_h2(xh, K, wh, winv, M, N, part, nullptr, st));
-    return skinny_reduce(part, skinny_h2_chunks(K), M, N, e, st);
+    return skinny_reduce(part, skinny_h2_chunks_linear(K), M, N, e, st);
 }
 
 bool skinny_ln_ok(int N) { return N % 4 == 0 && N <= 4096; }

@@ -61,7 +61,7 @@ int skinny_reduce_ln(const float* part, int S, int M, int N, const SkEpi& e, con
 // v_mfma_f32_16x16x32_f16 (16x the f32 MFMA rate), fp32 accumulation.
 bool skinny_h2_ok(int M, int N, int K);
 size_t skinny_h2_part_floats(int M, int N, int K);
-int skinny_h2_chunks(int K);
+int skinny_h2_chunks(int N, int K);  // partial planes of skinny_h2_partials at this shape
 int skinny_h2_partials(const void* xh, int K, const void* wh, const float* winv, int M, int N, float* part,
                        hipStream_t st);
 int skinny_h2_linear(const void* xh, int K, const void* wh, const float* winv, int M, int N, float* part,
