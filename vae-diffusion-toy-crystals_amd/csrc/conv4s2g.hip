@@ -31,16 +31,18 @@
 namespace tcx {
 namespace {
 
-constexpr int Q_TP = 128;                       // output pixels per tile
+constexpr int Q_TP = 128;                       // output pixels per tile and row block of waves (RT = 1)
 constexpr int Q_PAIR = 2 * 3 * 2 * 1024;        // B fragments of two k-steps (12 KB)
 __host__ __device__ constexpr int q_rs(int Wo) { return 2 * Wo + 4; }  // both parities (Wo + 1 each) + 2 pad
-__host__ __device__ constexpr int q_npx(int Wo) { return (2 * (Q_TP / Wo) + 2) * q_rs(Wo); }
+__host__ __device__ constexpr int q_npx(int Wo, int RT = 1) { return (2 * (RT * Q_TP / Wo) + 2) * q_rs(Wo); }
 // SLIM (2-byte bf16 sources, h2.hpp "b2"): a slot is the 16-B hi piece of the 8-channel chunk only, 64
 // slots per 1-KB DMA instruction, consecutive and unswizzled (a ds_read_b128 lane group reads 16
 // consecutive 16-B slots of one parity row: every bank once); config 5's ds1 (Wo = 128) fits only so
-__host__ __device__ constexpr int q_ni(int Wo, bool SLIM = false) { return (q_npx(Wo) + (SLIM ? 63 : 31)) / (SLIM ? 64 : 32); }
-constexpr size_t conv4s2g_lds_bytes(int Wo, bool SLIM = false) {
-    return (size_t)2 * q_ni(Wo, SLIM) * 1024 + 2 * (size_t)Q_PAIR;
+__host__ __device__ constexpr int q_ni(int Wo, bool SLIM = false, int RT = 1) {
+    return (q_npx(Wo, RT) + (SLIM ? 63 : 31)) / (SLIM ? 64 : 32);
+}
+constexpr size_t conv4s2g_lds_bytes(int Wo, bool SLIM = false, int RT = 1) {
+    return (size_t)2 * q_ni(Wo, SLIM, RT) * 1024 + 2 * (size_t)Q_PAIR;
 }
 constexpr int Q_WAIT_VM0 = 0x0F70;
 constexpr int Q_WAIT_LGKM0 = 0xC07F;
@@ -49,18 +51,22 @@ __device__ __forceinline__ void q_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
 
-template <int Wo, bool BF, bool SLIM = false>
+// RT (round 5): row blocks of 32 pixels per wave, so a tile is 128 RT pixels.  RT = 2 doubles the output
+// rows of a tile, so fewer halo rows are staged per output row (6 input rows for 2 output rows at Wo = 128,
+// where RT = 1 staged 4 for 1), and every B fragment read serves two A fragments (config 5's b2 forms)
+template <int Wo, bool BF, bool SLIM = false, int RT = 1>
 __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
     static_assert(!SLIM || BF, "the slim slot holds the bf16 hi piece only");
     constexpr int NT = 3;
-    constexpr int TR = Q_TP / Wo;        // output rows per tile
+    constexpr int TP = RT * Q_TP;        // output pixels per tile
+    constexpr int TR = TP / Wo;          // output rows per tile
     constexpr int RS = q_rs(Wo);         // halo slots per halo row (both column parities + 2 pad)
-    constexpr int NPX = q_npx(Wo);
-    constexpr int NI = q_ni(Wo, SLIM);
+    constexpr int NPX = q_npx(Wo, RT);
+    constexpr int NI = q_ni(Wo, SLIM, RT);
     constexpr int NIH = (NI + 1) / 2;    // halo DMA instructions per halo wave
     constexpr int HB = NI * 1024;
     constexpr int RING = 2 * HB;
-    static_assert(TR * Wo == Q_TP, "tile = whole output rows");
+    static_assert(TR * Wo == TP, "tile = whole output rows");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     char* const smc = reinterpret_cast<char*>(sm);
     int lz;  // LDS-DMA destinations from a base the optimiser cannot fold to a constant (conv3l.hip)
@@ -73,7 +79,7 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int mblk = tile / p.n_nblk;
     const int nblk = tile - mblk * p.n_nblk;
-    const int m0 = mblk * Q_TP, n0 = nblk * 32 * NT;
+    const int m0 = mblk * TP, n0 = nblk * 32 * NT;
     const int b = m0 / p.HoWo;
     const int r0 = (m0 - b * p.HoWo) / Wo;  // first output row of the tile
     const int bs = p.bmod > 0 ? b % p.bmod : b;
@@ -93,14 +99,18 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
     const bool b2 = BF && p.bf == 2;
     const int rowb = p.C1 * (b2 ? 2 : 4);
     auto halo_voff = [&](int i) {
-        int s = SLIM ? 64 * i + lane : 32 * i + (lane >> 1);
+        // RT = 2: recomputed at every issue from an opaque copy of the lane index (hoisted out of the chunk
+        // loop, the offsets of all NI instructions spilled beside the doubled accumulators; k_conv3m's note)
+        int ln = lane;
+        if constexpr (RT == 2) asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+        int s = SLIM ? 64 * i + ln : 32 * i + (ln >> 1);
         s = s < NPX ? s : NPX - 1;
         const int hr = s / RS, hc = s - (s / RS) * RS;
         const int swz = SLIM ? 0 : (hr & 1) ^ ((hc >> 3) & 1);
         const int par = hc >= Wo + 1 ? 1 : 0;
         const int cc = min(hc - par * (Wo + 1), Wo);  // the 2 pad slots re-read column Wo
         const int y = wrap_idx(2 * r0 - 1 + hr, H), x = wrap_idx(2 * cc + par - 1, W);
-        return ((bs * H + y) * W + x) * rowb + (b2 ? 0 : 16 * ((lane & 1) ^ swz));
+        return ((bs * H + y) * W + x) * rowb + (b2 ? 0 : 16 * ((ln & 1) ^ swz));
     };
     auto halo_issue = [&](int j, int buf, int q0, int q1) {
 #pragma unroll
@@ -121,23 +131,35 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
 
     // ---- A fragments: lane (li, lh) of k-step (dy, p) reads tap (dy, dx = 2 p + lh) of its pixel:
     // slot (2 r + dy) RS + (dx & 1)(Wo + 1) + c + (dx >> 1), r / c = the pixel's row / column in the tile
-    const int mloc = wv * 32 + li;
-    const int ahc = (mloc % Wo) + lh * (Wo + 1);  // halo column of k-step p = 0 (dx = 2 p + lh)
-    const int abase = 2 * (mloc / Wo) * RS + ahc;  // + dy RS + p
-    // piece swizzle of a slot (hr, hc): (hr & 1) ^ ((hc >> 3) & 1) — with the 2 pad slots per halo row,
-    // conflict-free for every ds_read_b128 lane group, tap and row width 16 / 32 / 64 (exhaustive check);
-    // hr = 2 r + dy, so its parity is dy's
-    const int asw0 = (ahc >> 3) & 1, asw1 = ((ahc + 1) >> 3) & 1;
-    f32x16 acc[NT];
+    // row block rt of wave wv is virtual wave RT wv + rt (the epilogue's numbering)
+    int abase[RT], asw0[RT], asw1[RT];
 #pragma unroll
-    for (int n = 0; n < NT; ++n) acc[n] = (f32x16){};
-    h8 a_h[2], a_l[2], b_h[2][NT], b_l[2][NT];
+    for (int rt = 0; rt < RT; ++rt) {
+        const int mloc = (RT * wv + rt) * 32 + li;
+        const int ahc = (mloc % Wo) + lh * (Wo + 1);  // halo column of k-step p = 0 (dx = 2 p + lh)
+        abase[rt] = 2 * (mloc / Wo) * RS + ahc;       // + dy RS + p
+        // piece swizzle of a slot (hr, hc): (hr & 1) ^ ((hc >> 3) & 1) — with the 2 pad slots per halo row,
+        // conflict-free for every ds_read_b128 lane group, tap and row width 16 / 32 / 64 (exhaustive check);
+        // hr = 2 r + dy, so its parity is dy's
+        asw0[rt] = (ahc >> 3) & 1;
+        asw1[rt] = ((ahc + 1) >> 3) & 1;
+    }
+    f32x16 acc[RT][NT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[rt][n] = (f32x16){};
+    h8 a_h[2][RT], a_l[2][RT], b_h[2][NT], b_l[2][NT];
     auto rd_a = [&](int set, int kc, int hb) {  // k-step kc = 2 dy + p of the chunk in halo buffer hb
-        const int s = abase + (kc >> 1) * RS + (kc & 1);
-        const int sw = ((kc >> 1) & 1) ^ ((kc & 1) ? asw1 : asw0);
-        const char* A = smc + hb * HB + s * (SLIM ? 16 : 32);
-        a_h[set] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(A + (SLIM ? 0 : 16 * sw)));
-        if constexpr (!BF) a_l[set] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(A + 16 * (sw ^ 1)));
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const int s = abase[rt] + (kc >> 1) * RS + (kc & 1);
+            const int sw = ((kc >> 1) & 1) ^ ((kc & 1) ? asw1[rt] : asw0[rt]);
+            const char* A = smc + hb * HB + s * (SLIM ? 16 : 32);
+            a_h[set][rt] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(A + (SLIM ? 0 : 16 * sw)));
+            if constexpr (!BF)
+                a_l[set][rt] = __builtin_bit_cast(h8, *reinterpret_cast<const float4*>(A + 16 * (sw ^ 1)));
+        }
     };
     const int bl = lane * 16;
     auto rd_b = [&](int set, int c) {  // k-step c: ring slot (c >> 1) & 1, half c & 1
@@ -151,20 +173,29 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
     auto mf = [&](int set) {
         if constexpr (BF) {
 #pragma unroll
-            for (int n = 0; n < NT; ++n)
-                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, a_h[set]),
-                                                                 __builtin_bit_cast(bf8, b_h[set][n]), acc[n], 0, 0, 0);
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, a_h[set][rt]),
+                                                                         __builtin_bit_cast(bf8, b_h[set][n]), acc[rt][n],
+                                                                         0, 0, 0);
             return;
         }
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
-            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[set], b_l[set][n], acc[n], 0, 0, 0);
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
-            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_l[set], b_h[set][n], acc[n], 0, 0, 0);
+            for (int n = 0; n < NT; ++n)
+                acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[set][rt], b_l[set][n], acc[rt][n], 0, 0, 0);
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
-            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[set], b_h[set][n], acc[n], 0, 0, 0);
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_l[set][rt], b_h[set][n], acc[rt][n], 0, 0, 0);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                acc[rt][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_h[set][rt], b_h[set][n], acc[rt][n], 0, 0, 0);
     };
     auto barrier = [&]() {
         __builtin_amdgcn_s_waitcnt(Q_WAIT_LGKM0);
@@ -234,7 +265,12 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
 
     __builtin_amdgcn_s_waitcnt(Q_WAIT_VM0);  // the clamped tail pairs land before LDS is reused
     __syncthreads();
-    conv_epilogue<NT, BF ? 2 : 1, 4>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
+    double* red = reinterpret_cast<double*>(sm);
+    conv_epi_store_rt<NT, BF ? 2 : 1, RT * 4, RT>(p, acc, m0, n0, RT * wv, lane, red);
+    if (p.gn) {
+        __syncthreads();
+        conv_epi_gn<NT, RT * 4>(p, m0, n0, tid, 256, red);
+    }
 }
 
 // fragment-ordered copy of a 4x4 h2 weight [cout_pad][16 Cin] (k = (4 dy + dx) Cin + ci):
@@ -261,29 +297,23 @@ __global__ void k_pack_frag4(const char* __restrict__ wh, char* __restrict__ wf,
     }
 }
 
-template <int Wo>
-int launch_q(const ConvParams& p, hipStream_t st) {
-    const int ai = p.bf == 2 ? 2 : p.bf ? 1 : 0;  // b2 sources take the slim slots
-    const size_t shm = conv4s2g_lds_bytes(Wo, ai == 2);
-    static bool attr[3] = {false, false, false};
-    auto kc = ai == 2 ? &k_conv4s2g<Wo, true, true> : ai == 1 ? &k_conv4s2g<Wo, true> : &k_conv4s2g<Wo, false>;
-    if (!attr[ai]) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)shm) != hipSuccess) {
-            set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", shm);
-            return TCX_EHIP;
-        }
-        attr[ai] = true;
-    }
-    hipLaunchKernelGGL(kc, dim3((p.M / Q_TP) * p.n_nblk), dim3(256), shm, st, p);
-    return check_launch("tcx_conv2d_h2(4x4/s2 lds-dma)");
+// row blocks per wave: 2 for the slim b2 form at Wo = 64 (config 5's ds2: 786 -> 672 us), 1 otherwise
+// (config 5's ds1 at Wo = 128: 1051 -> 1313 us with RT = 2; the 32-B-slot forms spill at RT = 2 and lose
+// ~20 % of the headline; profiles/r05_r_*); TCX_DS_RT=1 / 2 forces it (A/B, tests)
+int ds_rt(bool slim, int Wo) {
+    static const int forced = [] {
+        const char* e = getenv("TCX_DS_RT");
+        return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
+    }();
+    return forced ? forced : (slim && Wo == 64 ? 2 : 1);
 }
-// Wo = 128 (config 5's ds1): the slim b2 form only (the 32-B slots would not leave two workgroups per CU)
-int launch_q128(const ConvParams& p, hipStream_t st) {
-    constexpr size_t shm = conv4s2g_lds_bytes(128, true);
-    static_assert(shm <= 80 * 1024, "two workgroups per CU");
+
+template <int Wo, bool BF, bool SLIM, int RT>
+int launch_q_one(const ConvParams& p, hipStream_t st) {
+    constexpr size_t shm = conv4s2g_lds_bytes(Wo, SLIM, RT);
+    static_assert(shm <= 160 * 1024, "LDS");
     static bool attr = false;
-    auto kc = &k_conv4s2g<128, true, true>;
+    auto kc = &k_conv4s2g<Wo, BF, SLIM, RT>;
     if (!attr) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)shm) != hipSuccess) {
@@ -292,8 +322,24 @@ int launch_q128(const ConvParams& p, hipStream_t st) {
         }
         attr = true;
     }
-    hipLaunchKernelGGL(kc, dim3((p.M / Q_TP) * p.n_nblk), dim3(256), shm, st, p);
-    return check_launch("tcx_conv2d_h2(4x4/s2 lds-dma, Wo 128)");
+    hipLaunchKernelGGL(kc, dim3((p.M / (RT * Q_TP)) * p.n_nblk), dim3(256), shm, st, p);
+    return check_launch("tcx_conv2d_h2(4x4/s2 lds-dma)");
+}
+
+template <int Wo>
+int launch_q(const ConvParams& p, hipStream_t st) {
+    const int ai = p.bf == 2 ? 2 : p.bf ? 1 : 0;  // b2 sources take the slim slots
+    const bool rt2 = ds_rt(ai == 2, Wo) == 2 && p.HoWo % (2 * Q_TP) == 0;
+    if (ai == 2) return rt2 ? launch_q_one<Wo, true, true, 2>(p, st) : launch_q_one<Wo, true, true, 1>(p, st);
+    if (ai == 1) return rt2 ? launch_q_one<Wo, true, false, 2>(p, st) : launch_q_one<Wo, true, false, 1>(p, st);
+    return rt2 ? launch_q_one<Wo, false, false, 2>(p, st) : launch_q_one<Wo, false, false, 1>(p, st);
+}
+// Wo = 128 (config 5's ds1): the slim b2 form only (the 32-B slots would not leave two workgroups per CU)
+int launch_q128(const ConvParams& p, hipStream_t st) {
+    static_assert(conv4s2g_lds_bytes(128, true) <= 80 * 1024 && conv4s2g_lds_bytes(128, true, 2) <= 80 * 1024,
+                  "two workgroups per CU");
+    const bool rt2 = ds_rt(true, 128) == 2 && p.HoWo % (2 * Q_TP) == 0;
+    return rt2 ? launch_q_one<128, true, true, 2>(p, st) : launch_q_one<128, true, true, 1>(p, st);
 }
 
 }  // namespace
