@@ -297,9 +297,8 @@ __global__ void k_pack_frag4(const char* __restrict__ wh, char* __restrict__ wf,
     }
 }
 
-// row blocks per wave: 2 for the slim b2 form at Wo = 64 (config 5's ds2: 786 -> 672 us), 1 otherwise
-// (config 5's ds1 at Wo = 128: 1051 -> 1313 us with RT = 2; the 32-B-slot forms spill at RT = 2 and lose
-// ~20 % of the headline; profiles/r05_r_*); TCX_DS_RT=1 / 2 forces it (A/B, tests)
+// row blocks per wave of the slim b2 forms: 2 at Wo = 64 (config 5's ds2: 786 -> 672 us), 1 at Wo = 128
+// (config 5's ds1: 1051 -> 1313 us with RT = 2; profiles/r05_r_*); TCX_DS_RT=1 / 2 forces it (A/B, tests)
 int ds_rt(bool slim, int Wo) {
     static const int forced = [] {
         const char* e = getenv("TCX_DS_RT");
@@ -331,8 +330,10 @@ int launch_q(const ConvParams& p, hipStream_t st) {
     const int ai = p.bf == 2 ? 2 : p.bf ? 1 : 0;  // b2 sources take the slim slots
     const bool rt2 = ds_rt(ai == 2, Wo) == 2 && p.HoWo % (2 * Q_TP) == 0;
     if (ai == 2) return rt2 ? launch_q_one<Wo, true, true, 2>(p, st) : launch_q_one<Wo, true, true, 1>(p, st);
-    if (ai == 1) return rt2 ? launch_q_one<Wo, true, false, 2>(p, st) : launch_q_one<Wo, true, false, 1>(p, st);
-    return rt2 ? launch_q_one<Wo, false, false, 2>(p, st) : launch_q_one<Wo, false, false, 1>(p, st);
+    // the 32-B-slot forms stay at RT = 1: at RT = 2 they spill (255 VGPRs + 144-176 B of scratch) and the
+    // headline fell from 79.2 to 64.6 images/s with it (r05_r)
+    if (ai == 1) return launch_q_one<Wo, true, false, 1>(p, st);
+    return launch_q_one<Wo, false, false, 1>(p, st);
 }
 // Wo = 128 (config 5's ds1): the slim b2 form only (the 32-B slots would not leave two workgroups per CU)
 int launch_q128(const ConvParams& p, hipStream_t st) {
