@@ -57,11 +57,18 @@ SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 m
 # FETCH_SIZE x 2 (gfx950 reports half of 16-B/lane reads) + WRITE_SIZE, averaged over the conv
 # launches of two sampler steps.  A counter pass cannot run inside this process, so the measured
 # value is carried here with its source; it applies to the f16x3 path it was taken on.
-TRAFFIC_BYTES_PER_CONV_LAUNCH = {"f16x3": 529.8e6}
-TRAFFIC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE in separate passes over bench.py --lanes 1 "
-                  "(Bt = 256 per launch, the one-lane pass the roofline times), averaged over the 135 split-path "
-                  "conv launches (k_conv3m 16/32/64 h2-source and GN+SiLU-prologue forms, k_conv4s2g, k_lin1x1) "
-                  "of two sampler steps, profiles/r05_fin_pmc_traffic.txt")
+# keyed by (conv precision, image size): the 64x64 headline (f16x3) and config 5 (256x256 bf16)
+TRAFFIC_BYTES_PER_CONV_LAUNCH = {("f16x3", 64): 529.8e6, ("bf16", 256): 1324.1e6}
+TRAFFIC_SOURCE = {
+    ("f16x3", 64): ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE in separate passes over bench.py --lanes 1 "
+                    "(Bt = 256 per launch, the one-lane pass the roofline times), averaged over the 135 split-path "
+                    "conv launches (k_conv3m 16/32/64 h2-source and GN+SiLU-prologue forms, k_conv4s2g, k_lin1x1) "
+                    "of two sampler steps, profiles/r05_fin_pmc_traffic.txt"),
+    ("bf16", 256): ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE in separate passes over bench.py --img-size 256 "
+                    "--batch 64 --precision bf16 --lanes 1 (64 images per launch: the evaluation runs in two passes "
+                    "under the 2 GiB cap), averaged over the 270 conv launches (k_conv3lb, k_conv4s2g, k_lin1x1) of "
+                    "two sampler steps, profiles/r05_t_cfg5_pmc_traffic.txt"),
+}
 
 
 def _cpu_model() -> str:
@@ -301,7 +308,7 @@ def main() -> int:
     conv_avg_ms = ms.value / max(1, n.value)
     conv_avg_flop = fl.value / max(1, n.value)
     achieved = conv_avg_flop / (conv_avg_ms * 1e-3) / 1e12 if n.value else 0.0
-    traffic = TRAFFIC_BYTES_PER_CONV_LAUNCH.get(args.precision) if S == 64 else None
+    traffic = TRAFFIC_BYTES_PER_CONV_LAUNCH.get((args.precision, S))
     result = {
         "metric": "denoised images/sec (300-step reverse-SDE, CFG=1.5) at 1/2/4/8 MI355X",
         "value": round(value, 4),
@@ -326,8 +333,9 @@ def main() -> int:
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                      "traffic": traffic,
                      "traffic_unit": "HBM bytes per conv launch",
-                     "traffic_source": TRAFFIC_SOURCE if traffic is not None else
-                     "not measured for this configuration (PMC passes exist for the 64x64 f16x3 headline only)",
+                     "traffic_source": TRAFFIC_SOURCE[(args.precision, S)] if traffic is not None else
+                     "not measured for this configuration (PMC passes exist for the 64x64 f16x3 headline and the "
+                     "256x256 bf16 config 5 only)",
                      "peak_basis": peak_basis,
                      "measured_on": "one-lane roofline pass (same K sampling passes on one stream, HIP events per conv launch)",
                      "avg_launch_ms": round(conv_avg_ms, 5), "avg_launch_gflop": round(conv_avg_flop / 1e9, 4),
