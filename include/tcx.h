@@ -195,7 +195,10 @@ int tcx_attention_split_b2(const void* qkv, void* out, int Bt, int N, int C, int
  * (sde_score_model.py:103-107) feeding this conv, never written to memory; a source without
  * tables is h2.  Only k_conv3g takes prologues (wfrag given; 3x3 stride 1 pad 1, W in {32, 64,
  * 128}, Cin % 32 == 0, Cin <= 384, cout_pad % 96 == 0): otherwise a table is TCX_EINVAL.  Without
- * wfrag the call is tcx_conv2d_h2. */
+ * wfrag the call is tcx_conv2d_h2.  bf16: 0 f16x3 records, 1 bf16 records, 2 two-byte bf16; + 16: source 1
+ * is chunk-major ([C1/8][bsrc*H*W][32 B] record planes, tcx_gn_apply_tab_h2_cm; 4x4/s2 shapes of k_conv4s2g),
+ * + 32: source 2 is chunk-major (3x3 shapes of k_conv3m); f16x3 records without prologue only, else
+ * TCX_EINVAL. */
 int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
                       const void* wh, const void* wfrag, const float* wscale, const float* bias,
                       const float* bias_b,
@@ -207,6 +210,11 @@ int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmod, int H, i
 /* tcx_gn_apply_tab with the output written as h2 (x == y allowed: in place). */
 int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale,
                         const float* shift, int silu, unsigned* ovf, void* stream);
+/* GroupNorm + SiLU apply from tables into CHUNK-MAJOR f16x3 records: y = [C/8][Bt*HW][32 B] (x != y;
+ * C % 8 == 0 and HW a multiple of 1536 / (C / 8) pixels) — the U-Net's skip tensors h1 / h2
+ * (sde_score_model.py:248-263: h1, h2 and their concats), read by tcx_conv2d_h2_pro with the chunk-major bits. */
+int tcx_gn_apply_tab_h2_cm(const float* x, void* y, int Bt, int HW, int C, const float* scale,
+                           const float* shift, unsigned* ovf, void* stream);
 /* tcx_upsample2x with the output written as h2. */
 int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
                       const float* shift, unsigned* ovf, void* stream);

@@ -521,3 +521,78 @@ def test_quad_epilogue_equals_column_epilogue(B, C1, Co, H, out_h2):
     if ga is not None:
         # 128 fp32 values per partial: the two orders agree to a few fp32 ulps of the sum of |values|
         np.testing.assert_allclose(ga, gb, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,C1,C2,Co,H,ks", [
+    (2, 96, 0, 96, 64, 4), (3, 192, 0, 192, 32, 4),  # ds1 / ds2: source 1 chunk-major (k_conv4s2g)
+    (2, 96, 96, 96, 64, 3), (3, 192, 192, 96, 32, 3),  # up1.net.0 / up2.net.0: source 2 chunk-major (k_conv3m)
+])
+def test_chunk_major_source_equals_pixel_major(B, C1, C2, Co, H, ks):
+    """tcx_conv2d_h2_pro with a chunk-major source ([C/8][B*H*W][32 B] record planes, bf16 arg bit 16 for
+    source 1, bit 32 for source 2: the U-Net's skip tensors) gives bit-identical outputs and GroupNorm
+    partials to the same records pixel-major: the kernels stage the same bytes into the same LDS slots."""
+    cin = C1 + C2
+    x1 = rng.standard_normal((B, C1, H, H))
+    x2 = rng.standard_normal((B, C2, H, H)) if C2 else None
+    w = rng.standard_normal((Co, cin, ks, ks)) / np.sqrt(cin * ks * ks)
+    b = dev(rng.standard_normal(Co))
+    wh, ws, cpad, kpad = pack_h2(w)
+    wf = pack_frag(wh, cpad, kpad, cin)
+    stride = 2 if ks == 4 else 1
+    Ho = H // stride
+    r1, r2 = to_h2(dev(nhwc(x1))), (to_h2(dev(nhwc(x2))) if C2 else None)
+
+    def cm(r):  # pixel-major records [B][H][W][C/8][8 f32] -> chunk-major [C/8][B*H*W][8 f32]
+        return r.reshape(-1, r.shape[-1] // 8, 8).permute(1, 0, 2).contiguous()
+
+    def run(s1, s2, flag):
+        y = torch.empty((B, Ho, Ho, Co), device="cuda")
+        gnd = torch.zeros((B, Ho * Ho // 128, Co, 2), dtype=torch.float64, device="cuda")
+        ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+        chk(L().tcx_conv2d_h2_pro(s1.data_ptr(), s2.data_ptr() if s2 is not None else None, B, 0, H, H, C1, C2,
+                                  wh.data_ptr(), wf.data_ptr(), ws.data_ptr(), b.data_ptr(), None, None, y.data_ptr(),
+                                  0, Co, cpad, kpad, ks, stride, 1, 1, 0, gnd.data_ptr(), None, None, None, None, flag,
+                                  ovf.data_ptr(), st()))
+        torch.cuda.synchronize()
+        return y.cpu().numpy(), gnd.cpu().numpy()
+
+    ya, ga = run(r1, r2, 0)
+    yb, gb = (run(cm(r1), None, 16) if C2 == 0 else run(r1, cm(r2), 32))
+    assert np.array_equal(ya, yb) and np.array_equal(ga, gb)
+    ref = nn_np.conv2d(np.concatenate([x1, x2], 1) if C2 else x1, w, b.cpu().numpy(), stride=stride, padding=1,
+                       mode="circular")
+    close(nchw(yb), ref)
+
+
+def test_chunk_major_source_refused_off_its_kernels():
+    """A chunk-major flag on a shape its kernels do not take fails loudly (no silent pixel-major read)."""
+    x = to_h2(dev(nhwc(rng.standard_normal((1, 96, 16, 16)))))
+    w = rng.standard_normal((96, 96, 3, 3)) / 30.0
+    wh, ws, cpad, kpad = pack_h2(w)
+    y = torch.empty((1, 16, 16, 96), device="cuda")
+    rc = L().tcx_conv2d_h2_pro(x.data_ptr(), None, 1, 0, 16, 16, 96, 0, wh.data_ptr(), None, ws.data_ptr(), None,
+                               None, None, y.data_ptr(), 0, 96, cpad, kpad, 3, 1, 1, 1, 0, None, None, None, None, None,
+                               16, None, st())
+    assert rc != 0
+
+
+@pytest.mark.parametrize("B,HW,C", [(3, 4096, 96), (3, 1024, 192), (2, 256, 384)])
+def test_gn_apply_chunk_major_equals_pixel_major(B, HW, C):
+    """tcx_gn_apply_tab_h2_cm writes the same records as tcx_gn_apply_tab_h2 (GroupNorm + SiLU, f16x3
+    split), bit for bit, in [C/8][B*HW][32 B] planes."""
+    x = dev(rng.standard_normal((B, HW, C)).astype(np.float32) * 3)
+    sc = dev(rng.standard_normal((B, C)))
+    sh = dev(rng.standard_normal((B, C)))
+    pm, cm = torch.empty_like(x), torch.full_like(x, float("nan"))
+    ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+    chk(L().tcx_gn_apply_tab_h2(x.data_ptr(), pm.data_ptr(), B, HW, C, sc.data_ptr(), sh.data_ptr(), 1,
+                                ovf.data_ptr(), st()))
+    chk(L().tcx_gn_apply_tab_h2_cm(x.data_ptr(), cm.data_ptr(), B, HW, C, sc.data_ptr(), sh.data_ptr(),
+                                   ovf.data_ptr(), st()))
+    torch.cuda.synchronize()
+    want = pm.reshape(B * HW, C // 8, 8).permute(1, 0, 2).contiguous()
+    a = want.view(torch.int32).cpu().numpy()
+    b = cm.view(torch.int32).cpu().numpy().reshape(a.shape)
+    nbad = int((a != b).sum())
+    print(f"chunk-major apply: {nbad} of {a.size} words differ")
+    assert nbad == 0 and int(ovf.item()) == 0

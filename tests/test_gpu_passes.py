@@ -1,6 +1,7 @@
 """GPU: the round-5 forms of the U-Net evaluation's bandwidth passes against the forms they replace, one
 process per setting (the library reads its knobs once): k_attn_prep (the attention block's input side in
-one pass per image) against the four passes it replaces (TCX_ATTN_PREP=0), on a whole 64^2 forward."""
+one pass per image) against the four passes it replaces (TCX_ATTN_PREP=0), and the chunk-major skip
+tensors (TCX_SKIP_CM) against the pixel-major in-place apply, on whole forwards."""
 import os
 import subprocess
 import sys
@@ -50,3 +51,13 @@ def test_attention_input_pass_vs_four_passes(tmp_path, prec):
     d = float(np.abs(a - b).max()) / scale
     print(f"attention input pass vs four passes ({prec}): max {d:.2e} of scale")
     assert d <= (2e-6 if prec == "f16x3" else 2e-3)
+
+
+@pytest.mark.parametrize("H", [64, 32])
+def test_chunk_major_skips_bit_identical(tmp_path, H):
+    """Skip tensors h1 / h2 written chunk-major by gn_apply_cm (the same fmaf + SiLU + record split as the
+    in-place apply) and read by the downsample and the concat conv from their planes: the whole forward is
+    bit-identical to TCX_SKIP_CM=0 (at 32^2 only h1 qualifies: h2's downsample output is 8 px wide)."""
+    a = _forward(tmp_path, "cm", {"TCX_SKIP_CM": "3"}, "f16x3", 64, H)
+    b = _forward(tmp_path, "pm", {"TCX_SKIP_CM": "0"}, "f16x3", 64, H)
+    assert np.array_equal(a, b)

@@ -20,6 +20,7 @@
 #include "conv_common.hpp"
 
 namespace tcx {
+bool conv3m_takes(const ConvParams& p);  // conv3m.hip
 namespace {
 
 // MODE 0: float4 loads, per-lane (tap, ci) decode (Cin % 4 == 0)
@@ -629,7 +630,11 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
     p.gn = gn_stats;
     p.nsplit = cdiv(p.HoWo, BM);
     if (gn_stats) TCX_REQUIRE(p.HoWo % BM == 0, "tcx_conv2d_h2: fused GN stats need Ho*Wo %% 128 == 0");
-    TCX_REQUIRE(bf16 >= 0 && bf16 <= 2, "tcx_conv2d_h2: bf16 must be 0 (f16x3), 1 (bf16 records) or 2 (2-byte bf16)");
+    // bits 4 / 5 of bf16: source 1 / source 2 chunk-major ([C/8][B][H][W][32 B] records, ConvParams::cm1/cm2)
+    const int cmf = bf16 >> 4;
+    bf16 &= 15;
+    TCX_REQUIRE(bf16 >= 0 && bf16 <= 2 && cmf >= 0 && cmf <= 3,
+                "tcx_conv2d_h2: bf16 must be 0 (f16x3), 1 (bf16 records) or 2 (2-byte bf16), plus chunk-major bits 16/32");
     const size_t bsrc = bmod > 0 ? (size_t)bmod : (size_t)Bt;
     const size_t lim = (size_t)1 << 31;
     const size_t esz = bf16 == 2 ? 2 : 4;  // bytes per source element (the prologue's fp32 sources: 4)
@@ -652,6 +657,20 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
                         lin1x1_applies(p, cout_pad);
         TCX_REQUIRE(ok, "tcx_conv2d_h2: 2-byte bf16 operands need k_conv3lb (3x3, rows of 64/128/256 px), "
                         "k_conv4s2g (4x4/s2) or k_lin1x1 (1x1) shapes");
+    }
+    if (cmf) {
+        // chunk-major sources: the 4x4/s2 LDS-DMA kernel (source 1) or k_conv3m (source 2) only
+        p.cm1 = cmf & 1;
+        p.cm2 = cmf >> 1;
+        TCX_REQUIRE(bf16 == 0 && !pro_scale1 && !pro_scale2 && (!p.cm2 || C2 > 0),
+                    "tcx_conv2d_h2: chunk-major sources are f16x3 records without a prologue");
+        if (p.cm1) {
+            TCX_REQUIRE(conv4s2g_applies(p, cout_pad), "tcx_conv2d_h2: a chunk-major source 1 needs a k_conv4s2g shape");
+            return launch_conv4s2g(p, cout_pad, (hipStream_t)stream);
+        }
+        TCX_REQUIRE(conv3g_applies(p, cout_pad) && conv3m_takes(p),
+                    "tcx_conv2d_h2: a chunk-major source 2 needs a k_conv3m shape");
+        return launch_conv3g(p, cout_pad, (hipStream_t)stream);
     }
     if (conv3g_applies(p, cout_pad)) return launch_conv3g(p, cout_pad, (hipStream_t)stream);
     TCX_REQUIRE(!pro_scale1 && !pro_scale2,

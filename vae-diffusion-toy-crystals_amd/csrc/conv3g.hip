@@ -59,6 +59,7 @@ bool conv3g_applies(const ConvParams& p, int cout_pad) {
 // conv3l.hip: the same conv with the B fragments staged once per workgroup in an LDS ring
 bool conv3l_takes(const ConvParams& p);
 int launch_conv3l(const ConvParams& p, hipStream_t st);
+int launch_conv3m(const ConvParams& p, hipStream_t st);
 // conv3lb.hip: the bf16 LDS-DMA form for rows of 64 / 128 / 256 pixels (h2 / bf16 record sources)
 bool conv3lb_takes(const ConvParams& p);
 int launch_conv3lb(const ConvParams& p, hipStream_t st);
@@ -68,7 +69,8 @@ int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st) {
     if (p.M == 0) return TCX_OK;
     prof_begin(st);
     int rc;
-    if (conv3lb_takes(p)) rc = launch_conv3lb(p, st);
+    if (p.cm2) rc = launch_conv3m(p, st);  // chunk-major source 2 (tcx_conv2d_h2_pro checked conv3m_takes)
+    else if (conv3lb_takes(p)) rc = launch_conv3lb(p, st);
     else if (conv3l_takes(p)) rc = launch_conv3l(p, st);
     else if (p.W == 64) rc = launch3g_w64(p, st);
     else if (p.W == 32) rc = launch3g_w32(p, st);

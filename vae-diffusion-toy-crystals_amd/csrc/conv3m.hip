@@ -57,7 +57,7 @@ __host__ __device__ constexpr int m_npx(int W) { return (M_TP / W + 2) * (W + 2)
 // PRO 1: + the image's GroupNorm tables [scale | shift][Cin <= 384] after the ring
 template <int W, int PRO = 0>
 constexpr size_t conv3m_lds_bytes() {
-    return (size_t)2 * ((m_npx(W) + 15) / 16) * 16 * 64 + 2 * (size_t)M_PAIR + (PRO ? 2 * 384 * sizeof(float) : 0);
+    return (size_t)2 * ((m_npx(W) + 15) / 16) * 16 * 64 + 2 * (size_t)M_PAIR + (PRO == 1 ? 2 * 384 * sizeof(float) : 0);
 }
 // PRO 1 transform units per thread: the 2 NPX 8-channel halo units of a chunk over 256 threads
 __host__ __device__ constexpr int m_tu(int W) { return (2 * m_npx(W) + 255) / 256; }
@@ -174,7 +174,9 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     const int hw = wv & 1;
     const int rowb = p.C1 * 4;
     const int img0 = bs * H;
-    auto halo_voff = [&](int i) __attribute__((always_inline)) {
+    // rb: bytes per pixel of the source (C1 * 4 pixel-major; 32 in a chunk-major source's 8-channel plane);
+    // ph: the byte distance of the chunk's second record (32 pixel-major; one plane chunk-major)
+    auto halo_voff = [&](int i, int rb, int ph) __attribute__((always_inline)) {
         // PRO 1 at 64-px rows: recomputed at every issue (an opaque copy of the lane index keeps hipcc from
         // hoisting all 13 offsets out of the tap loop, where they spilled with the transform's registers)
         int ls = lane >> 2;
@@ -182,28 +184,34 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         const int hr0 = (16 * i) / W2;
         const int th = W2 * (hr0 + 1) - 16 * i;
         const int y0 = wrap_idx(r0 + hr0 - 1, H), y1 = wrap_idx(r0 + hr0, H);
-        const int yo0 = (img0 + y0) * W * rowb, yo1 = (img0 + y1) * W * rowb;
+        const int yo0 = (img0 + y0) * W * rb, yo1 = (img0 + y1) * W * rb;
         const bool nx = ls >= th;
         int hc = 16 * i - hr0 * W2 + ls - (nx ? W2 : 0);
         const int sl = 16 * i + ls;
         const int hcs = hc;
         if (sl >= NPX) hc = (NPX - 1) % W2;  // padding slots read a valid pixel
         const int x = hc == 0 ? W - 1 : (hc == W + 1 ? 0 : hc - 1);
-        const int yo = (sl >= NPX) ? (img0 + wrap_idx(r0 + (NPX - 1) / W2 - 1, H)) * W * rowb : (nx ? yo1 : yo0);
-        return yo + x * rowb + 16 * ((lane & 3) ^ sw(hcs));
+        const int yo = (sl >= NPX) ? (img0 + wrap_idx(r0 + (NPX - 1) / W2 - 1, H)) * W * rb : (nx ? yo1 : yo0);
+        const int pc = (lane & 3) ^ sw(hcs);
+        if constexpr (PRO != 2) return yo + x * rb + 16 * pc;  // pixel-major only (rb = rowb, ph = 32)
+        else return yo + x * rb + 16 * (pc & 1) + (pc >> 1) * ph;
     };
+    // PRO 2 (p.cm2): PRO 0 with source 2 chunk-major, the 16-channel chunk two planes of 32-B pixel records
+    const int plane2 = PRO == 2 ? (int)(p.bytes2 / (unsigned)(p.C2 / 8)) : 0;
     // third `th` (0..2) of chunk j's halo into buffer buf
     auto halo_third = [&](int j, int buf, int th) __attribute__((always_inline)) {
         const int ci0 = j * M_KC;
         const bool s1 = ci0 < p.C1;
-        const int cc = (s1 ? ci0 : ci0 - p.C1) * 4;
+        const bool cm = PRO == 2 && !s1;
+        const int cc = cm ? ((ci0 - p.C1) / 8) * plane2 : (s1 ? ci0 : ci0 - p.C1) * 4;
+        const int rb = cm ? 32 : rowb, ph = cm ? plane2 : 32;
         const __amdgpu_buffer_rsrc_t rs = s1 ? r1 : r2;
         const int q0 = (NIH * th) / 3, q1 = (NIH * (th + 1)) / 3;
 #pragma unroll
         for (int q = 0; q < NIH; ++q) {
             if (q < q0 || q >= q1) continue;
             const int i = 2 * q + hw;
-            if (i < NI) m_dma16(rs, smd + buf * HB + i * 1024, halo_voff(i), cc);
+            if (i < NI) m_dma16(rs, smd + buf * HB + i * 1024, halo_voff(i, rb, ph), cc);
         }
     };
     auto halo_all = [&](int j, int buf) __attribute__((always_inline)) {
@@ -625,11 +633,13 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
 
 template <int W>
 int launch3m(const ConvParams& p, hipStream_t st) {
-    static bool attr[3] = {};
+    static bool attr[4] = {};
     const bool pro = p.sc1 != nullptr;
     const bool fast = p.act == 0 && !p.out_h2;
-    const int ai = pro ? 2 : (int)fast;
-    void (*const k)(ConvParams) = pro ? &k_conv3m<W, true, 1> : fast ? &k_conv3m<W, true, 0> : &k_conv3m<W, false, 0>;
+    const int ai = pro ? 2 : p.cm2 ? 3 : (int)fast;
+    void (*const k)(ConvParams) = pro ? &k_conv3m<W, true, 1>
+                                  : p.cm2 ? &k_conv3m<W, true, 2>
+                                  : fast ? &k_conv3m<W, true, 0> : &k_conv3m<W, false, 0>;
     const size_t lds = pro ? conv3m_lds_bytes<W, 1>() : conv3m_lds_bytes<W, 0>();
     if (!attr[ai]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
@@ -668,6 +678,8 @@ bool conv3mg_enabled() {
 bool conv3m_takes(const ConvParams& p) {
     const bool pro = p.sc1 != nullptr;
     if (pro && (!conv3mg_enabled() || p.C2 != 0 || p.act != 0 || p.out_h2 || p.sh1 == nullptr)) return false;
+    // chunk-major: source 2 of the h2 form (PRO 2), fp32 output, no activation
+    if (p.cm1 || (p.cm2 && (pro || p.C2 % 16 != 0 || p.act != 0 || p.out_h2))) return false;
     return !p.bf && p.circular && !(p.C2 > 0 && p.sc2 != nullptr) &&
            (p.W == 16 || p.W == 32 || p.W == 64) && p.M % M_TP == 0 && p.HoWo % M_TP == 0 && p.Cin % 32 == 0 &&
            p.Cin <= 384 && p.Cout % M_BN == 0 && p.osy == 1 && p.osx == 1 && p.bias_b == nullptr &&

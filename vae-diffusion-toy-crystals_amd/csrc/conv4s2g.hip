@@ -97,7 +97,11 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
     // b2 sources (BF, p.bf == 2, h2.hpp): the 8-channel chunk is ONE 16-B hi piece at byte 16 j of the
     // pixel's 2-byte row; both DMA lanes of a slot read it (the lo slot half is never read by BF)
     const bool b2 = BF && p.bf == 2;
-    const int rowb = p.C1 * (b2 ? 2 : 4);
+    // chunk-major source (p.cm1, ConvParams): the 8-channel chunk j is the plane at byte j * plane, a
+    // pixel's record at 32 * pixel inside it
+    const bool cm = !BF && p.cm1;
+    const int rowb = cm ? 32 : p.C1 * (b2 ? 2 : 4);
+    const int plane = cm ? (int)(p.bytes1 / (unsigned)(p.C1 / 8)) : 32;
     auto halo_voff = [&](int i) {
         // RT = 2: recomputed at every issue from an opaque copy of the lane index (hoisted out of the chunk
         // loop, the offsets of all NI instructions spilled beside the doubled accumulators; k_conv3m's note)
@@ -117,7 +121,7 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
         for (int q = 0; q < NIH; ++q) {
             if (q < q0 || q >= q1) continue;
             const int i = 2 * q + hw;
-            if (i < NI) q_dma16(r1, smd + buf * HB + i * 1024, halo_voff(i), (b2 ? 16 : 32) * j);
+            if (i < NI) q_dma16(r1, smd + buf * HB + i * 1024, halo_voff(i), (b2 ? 16 : plane) * j);
         }
     };
     // ---- weight pairs (waves 0-1): pair k = k-steps 2k, 2k + 1 -> ring slot k & 1; wave w moves KB [6 w, 6 w + 6)
@@ -351,7 +355,8 @@ bool conv4s2g_applies(const ConvParams& p, int cout_pad) {
            p.Hi == p.H && p.Wi == p.W && (p.Wo == 16 || p.Wo == 32 || p.Wo == 64 || (p.Wo == 128 && p.bf == 2)) &&
            p.H == 2 * p.Ho &&
            p.W == 2 * p.Wo && p.HoWo % Q_TP == 0 && cout_pad % 96 == 0 && p.Cin % 8 == 0 && p.C2 == 0 &&
-           p.x2 == nullptr && p.kpad == 16 * p.Cin && p.osy == 1 && p.osx == 1 && p.sc1 == nullptr;
+           p.x2 == nullptr && p.kpad == 16 * p.Cin && p.osy == 1 && p.osx == 1 && p.sc1 == nullptr &&
+           !(p.cm1 && p.bf) && !p.cm2;
 }
 
 int launch_conv4s2g(ConvParams& p, int cout_pad, hipStream_t st) {

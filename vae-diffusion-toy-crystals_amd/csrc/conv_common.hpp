@@ -40,6 +40,9 @@ struct ConvParams {
     // bf16 single-product mode (h2.hpp): the records hold bf16 halves, weights unscaled, one
     // v_mfma_f32_32x32x16_bf16 (hi x hi) per product instead of three f16 ones
     int bf;
+    // chunk-major h2 sources (round 5): [C/8][B][H][W][32 B], one plane of h2 records per 8 channels,
+    // read by k_conv4s2g (source 1) and k_conv3m (source 2) only
+    int cm1, cm2;
 };
 
 // Halo-staged 3x3 kernel (conv3h.hip): applicability test and launcher for tcx_conv2d_h2.

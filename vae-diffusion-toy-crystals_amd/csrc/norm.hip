@@ -807,6 +807,77 @@ __global__ __launch_bounds__(256) void k_gn_apply_tab_h2(const float* x, char* y
     h2_flag(ovf, bad && !bf);
 }
 
+// GroupNorm + SiLU apply from tables into CHUNK-MAJOR h2 records (round 5): y = [C/8][Bt * HW][32 B], one
+// plane of records per 8 channels, for the skip tensors h1 / h2 (read by the 4x4/s2 downsample as source 1
+// and by the up-path concat conv as source 2: ConvParams::cm1 / cm2).  A pixel-major record source makes the
+// downsample's halo DMA fetch 32 B at a stride of C * 4 B (its LDS staging re-fetches every line; DESIGN
+// §3l); a plane is contiguous.  Out of place: one workgroup per CM_NR * 256 records (1536 / (C / 8) pixels
+// of one image) reads pixel-major (coalesced), transposes the records through LDS and stores each plane's
+// run of pixels contiguously.
+constexpr int CM_NR = 6;  // records per thread
+
+__global__ __launch_bounds__(256) void k_gn_apply_cm(const float* __restrict__ x, char* __restrict__ y, int HW,
+                                                     int C, const float* __restrict__ tsc,
+                                                     const float* __restrict__ tsh, unsigned* ovf) {
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    const int C8 = C / 8;
+    const int tpx = 256 * CM_NR / C8;  // pixels per workgroup
+    const int rs = tpx * 32 + 16;      // LDS bytes per plane row (+16: consecutive planes on other banks)
+    float* sc = lsm;
+    float* sh = lsm + C;
+    char* rec = reinterpret_cast<char*>(lsm + 2 * C);
+    const int b = blockIdx.y, tid = threadIdx.x;
+    for (int c = tid; c < C; c += 256) {
+        sc[c] = tsc[(size_t)b * C + c];
+        sh[c] = tsh[(size_t)b * C + c];
+    }
+    const size_t pix0 = (size_t)b * HW + (size_t)blockIdx.x * tpx;
+    const float* src = x + pix0 * C;
+    float4 v0[CM_NR], v1[CM_NR];
+#pragma unroll
+    for (int k = 0; k < CM_NR; ++k) {
+        const float* q = src + (size_t)(tid + 256 * k) * 8;
+        v0[k] = *reinterpret_cast<const float4*>(q);
+        v1[k] = *reinterpret_cast<const float4*>(q + 4);
+    }
+    __syncthreads();
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < CM_NR; ++k) {
+        const int idx = tid + 256 * k;
+        const int px = idx / C8, c8 = idx - px * C8, c0 = 8 * c8;
+        float4 a = v0[k], d = v1[k];
+        a.x = silu_hw(fmaf(a.x, sc[c0], sh[c0]));         a.y = silu_hw(fmaf(a.y, sc[c0 + 1], sh[c0 + 1]));
+        a.z = silu_hw(fmaf(a.z, sc[c0 + 2], sh[c0 + 2])); a.w = silu_hw(fmaf(a.w, sc[c0 + 3], sh[c0 + 3]));
+        d.x = silu_hw(fmaf(d.x, sc[c0 + 4], sh[c0 + 4])); d.y = silu_hw(fmaf(d.y, sc[c0 + 5], sh[c0 + 5]));
+        d.z = silu_hw(fmaf(d.z, sc[c0 + 6], sh[c0 + 6])); d.w = silu_hw(fmaf(d.w, sc[c0 + 7], sh[c0 + 7]));
+        // the SiLU product rounded to fp32 before the split (as k_gn_apply_tab_h2, whose silu branch keeps
+        // it apart): straight-line, hipcc would contract SiLU's last multiply with split1's v - hi
+        asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w), "+v"(d.x), "+v"(d.y), "+v"(d.z), "+v"(d.w));
+        uint2 h0, l0, h1, l1;
+        split4x(a, h0, l0, false);
+        split4x(d, h1, l1, false);
+        char* r = rec + c8 * rs + px * 32;
+        *reinterpret_cast<uint4*>(r) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+        *reinterpret_cast<uint4*>(r + 16) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+        bad = bad || h2_bad(a.x) || h2_bad(a.y) || h2_bad(a.z) || h2_bad(a.w) || h2_bad(d.x) || h2_bad(d.y) ||
+              h2_bad(d.z) || h2_bad(d.w);
+    }
+    __syncthreads();
+    const size_t npix = (size_t)gridDim.y * HW;  // pixels per plane
+#pragma unroll
+    for (int k = 0; k < CM_NR; ++k) {
+        const int idx = tid + 256 * k;
+        const int c8 = idx / tpx, px = idx - c8 * tpx;
+        const char* r = rec + c8 * rs + px * 32;
+        const uint4 hi = *reinterpret_cast<const uint4*>(r), lo = *reinterpret_cast<const uint4*>(r + 16);
+        char* g = y + ((size_t)c8 * npix + pix0 + px) * 32;
+        *reinterpret_cast<uint4*>(g) = hi;
+        *reinterpret_cast<uint4*>(g + 16) = lo;
+    }
+    h2_flag(ovf, bad);
+}
+
 // The attention block's input side in one pass per image (round 5; sde_score_model.py:130-157 with the
 // mid block's last GroupNorm+SiLU): x = silu(GN_mid(a)) is written back in place as the fp32 residual,
 // the attn.norm statistics of x are summed (fp64) while x is still in registers, the attn.norm tables
@@ -1113,6 +1184,23 @@ int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const fl
     return check_launch("tcx_upsample2x_h2");
 }
 
+bool gn_apply_cm_ok(int HW, int C) {
+    if (C % 8 != 0) return false;
+    const int c8 = C / 8;
+    return 256 * CM_NR % c8 == 0 && HW % (256 * CM_NR / c8) == 0;
+}
+
+int gn_apply_cm(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift,
+                unsigned* ovf, hipStream_t st) {
+    TCX_REQUIRE(x && y && scale && shift && (const void*)x != y && aligned16(x) && aligned16(y) && gn_apply_cm_ok(HW, C),
+                "gn_apply_cm: needs distinct 16-B aligned buffers, C %% 8 == 0 and whole workgroup tiles");
+    if (Bt == 0) return TCX_OK;
+    const int tpx = 256 * CM_NR / (C / 8);
+    const size_t shm = (size_t)2 * C * sizeof(float) + (size_t)(C / 8) * (tpx * 32 + 16);
+    hipLaunchKernelGGL(k_gn_apply_cm, dim3(HW / tpx, Bt), dim3(256), shm, st, x, (char*)y, HW, C, scale, shift, ovf);
+    return check_launch("gn_apply_cm");
+}
+
 int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
                     unsigned* ovf, int bf, hipStream_t st) {
     TCX_REQUIRE(x && y && scale && shift && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_gn_apply_tab_h2: bad args");
@@ -1185,6 +1273,11 @@ extern "C" int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, 
 extern "C" int tcx_upsample2x_bf16(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
                                    const float* shift, void* stream) {
     return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, nullptr, 1, (hipStream_t)stream);
+}
+
+extern "C" int tcx_gn_apply_tab_h2_cm(const float* x, void* y, int Bt, int HW, int C, const float* scale,
+                                      const float* shift, unsigned* ovf, void* stream) {
+    return gn_apply_cm(x, y, Bt, HW, C, scale, shift, ovf, (hipStream_t)stream);
 }
 
 extern "C" int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale,

@@ -28,6 +28,9 @@ int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float*
                     unsigned* ovf, int bf, hipStream_t st);
 int gn_apply_b2_inplace(void* x, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
                         hipStream_t st);
+bool gn_apply_cm_ok(int HW, int C);  // norm.hip: chunk-major skip-tensor records
+int gn_apply_cm(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift,
+                unsigned* ovf, hipStream_t st);
 int attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads, int bf, hipStream_t st);
 }
 
@@ -1037,6 +1040,25 @@ bool attn_prep_enabled() {
     return on;
 }
 
+// TCX_SKIP_CM=0: the skip tensors h1 / h2 as pixel-major records (the in-place apply pass), A/B;
+// 1 / 2: h1 / h2 only chunk-major (default 3: both)
+int skip_cm_mask() {
+    static const int m = [] {
+        const char* e = getenv("TCX_SKIP_CM");
+        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
+    }();
+    return m;
+}
+
+// a skip tensor (H x W x C) can be chunk-major when both readers take it: the downsample on k_conv4s2g
+// (fragment-ordered 4x4 weights, Wo in {16, 32, 64}) and the concat conv on k_conv3m (fragment-ordered 3x3
+// weights, rows of 16 / 32 / 64 px, Cin = 2 C <= 384, Cout a multiple of 96), neither with a prologue
+bool skip_cm_ok(const tcx_conv& ds, const tcx_conv& cat, int H, int W, int C, bool pro) {
+    return !pro && gn_apply_cm_ok(H * W, C) && ds.whf && cat.whf && ds.ks == 4 && cat.ks == 3 && H % 2 == 0 &&
+           (W == 32 || W == 64) && (H * W / 4) % 128 == 0 && ds.cout_pad % 96 == 0 && 2 * C <= 384 &&
+           C % 16 == 0 && cat.cout_pad % 96 == 0 && cat.cout % 96 == 0 && (H * W) % 256 == 0;
+}
+
 // TCX_ATTN_SPLIT=0 keeps the split evaluator's attention on fp32 MFMA (A/B measurements)
 bool attn_split_enabled() {
     static const bool on = [] {
@@ -1208,22 +1230,41 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         }
     }
     if (!first_fused) TCX_TRY(norm(0, P.a64, P.P0, C));
-    TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.h1, gn, &ns, st,
-                    SC(0), SH(0), nullptr, nullptr, h2, pre_b2));
-    TCX_TRY(norm(1, P.h1, P.P0, C));  // h1 stays raw; its two consumers apply table 1
+    // Chunk-major skip tensors (round 5, TCX_SKIP_CM=0 off): silu(gn(h1)) / silu(gn(h2)) are written as
+    // [C/8][Bt*HW][32 B] record planes (gn_apply_cm) for their two readers, the 4x4/s2 downsample (source 1,
+    // whose halo DMA re-fetched pixel-major lines) and the up-path concat conv on k_conv3m (source 2).  The
+    // raw conv output goes to a buffer that is free at that point (b64 / a32) and the apply writes h1 / h2.
+    const bool cm1 = h2.on && fmt == 0 && (skip_cm_mask() & 1) && skip_cm_ok(net->ds1, net->up1_0, H, W, C, pro[1]);
+    const bool cm2 = h2.on && fmt == 0 && (skip_cm_mask() & 2) && skip_cm_ok(net->ds2, net->up2_0, H1, W1, C2, pro[3]);
+    H2Ctx h2cs = h2, h2cc = h2;  // h2 with the chunk-major bits: source 1 (downsample), source 2 (concat)
+    h2cs.fmt |= 16;
+    h2cc.fmt |= 32;
+    TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, cm1 ? P.b64 : P.h1, gn,
+                    &ns, st, SC(0), SH(0), nullptr, nullptr, h2, pre_b2));
+    if (cm1) {
+        TCX_TRY(gn_tab(net, P, 1, P.P0, C, gn, ns, st));
+        TCX_TRY(gn_apply_cm(P.b64, P.h1, Bt, P.P0, C, P.sc(1), P.sh(1), h2.ovf, st));
+    } else {
+        TCX_TRY(norm(1, P.h1, P.P0, C));  // h1 stays raw; its two consumers apply table 1
+    }
     // ds1: 4x4/s2 circular on silu(gn(h1))
     TCX_TRY(conv_gn(net->ds1, P.h1, nullptr, C, 0, Bt, 0, H, W, 2, 1, nullptr, nullptr, P.a32, nullptr, &ns, st,
-                    SC(1), SH(1), nullptr, nullptr, h2, 1));
+                    SC(1), SH(1), nullptr, nullptr, cm1 ? h2cs : h2, 1));
     // down2
     TCX_TRY(conv_gn(net->down2_0, P.a32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st,
                     nullptr, nullptr, nullptr, nullptr, h2, pre_b2));
     TCX_TRY(norm(2, P.b32, P.P1, C2));
-    TCX_TRY(conv_gn(net->down2_1, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.h2, gn, &ns, st,
-                    SC(2), SH(2), nullptr, nullptr, h2, pre_b2));
-    TCX_TRY(norm(3, P.h2, P.P1, C2));  // h2 raw; consumers apply table 3
+    TCX_TRY(conv_gn(net->down2_1, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, cm2 ? P.a32 : P.h2, gn,
+                    &ns, st, SC(2), SH(2), nullptr, nullptr, h2, pre_b2));
+    if (cm2) {
+        TCX_TRY(gn_tab(net, P, 3, P.P1, C2, gn, ns, st));
+        TCX_TRY(gn_apply_cm(P.a32, P.h2, Bt, P.P1, C2, P.sc(3), P.sh(3), h2.ovf, st));
+    } else {
+        TCX_TRY(norm(3, P.h2, P.P1, C2));  // h2 raw; consumers apply table 3
+    }
     // ds2
     TCX_TRY(conv_gn(net->ds2, P.h2, nullptr, C2, 0, Bt, 0, H1, W1, 2, 1, nullptr, nullptr, P.a16, nullptr, &ns, st,
-                    SC(3), SH(3), nullptr, nullptr, h2, 1));
+                    SC(3), SH(3), nullptr, nullptr, cm2 ? h2cs : h2, 1));
     // mid
     TCX_TRY(conv_gn(net->mid_0, P.a16, nullptr, C2, 0, Bt, 0, H2, W2, 1, 1, nullptr, nullptr, P.b16, gn, &ns, st,
                     nullptr, nullptr, nullptr, nullptr, h2, pre_b2));
@@ -1272,7 +1313,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                     nullptr, nullptr, nullptr, nullptr, h2, 1));
     // up2 on cat[a32, silu(gn(h2))]
     TCX_TRY(conv_gn(net->up2_0, P.a32, P.h2, C2, C2, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st,
-                    nullptr, nullptr, SC(3), SH(3), h2, pre_b2));
+                    nullptr, nullptr, SC(3), SH(3), cm2 ? h2cc : h2, pre_b2));
     TCX_TRY(norm(7, P.b32, P.P1, C));
     TCX_TRY(conv_gn(net->up2_1, P.b32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, gn, &ns, st,
                     SC(7), SH(7), nullptr, nullptr, h2));
@@ -1292,7 +1333,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                     nullptr, nullptr, nullptr, nullptr, h2, 1));
     // up1 on cat[a64, silu(gn(h1))]
     TCX_TRY(conv_gn(net->up1_0, P.a64, P.h1, C, C, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.b64, gn, &ns, st, nullptr,
-                    nullptr, SC(1), SH(1), h2, pre_b2));
+                    nullptr, SC(1), SH(1), cm1 ? h2cc : h2, pre_b2));
     TCX_TRY(norm(9, P.b64, P.P0, C));
     TCX_TRY(conv_gn(net->up1_1, P.b64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, P.a64, gn, &ns, st,
                     SC(9), SH(9), nullptr, nullptr, h2, pre_b2));  // b2: the head reads it as bf16

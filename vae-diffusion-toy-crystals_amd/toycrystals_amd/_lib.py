@@ -108,6 +108,7 @@ _SIGS = {
     "tcx_conv_weight_h2_frag4_bytes": (c_size, [c_int, c_int]),
     "tcx_pack_conv_weight_h2_frag4": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp]),
     "tcx_gn_apply_tab_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp, c_fp]),
+    "tcx_gn_apply_tab_h2_cm": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
     "tcx_upsample2x_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
     "tcx_attention_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),
     "tcx_attention_split": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
