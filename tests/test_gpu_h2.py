@@ -596,3 +596,36 @@ def test_gn_apply_chunk_major_equals_pixel_major(B, HW, C):
     nbad = int((a != b).sum())
     print(f"chunk-major apply: {nbad} of {a.size} words differ")
     assert nbad == 0 and int(ovf.item()) == 0
+
+
+@pytest.mark.parametrize("B,Ci,Co,H,ks", [
+    (2, 96, 96, 64, 3), (2, 192, 192, 32, 3), (2, 192, 192, 16, 3),  # k_conv3m (us1 / us2 convs write h2)
+    (2, 96, 96, 64, 4), (2, 192, 192, 32, 4),  # k_conv4s2g (ds1 / ds2)
+    (2, 192, 576, 16, 1),  # k_lin1x1 (qkv)
+])
+def test_conv_h2_output_equals_split_of_fp32_output(B, Ci, Co, H, ks):
+    """An h2-output conv (16-B paired record stores, store_h2_pair) writes exactly tcx_f32_to_h2 of the
+    same conv's fp32 output, word for word."""
+    x = rng.standard_normal((B, Ci, H, H))
+    w = rng.standard_normal((Co, Ci, ks, ks)) / np.sqrt(Ci * ks * ks)
+    b = dev(rng.standard_normal(Co))
+    wh, ws, cpad, kpad = pack_h2(w)
+    wf = pack_frag(wh, cpad, kpad, Ci) if ks in (3, 4) else None
+    stride, pad = (2, 1) if ks == 4 else (1, ks // 2)
+    Ho = H // stride
+    xd = to_h2(dev(nhwc(x)))
+
+    def run(out_h2):
+        y = torch.full((B, Ho, Ho, Co), float("nan"), device="cuda")
+        ovf = torch.zeros(1, dtype=torch.int32, device="cuda")
+        chk(L().tcx_conv2d_h2_pro(xd.data_ptr(), None, B, 0, H, H, Ci, 0, wh.data_ptr(),
+                                  wf.data_ptr() if wf is not None else None, ws.data_ptr(), b.data_ptr(), None, None,
+                                  y.data_ptr(), out_h2, Co, cpad, kpad, ks, stride, pad, 1, 0, None, None, None, None,
+                                  None, 0, ovf.data_ptr(), st()))
+        return y
+
+    want = to_h2(run(0)).view(torch.int32).cpu().numpy()
+    got = run(1).view(torch.int32).cpu().numpy()
+    nbad = int((want != got).sum())
+    print(f"h2 output vs split fp32 output: {nbad} of {want.size} words differ")
+    assert nbad == 0

@@ -647,6 +647,11 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
                 "tcx_conv2d_h2: prologue tables come in scale/shift pairs per source");
     p.sc1 = pro_scale1; p.sh1 = pro_shift1; p.sc2 = pro_scale2; p.sh2 = pro_shift2;
     p.wf = wfrag;
+    static const int h2pair = [] {
+        const char* e = getenv("TCX_H2_PAIR");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    p.h2pair = h2pair;
     p.bf = bf16;  // k_conv3p / k_conv3h have no bf16 form: those shapes take the im2col kernel
     if (bf16 == 2) {
         // 2-byte bf16 tensors (config 5 at 256^2): only the LDS-DMA kernels read them

@@ -581,10 +581,13 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
                     const unsigned hi0 = (a0 & 0xffffu) | (a1 << 16), hi1 = (a2 & 0xffffu) | (a3 << 16);
                     const unsigned lo0 = (a0 >> 16) | (a1 & 0xffff0000u), lo1 = (a2 >> 16) | (a3 & 0xffff0000u);
                     const int sh = (16 * rb * p.Cout + 16 * nb) * 4;  // 16 channels = two whole records
-                    __builtin_amdgcn_raw_buffer_store_b64((u32x2){hi0, hi1},
-                                                          ry, voh, sh, 0);
-                    __builtin_amdgcn_raw_buffer_store_b64((u32x2){lo0, lo1},
-                                                          ry, voh + 16, sh, 0);
+                    if (p.h2pair) {
+                        store_h2_pair((u32x2_h2){hi0, hi1}, (u32x2_h2){lo0, lo1}, (qc & 1) != 0, ry,
+                                      voh - (qc & 1) * 8, sh);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b64((u32x2){hi0, hi1}, ry, voh, sh, 0);
+                        __builtin_amdgcn_raw_buffer_store_b64((u32x2){lo0, lo1}, ry, voh + 16, sh, 0);
+                    }
                     bad = bad || h2_bad(v[0]) || h2_bad(v[1]) || h2_bad(v[2]) || h2_bad(v[3]);
                 } else {
                     store_b128_guarded(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry, vo32, so);

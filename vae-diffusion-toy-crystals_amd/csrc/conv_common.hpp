@@ -43,6 +43,8 @@ struct ConvParams {
     // chunk-major h2 sources (round 5): [C/8][B][H][W][32 B], one plane of h2 records per 8 channels,
     // read by k_conv4s2g (source 1) and k_conv3m (source 2) only
     int cm1, cm2;
+    // h2 outputs as one 16-B store per lane pair half (store_h2_pair; TCX_H2_PAIR=0: two 8-B stores)
+    int h2pair;
 };
 
 // Halo-staged 3x3 kernel (conv3h.hip): applicability test and launcher for tcx_conv2d_h2.
@@ -150,6 +152,20 @@ __device__ __forceinline__ void store_b128_guarded(u32x4 v, __amdgpu_buffer_rsrc
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 1");
     __builtin_amdgcn_sched_barrier(0);
+}
+
+// Store of one lane's 4 channels of an h2 record (hi, lo: 8 B each) after quad_transpose4, where lane ^ 4
+// holds the record's other 4 channels: the lanes swap 8 B (ds_swizzle, xor 4) so the even lane (`odd`
+// false) stores the record's 16-B hi half and the odd lane its lo half — one 16-B store per lane, the fp32
+// output's instruction count, instead of two 8-B stores.  vrec: byte offset of the record.
+typedef unsigned int u32x2_h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void store_h2_pair(u32x2_h2 hi, u32x2_h2 lo, bool odd, __amdgpu_buffer_rsrc_t r, int vrec,
+                                              int soff) {
+    const int s0 = (int)(odd ? hi.x : lo.x), s1 = (int)(odd ? hi.y : lo.y);
+    const unsigned r0 = (unsigned)__builtin_amdgcn_ds_swizzle(s0, 0x101F);  // and 0x1F, xor 4
+    const unsigned r1 = (unsigned)__builtin_amdgcn_ds_swizzle(s1, 0x101F);
+    const u32x4 v = odd ? (u32x4){r0, r1, lo.x, lo.y} : (u32x4){hi.x, hi.y, r0, r1};
+    store_b128_guarded(v, r, vrec + (odd ? 16 : 0), soff);
 }
 
 // 4x4 transpose across the 4 lanes of a DPP quad (lane i = lane & 3): element r of lane i becomes
@@ -319,8 +335,13 @@ __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 
                                    a3 = split1x(v[3], bf);
                     const u32x2_ hi = {(a0 & 0xffffu) | (a1 << 16), (a2 & 0xffffu) | (a3 << 16)};
                     const u32x2_ lo = {(a0 >> 16) | (a1 & 0xffff0000u), (a2 >> 16) | (a3 & 0xffff0000u)};
-                    __builtin_amdgcn_raw_buffer_store_b64(hi, ry, voh, so, 0);
-                    __builtin_amdgcn_raw_buffer_store_b64(lo, ry, voh + 16, so, 0);
+                    if (p.h2pair) {
+                        store_h2_pair((u32x2_h2){hi.x, hi.y}, (u32x2_h2){lo.x, lo.y}, (qc & 1) != 0, ry,
+                                      voh - (qc & 1) * 8, so);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b64(hi, ry, voh, so, 0);
+                        __builtin_amdgcn_raw_buffer_store_b64(lo, ry, voh + 16, so, 0);
+                    }
                     bad = bad || (!bf && (h2_bad(v[0]) || h2_bad(v[1]) || h2_bad(v[2]) || h2_bad(v[3])));
                 } else {
                     store_b128_guarded<SPL == 2 ? EPI_NT : 0>(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry, vo32, so);
