@@ -61,3 +61,11 @@ def test_chunk_major_skips_bit_identical(tmp_path, H):
     a = _forward(tmp_path, "cm", {"TCX_SKIP_CM": "3"}, "f16x3", 64, H)
     b = _forward(tmp_path, "pm", {"TCX_SKIP_CM": "0"}, "f16x3", 64, H)
     assert np.array_equal(a, b)
+
+
+def test_conv3m_h2_output_form_bit_identical(tmp_path):
+    """k_conv3m's PRO 3 form (h2 output, no activation: the us1 / us2 convs) against the generic epilogue
+    (TCX_CONV3M_OH2=0): the same values, the same stores; the whole 64^2 forward is bit-identical."""
+    a = _forward(tmp_path, "oh2", {"TCX_CONV3M_OH2": "1"}, "f16x3", 64, 64)
+    b = _forward(tmp_path, "gen", {"TCX_CONV3M_OH2": "0"}, "f16x3", 64, 64)
+    assert np.array_equal(a, b)

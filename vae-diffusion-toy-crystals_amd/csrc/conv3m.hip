@@ -196,6 +196,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
         if constexpr (PRO != 2) return yo + x * rb + 16 * pc;  // pixel-major only (rb = rowb, ph = 32)
         else return yo + x * rb + 16 * (pc & 1) + (pc >> 1) * ph;
     };
+    // PRO 3: PRO 0 with an h2 output and no activation (the epilogue's h2 path straight-line)
     // PRO 2 (p.cm2): PRO 0 with source 2 chunk-major, the 16-channel chunk two planes of 32-B pixel records
     const int plane2 = PRO == 2 ? (int)(p.bytes2 / (unsigned)(p.C2 / 8)) : 0;
     // third `th` (0..2) of chunk j's halo into buffer buf
@@ -576,7 +577,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
                 }
                 quad_transpose4(v, qi);
                 const int so = (16 * rb * p.Cout + 16 * nb) * 4;
-                if (!FAST && p.out_h2) {
+                if ((!FAST && p.out_h2) || PRO == 3) {
                     const unsigned a0 = split1(v[0]), a1 = split1(v[1]), a2 = split1(v[2]), a3 = split1(v[3]);
                     const unsigned hi0 = (a0 & 0xffffu) | (a1 << 16), hi1 = (a2 & 0xffffu) | (a3 << 16);
                     const unsigned lo0 = (a0 >> 16) | (a1 & 0xffff0000u), lo1 = (a2 >> 16) | (a3 & 0xffff0000u);
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
                     store_b128_guarded(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry, vo32, so);
                 }
             }
-            if constexpr (!FAST) h2_flag(p.ovf, bad);
+            if constexpr (!FAST || PRO == 3) h2_flag(p.ovf, bad);
             if (p.gn) {
                 double ds = (double)s, dss = (double)ss;
                 ds += __shfl_xor(ds, 16);
@@ -634,14 +635,25 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     }
 }
 
+// TCX_CONV3M_OH2=0: h2-output convs on the generic epilogue (FAST false) instead of PRO 3 (A/B)
+bool conv3m_oh2_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("TCX_CONV3M_OH2");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <int W>
 int launch3m(const ConvParams& p, hipStream_t st) {
-    static bool attr[4] = {};
+    static bool attr[5] = {};
     const bool pro = p.sc1 != nullptr;
     const bool fast = p.act == 0 && !p.out_h2;
-    const int ai = pro ? 2 : p.cm2 ? 3 : (int)fast;
+    const bool oh2 = p.act == 0 && p.out_h2 && !p.cm2 && conv3m_oh2_enabled();  // PRO 3: h2 output, no act
+    const int ai = pro ? 2 : p.cm2 ? 3 : oh2 ? 4 : (int)fast;
     void (*const k)(ConvParams) = pro ? &k_conv3m<W, true, 1>
                                   : p.cm2 ? &k_conv3m<W, true, 2>
+                                  : oh2 ? &k_conv3m<W, true, 3>
                                   : fast ? &k_conv3m<W, true, 0> : &k_conv3m<W, false, 0>;
     const size_t lds = pro ? conv3m_lds_bytes<W, 1>() : conv3m_lds_bytes<W, 0>();
     if (!attr[ai]) {
