@@ -326,8 +326,8 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     auto t_valA = [&](int k) __attribute__((always_inline)) {
         if (k == 0) __builtin_amdgcn_s_waitcnt(M_WAIT_LGKM0);  // the unit's asm reads (t_load)
         const int q = k >> 1, e = k & 1;
-        ux[k] = fmaf(ux[k], tsc[q & 1][e], tsh[q & 1][e]);
-        ue[k & 1] = __builtin_amdgcn_exp2f(-1.4426950408889634f * ux[k]);
+        ux[k] = fmaf(ux[k], tsc[q & 1][e], tsh[q & 1][e]);  // u = -log2(e) t (the tables' staging)
+        ue[k & 1] = __builtin_amdgcn_exp2f(ux[k]);
     };
     auto t_valB = [&](int k) __attribute__((always_inline)) { ux[k] = ux[k] * __builtin_amdgcn_rcpf(1.0f + ue[k & 1]); };
     auto t_val = [&](int k) __attribute__((always_inline)) {
@@ -388,9 +388,13 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     }
     if constexpr (PRO == 1) {
         float* const Twr = reinterpret_cast<float*>(smc + TAB);
+        // staged as -log2(e) * (scale, shift): the transform's fma gives u = -log2(e) t (t the GroupNorm
+        // value), exp2(u) = e^-t directly, and it stages u / (1 + e^-t) = -log2(e) silu(t); the constant
+        // factor of every input of this single-source conv comes out in the epilogue (wscale * -ln 2).
+        // One multiply per value fewer than the t-based form, no register for a constant
         for (int c = tid; c < p.C1; c += 64 * M_NW) {
-            Twr[c] = p.sc1[(size_t)b * p.C1 + c];
-            Twr[p.C1 + c] = p.sh1[(size_t)b * p.C1 + c];
+            Twr[c] = -1.4426950408889634f * p.sc1[(size_t)b * p.C1 + c];
+            Twr[p.C1 + c] = -1.4426950408889634f * p.sh1[(size_t)b * p.C1 + c];
         }
     }
     __builtin_amdgcn_s_waitcnt(M_WAIT_VM0);
@@ -544,7 +548,8 @@ __global__ __launch_bounds__(64 * M_NW, 2) void k_conv3m(ConvParams p) {
     double* red = reinterpret_cast<double*>(sm);
     {
         const int col = lane & 15, rg = lane >> 4, qi = lane & 3, qc = col >> 2;
-        const float wsc = *p.wscale;
+        // PRO 1: the staged inputs are -log2(e) silu(.) (the transform's tables)
+        const float wsc = PRO == 1 ? *p.wscale * -0.6931471805599453f : *p.wscale;
         const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, (unsigned)((long long)p.M * p.Cout * 4));
         const int rowo = p.Cout * 4;
         const int pixq = m0 + 64 * wv + 4 * rg + qi;  // this lane's pixel after the transpose (row block 0)
