@@ -34,13 +34,13 @@ LAYERS = [
     ("down1.net.0 conv 1->96 + GN0 + SiLU -> records", mem(BT * P0 * C * E4)),
     ("down1.net.3 conv (down1_1)", conv(P0, C, C, 9)),
     ("fin 1", None),
-    ("apply GN1+SiLU -> h2 (skip h1)", mem(2 * BT * P0 * C * E4)),
+    ("apply GN1+SiLU -> h2 (skip h1, chunk-major)", mem(2 * BT * P0 * C * E4)),
     ("ds1 4x4/s2", conv(P1, C, C, 16)),
     ("down2.net.0 conv (down2_0)", conv(P1, C, C2, 9)),
     ("fin 2", None),
     ("down2.net.3 conv, GN2 prologue (down2_1)", conv(P1, C2, C2, 9)),
     ("fin 3", None),
-    ("apply GN3+SiLU -> h2 (skip h2)", mem(2 * BT * P1 * C2 * E4)),
+    ("apply GN3+SiLU -> h2 (skip h2, chunk-major)", mem(2 * BT * P1 * C2 * E4)),
     ("ds2 4x4/s2", conv(P2, C2, C2, 16)),
     ("mid.net.0 conv (mid_0)", conv(P2, C2, C2, 9)),
     ("fin 4", None),
