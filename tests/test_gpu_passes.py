@@ -69,3 +69,13 @@ def test_conv3m_h2_output_form_bit_identical(tmp_path):
     a = _forward(tmp_path, "oh2", {"TCX_CONV3M_OH2": "1"}, "f16x3", 64, 64)
     b = _forward(tmp_path, "gen", {"TCX_CONV3M_OH2": "0"}, "f16x3", 64, 64)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("prec", ["f16x3", "bf16"])
+def test_quad_epilogue_static_output_form_bit_identical(tmp_path, prec):
+    """The quad epilogue with its output form compiled in (fp32 / h2 records / 2-byte bf16: the
+    downsamples, the 1x1 convs, k_conv3lb) against the run-time choice (TCX_EPI_STATIC=0): the whole
+    forward is bit-identical."""
+    a = _forward(tmp_path, "st", {"TCX_EPI_STATIC": "1"}, prec, 64, 64)
+    b = _forward(tmp_path, "rt", {"TCX_EPI_STATIC": "0"}, prec, 64, 64)
+    assert np.array_equal(a, b)

@@ -652,6 +652,11 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
         return (e && e[0] == '0') ? 0 : 1;
     }();
     p.h2pair = h2pair;
+    static const int epi_static = [] {
+        const char* e = getenv("TCX_EPI_STATIC");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    p.epi_static = epi_static;
     p.bf = bf16;  // k_conv3p / k_conv3h have no bf16 form: those shapes take the im2col kernel
     if (bf16 == 2) {
         // 2-byte bf16 tensors (config 5 at 256^2): only the LDS-DMA kernels read them

@@ -45,6 +45,8 @@ struct ConvParams {
     int cm1, cm2;
     // h2 outputs as one 16-B store per lane pair half (store_h2_pair; TCX_H2_PAIR=0: two 8-B stores)
     int h2pair;
+    // quad epilogue with the output form compiled in (conv_epi_store_quad OUT; TCX_EPI_STATIC=0: run time)
+    int epi_static;
 };
 
 // Halo-staged 3x3 kernel (conv3h.hip): applicability test and launcher for tcx_conv2d_h2.
@@ -282,7 +284,10 @@ __device__ __forceinline__ void conv_epi_store_cols(const ConvParams& p, f32x16 
 // one 16-B store (fp32) or two 8-B stores (the hi and lo halves of the h2 record) per lane and group,
 // 4 instead of 16 store instructions per 32x32 block.  ACT: the activation is a run-time branch
 // (false: none, straight-line code).  GroupNorm partials from the columns before the transpose.
-template <int NT, int SPL, int NW, int RT, bool ACT>
+// OUT (round 5): the output form compiled in (0 fp32, 1 h2 records, 2 two-byte bf16) or -1: chosen at
+// run time per group (a run-time branch per store split k_conv3m's epilogue into blocks the scheduler
+// could not overlap: 27 us of a 440-us 64^2 conv, r05_x)
+template <int NT, int SPL, int NW, int RT, bool ACT, int OUT = -1>
 __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
                                                     int wv0, int lane, double* red) {
     constexpr int BN = 32 * NT;
@@ -296,7 +301,9 @@ __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 
 #pragma unroll
     for (int n = 0; n < NT; ++n) bco[n] = p.bias ? p.bias[n0 + n * 32 + li] : 0.f;
     const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, (unsigned)((long long)p.M * p.Cout * 4));
-    const bool b2 = p.out_h2 && p.bf == 2;  // 2-byte bf16 output (h2.hpp "b2"): one 8-B store per lane and group
+    // 2-byte bf16 output (h2.hpp "b2"): one 8-B store per lane and group
+    const bool b2 = OUT >= 0 ? OUT == 2 : (p.out_h2 && p.bf == 2);
+    const bool oh2 = OUT >= 0 ? OUT == 1 : (bool)p.out_h2;
     const int rowb = p.Cout * (b2 ? 2 : 4);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -330,7 +337,7 @@ __device__ __forceinline__ void conv_epi_store_quad(const ConvParams& p, f32x16 
                 if (b2) {
                     const u32x2_ w2 = {pack2_bf(v[0], v[1]), pack2_bf(v[2], v[3])};
                     __builtin_amdgcn_raw_buffer_store_b64(w2, ry, (pixq * p.Cout + c4) * 2, so, 0);
-                } else if (p.out_h2) {
+                } else if (oh2) {
                     const unsigned a0 = split1x(v[0], bf), a1 = split1x(v[1], bf), a2 = split1x(v[2], bf),
                                    a3 = split1x(v[3], bf);
                     const u32x2_ hi = {(a0 & 0xffffu) | (a1 << 16), (a2 & 0xffffu) | (a3 << 16)};
@@ -367,7 +374,10 @@ template <int NT, int SPL, int NW, int RT>
 __device__ __forceinline__ void conv_epi_store_fast(const ConvParams& p, f32x16 (&acc)[RT][NT], int m0, int n0,
                                                     int wv0, int lane, double* red) {
     if (p.resid) conv_epi_store_cols<NT, SPL, NW, RT>(p, acc, m0, n0, wv0, lane, red);  // attention proj
-    else if (p.act == 0) conv_epi_store_quad<NT, SPL, NW, RT, false>(p, acc, m0, n0, wv0, lane, red);
+    else if (p.act == 0 && !p.epi_static) conv_epi_store_quad<NT, SPL, NW, RT, false>(p, acc, m0, n0, wv0, lane, red);
+    else if (p.act == 0 && p.out_h2 && p.bf == 2) conv_epi_store_quad<NT, SPL, NW, RT, false, 2>(p, acc, m0, n0, wv0, lane, red);
+    else if (p.act == 0 && p.out_h2) conv_epi_store_quad<NT, SPL, NW, RT, false, 1>(p, acc, m0, n0, wv0, lane, red);
+    else if (p.act == 0) conv_epi_store_quad<NT, SPL, NW, RT, false, 0>(p, acc, m0, n0, wv0, lane, red);
     else conv_epi_store_quad<NT, SPL, NW, RT, true>(p, acc, m0, n0, wv0, lane, red);
 }
 
