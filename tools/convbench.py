@@ -107,4 +107,5 @@ for l in LAYERS:
     us, fl = r
     if l[0] not in ("us2(pre)",):
         tot_us += us; tot_fl += fl
-print(f"TOTAL {tot_us:.1f} us  {tot_fl / tot_us / 1e6:.1f} TF (mid counted once)")
+if tot_us:
+    print(f"TOTAL {tot_us:.1f} us  {tot_fl / tot_us / 1e6:.1f} TF (mid counted once)")
