@@ -285,7 +285,9 @@ size_t tcx_unet_workspace_size(const tcx_unet* net, int Bt, int H, int W);
 /* Concurrent sampling lanes of tcx_sde_sample: the batch is split into `lanes` (1-4) groups of
  * images advanced step by step on their own HIP streams (joined to the caller's stream at the
  * end); results are identical to one lane.  0 restores the TCX_LANES environment default (1).
- * Returns the previous setting.  Workspace queries made after the call size for the lanes. */
+ * Returns the previous setting.  Workspace queries made after the call size for the lanes.
+ * The setting is per host thread (query the workspace and sample on the thread that set it); the
+ * lane streams are created per device on first use, so two devices in one process never share them. */
 int tcx_set_sample_lanes(int lanes);
 
 /* Per-step scalar table used by the fused step kernels: row i = {t_i, t_{i+1}, dt, beta(t_i),
@@ -344,17 +346,24 @@ int tcx_ode_sample_ex(const tcx_unet* net, float* x, const int64_t* y_cat, const
  * U-Net workspace of the (CFG-doubled) rows under the current lane setting, the conditioning tables
  * of the call's n_steps + 1 step-table rows (time / condition maps and the per-(step, image)
  * first-conv bias rows that replace the reference's per-call _make_maps, sde_score_model.py:227-241)
- * and, for the PF-ODE, its drift / Euler-point images.  A smaller ws_bytes is TCX_EWS.  Query after
- * tcx_set_sample_lanes. */
+ * and, for the PF-ODE, its drift / Euler-point images.  A smaller ws_bytes is TCX_EWS, whose error
+ * message (tcx_last_error) carries the required size.  Query after tcx_set_sample_lanes.
+ * BREAKING CHANGE (round 5): the sampler entry points (tcx_sde_sample, tcx_sde_sample_ex,
+ * tcx_sde_sample_shard, tcx_ode_sample, tcx_ode_sample_ex) need these sizes; a workspace sized by
+ * tcx_unet_workspace_size alone (the round-1..4 contract) is now TCX_EWS, since the conditioning
+ * tables grow with n_steps and the library no longer allocates them itself. */
 size_t tcx_sde_workspace_size(const tcx_unet* net, int B, int H, int W, int n_steps, float guidance);
 size_t tcx_ode_workspace_size(const tcx_unet* net, int B, int H, int W, int n_steps, float guidance);
 
 /* Test hook for the samplers' error paths: the k-th U-Net evaluation after the call (k > 0) fails
- * with TCX_EINVAL before launching anything (one shot; 0 disarms).  Every sampler exit joins its
- * lane streams back into the caller's stream, so a failed call leaves nothing running unordered. */
+ * with TCX_EINVAL before launching anything (one shot; 0 disarms).  Per host thread: arming it never
+ * fails another thread's evaluations.  Every sampler exit joins its lane streams back into the
+ * caller's stream, so a failed call leaves nothing running unordered. */
 int tcx_debug_fail_eval(int k);
 
-/* tcx_sde_sample_ex on one shard of a larger sampling batch (batch-DP sampling):
+/* (Workspace: tcx_sde_workspace_size(net, B, H, W, n_steps, guidance) bytes — see the breaking-change
+ * note above; tcx_ode_sample_ex likewise needs tcx_ode_workspace_size.)
+ * tcx_sde_sample_ex on one shard of a larger sampling batch (batch-DP sampling):
  * the Philox counter of element i of x is e_base + i, so images [s, e) of a B-image batch sampled
  * with e_base = s*H*W are bit-identical to those rows of the whole batch sampled in one call with the
  * same seed (the reference draws ONE stream for the whole batch, sde_score_model.py:537,557).

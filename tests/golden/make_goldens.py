@@ -364,6 +364,59 @@ def gen_train_score32(name: str) -> None:
          drop=drop_u.numpy(), loss=np.float64(loss.item()), p_uncond=np.float64(0.5), base_ch=np.int64(32), **ck, **gs)
 
 
+def _param_sample(prefix: str, name: str, t: torch.Tensor, idx: np.ndarray) -> dict:
+    return {f"{prefix}/{name}": t.detach().double().reshape(-1).numpy()[idx].astype(np.float64)}
+
+
+def gen_train_score96(name: str) -> None:
+    """Config 3's width: one diffusion_loss_eps backward at base_ch=96 (the 96/192/384-
+    channel dgrad / wgrad forms and the first conv of the training path), then one torch.optim.Adam step and
+    the EMA update (train_sde_score_model.py:217-240), draws injected.  Stored: seeds, inputs, draws, the
+    loss, per-parameter gradient checksums + 64 fixed-index samples, and 64 fixed-index samples of every
+    parameter after the Adam step and of its EMA (no weights: they are rebuilt from the seed)."""
+    torch.manual_seed(0)
+    model = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=96)
+    perturb_norms(model, 5)
+    ck = sd_checksums(model)
+    ema = ref_sde.CondUNetTiny(n_types=4, y_cont_dim=4, base_ch=96)
+    ema.load_state_dict(model.state_dict())
+    sde = ref_sde.VPSDE(0.1, 30.0)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    g = torch.Generator().manual_seed(31)
+    B = 3
+    x0 = torch.rand(B, 1, 64, 64, generator=g)
+    y_cat, y_cont = cond_inputs(B, null_last=False)
+    torch.manual_seed(300)
+    u = torch.rand((B,))
+    eps = torch.randn((B, 1, 64, 64))
+    drop_u = torch.rand((B,))
+    torch.manual_seed(300)
+    loss = ref_sde.diffusion_loss_eps(model, sde, x0, y_cat, y_cont, p_uncond=0.5, t_power=1.0)
+    opt.zero_grad(set_to_none=True)
+    loss.backward()
+    gs = {}
+    rs = np.random.RandomState(96)
+    grads = {}
+    for k, p in model.named_parameters():
+        gs.update(_grad_sample(k, p.grad))
+        grads[k] = p.grad.detach().clone()
+    opt.step()
+    with torch.no_grad():
+        for pe, p in zip(ema.parameters(), model.parameters()):
+            pe.data.mul_(0.9).add_(p.data, alpha=1.0 - 0.9)
+    ps = {}
+    for (k, p), pe in zip(model.named_parameters(), ema.parameters()):
+        n = p.numel()
+        idx = np.sort(rs.choice(n, size=min(n, 64), replace=False)).astype(np.int64)
+        ps["pi/" + k] = idx
+        ps.update(_param_sample("gp", k, grads[k], idx))  # the gradient at these indices (sign reliability)
+        ps.update(_param_sample("p1", k, p, idx))
+        ps.update(_param_sample("ema1", k, pe, idx))
+    save(name, x0=x0.numpy(), y_cat=y_cat.numpy(), y_cont=y_cont.numpy(), u=u.numpy(), eps=eps.numpy(),
+         drop=drop_u.numpy(), loss=np.float64(loss.item()), p_uncond=np.float64(0.5), base_ch=np.int64(96),
+         lr=np.float64(1e-3), ema_decay=np.float64(0.9), **ck, **gs, **ps)
+
+
 def gen_train_score(name: str) -> None:
     """diffusion_loss_eps backward (all parameter grads) + two torch.optim.Adam steps + EMA
     (train_sde_score_model.py:217-240) at base_ch=16, draws recorded."""
@@ -627,6 +680,8 @@ def main() -> int:
         gen_prior("prior_w1024_b8", 1024, 8, store_weights=False)
     if want("train32"):
         gen_train_score32("train32_b4")
+    if want("train96"):
+        gen_train_score96("train96_b3")
     if want("train"):
         gen_train_score("train16_b3")
         gen_train_vae("train_condvae_b4")

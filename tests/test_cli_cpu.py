@@ -16,7 +16,7 @@ from make_cli_golden import describe  # noqa: E402  (shared describer; no refere
 
 # flags a mirror adds on top of the reference's (additive only: every reference flag is kept as is)
 ADDITIVE = {"build_dataset": {"device", "render_batch"}, "train_sde_score_model": {"global_draws"},
-            "train_vae": {"global_draws", "replay_draws"}, "train_diffusion_prior": {"global_draws"}}
+            "train_vae": {"global_draws", "replay_draws"}, "train_diffusion_prior": {"global_draws", "zero"}}
 
 
 @pytest.mark.parametrize("name", ["train_sde_score_model", "sample_sde_score_model", "train_vae",

@@ -517,3 +517,36 @@ def test_b2_256px_forward_vs_records_and_reference(tmp_path, golden):
     print(f"256^2 bf16 forward vs reference: b2 {e_b2:.2e}, records {e_rec:.2e}; b2 vs records {d:.2e}")
     assert e_b2 < 3e-2 and e_rec < 3e-2
     assert d > 0.0  # the b2 path really ran (its pre-norm rounding)
+
+
+def test_b2_head_rejects_misaligned_out_w():
+    """config 5 (256^2 bf16, b2 tensors): up1_1 writes 2-byte bf16 that only the register-weight head reads,
+    whose constant loads need out_w 16-byte aligned.  A C-ABI caller's misaligned out_w is an error with a
+    message, never a fall-through to a head that reads the b2 tensor as fp32"""
+    from toycrystals_amd import _lib
+    from toycrystals_amd.models.sde_score_model import CondUNetTiny
+    torch.manual_seed(0)
+    m = CondUNetTiny(4, 4, 96).cuda().eval()
+    B, H = 1, 256
+    x = torch.randn(B, 1, H, H, device="cuda")
+    t = torch.full((B,), 0.5, device="cuda")
+    yc = torch.zeros(B, dtype=torch.long, device="cuda")
+    yv = torch.zeros(B, 4, device="cuda")
+    prev = _lib.conv_precision()
+    _lib.set_conv_precision("bf16")
+    try:
+        with torch.no_grad():
+            good = m(x, t, yc, yv)  # aligned (the pack's own copy): runs
+            pk = m.tcx_pack(x.device)
+            keep = pk.net.out_w
+            buf = torch.zeros(96 * 9 + 4, device="cuda")  # the head weights' size, one float past 16 B
+            pk.net.out_w = buf.data_ptr() + 4
+            try:
+                with pytest.raises(_lib.TcxError, match="aligned"):
+                    m(x, t, yc, yv)
+            finally:
+                pk.net.out_w = keep
+            again = m(x, t, yc, yv)
+    finally:
+        _lib.set_conv_precision(prev)
+    assert torch.equal(good, again)  # the library state is intact after the rejected call

@@ -148,22 +148,30 @@ def test_vae_and_prior_scripts_world2_equal_world1(tmp_path, dataset):
         assert len(a) == len(b) == 2 and all(abs(x - y) <= 1e-4 * max(abs(x), 1e-3) for x, y in zip(a, b)), key
     assert out[2].count("epoch 02/2 loss=") == 1
 
-    prior_args = ["--data-path", dataset, "--epochs", 2, "--batch-size", 32, "--width", 256, "--T", 50,
+    # the prior at world 1, at world 2 and 3 with ZeRO-1 (the default: reduce-scatter, sharded fused Adam,
+    # all-gather; 3 ranks make shards that cut tensors at odd offsets) and at world 2 with the bucketed
+    # all-reduce (--zero 0).  Global batch 48 (divisible by 2 and 3), 2 steps per epoch.
+    prior_args = ["--data-path", dataset, "--epochs", 2, "--batch-size", 48, "--width", 256, "--T", 50,
                   "--ddim-steps", 3, "--latent-cache", "lat.pt", "--seed", 7]
-    for world in (1, 2):
-        d = tmp_path / f"prior{world}"
+    runs = {"w1": (1, []), "w2": (2, []), "w3": (3, []), "w2ar": (2, ["--zero", 0])}
+    ck, outp = {}, {}
+    for name, (world, extra) in runs.items():
+        d = tmp_path / f"prior_{name}"
         os.makedirs(d / "checkpoints", exist_ok=True)
         shutil.copy(tmp_path / "vae1" / "checkpoints" / "vae_last.pt", d / "checkpoints" / "vae_last.pt")
-        out[world] = run(d, world, "train_diffusion_prior.py", *prior_args)
-    p1 = torch.load(tmp_path / "prior1" / "checkpoints" / "diffusion_prior_last.pt", map_location="cpu",
-                    weights_only=True)
-    p2 = torch.load(tmp_path / "prior2" / "checkpoints" / "diffusion_prior_last.pt", map_location="cpu",
-                    weights_only=True)
-    compare_tensors(p1, p2, "prior")
-    a, b = losses(out[1], "diffusion_loss"), losses(out[2], "diffusion_loss")
-    print("diffusion_loss", a, b)
-    assert len(a) == len(b) == 2 and all(abs(x - y) <= 1e-5 * abs(x) for x, y in zip(a, b))
-    assert out[2].count("epoch 02/2 diffusion_loss=") == 1
-    l1 = torch.load(tmp_path / "prior1" / "lat.pt", map_location="cpu", weights_only=True)
-    l2 = torch.load(tmp_path / "prior2" / "lat.pt", map_location="cpu", weights_only=True)
-    assert torch.equal(l1["z0"], l2["z0"])
+        outp[name] = run(d, world, "train_diffusion_prior.py", *prior_args, *extra)
+        ck[name] = torch.load(d / "checkpoints" / "diffusion_prior_last.pt", map_location="cpu", weights_only=True)
+    for name in ("w2", "w3", "w2ar"):
+        compare_tensors(ck["w1"], ck[name], f"prior {name}")
+        a, b = losses(outp["w1"], "diffusion_loss"), losses(outp[name], "diffusion_loss")
+        print("diffusion_loss", name, a, b)
+        assert len(a) == len(b) == 2 and all(abs(x - y) <= 1e-5 * abs(x) for x, y in zip(a, b))
+        assert outp[name].count("epoch 02/2 diffusion_loss=") == 1
+    # ZeRO-1 at world 2 vs the all-reduce form at world 2: the same two-term sums, the same element-wise Adam
+    zd = max(float((ck["w2"][k].double() - ck["w2ar"][k].double()).abs().max()) for k in ck["w2"])
+    print(f"prior world 2: ZeRO-1 vs bucketed all-reduce max |diff| {zd:.3e}")
+    assert zd == 0.0
+    l1 = torch.load(tmp_path / "prior_w1" / "lat.pt", map_location="cpu", weights_only=True)
+    for name in ("w2", "w3"):
+        assert torch.equal(l1["z0"], torch.load(tmp_path / f"prior_{name}" / "lat.pt", map_location="cpu",
+                                                weights_only=True)["z0"])

@@ -422,6 +422,73 @@ def test_score_training_step_base32_vs_reference(golden, monkeypatch, split):
         _lib.set_conv_precision(old)
 
 
+@pytest.mark.parametrize("split", [True, False], ids=["split-convs", "fp32-convs"])
+def test_score_training_step_base96_vs_reference(golden, monkeypatch, split):
+    """Config 3's width (CondUNetTiny(base_ch=96), BASELINE configs[2]):
+    diffusion_loss_eps backward through the 96/192/384-channel training convs, then one fused Adam
+    step and the EMA update, against the reference (sde_score_model.py:358-399,
+    train_sde_score_model.py:217-240) on injected u / eps / drop draws.
+
+    Gates: the loss to 1e-5 relative; every parameter's gradient |sum| checksum and 64 fixed-index samples
+    to 1e-4 of the tensor's largest sampled magnitude (the base-32 gate); after the Adam step, 64
+    fixed-index samples of every parameter: Adam's first step moves a component by lr * g / (|g| + eps),
+    i.e. by lr * sign(g) wherever |g| >> eps, so a component whose reference gradient lies inside the
+    gradient gate (|g| <= 1e-4 of the tensor's max) may legitimately move the other way (<= 2 lr + 1e-6);
+    every other component to 1e-6 absolute; the EMA (0.9 p0 + 0.1 p1) to a tenth of those."""
+    from toycrystals_amd import _lib
+    from toycrystals_amd import functional as TF
+    from toycrystals_amd.models.sde_score_model import CondUNetTiny, VPSDE, diffusion_loss_eps
+    from toycrystals_amd.optim import Adam, ema_update
+    monkeypatch.setattr(TF, "_SPLIT_MIN_MACS", 0.0 if split else float("inf"))
+    old = _lib.conv_precision()
+    _lib.set_conv_precision("f16x3")
+    try:
+        gd = golden("train96_b3")
+        torch.manual_seed(0)
+        model = CondUNetTiny(4, 4, 96)
+        _perturb_norms(model, 5)
+        _check_checksums(model, gd)
+        model = model.cuda()
+        ema = CondUNetTiny(4, 4, 96).cuda()
+        ema.load_state_dict(model.state_dict())
+        opt = Adam(model.parameters(), lr=float(gd["lr"]))
+        draws = (cu(gd["u"]), cu(gd["eps"]), cu(gd["drop"]))
+        loss = diffusion_loss_eps(model, VPSDE(0.1, 30.0), cu(gd["x0"]), cu(gd["y_cat"], torch.int64), cu(gd["y_cont"]),
+                                  p_uncond=float(gd["p_uncond"]), draws=draws)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        assert abs(float(loss) - float(gd["loss"])) <= 1e-5 * float(gd["loss"])
+        worst = (0.0, "")
+        for k, p in model.named_parameters():
+            _cmp_grad_samples(k, p.grad, gd)
+            ref = gd["gs/" + k] if "gs/" + k in gd else gd["g/" + k].reshape(-1)
+            got = p.grad.detach().double().cpu().reshape(-1).numpy()
+            got = got[gd["gi/" + k]] if "gi/" + k in gd else got
+            worst = max(worst, (float(np.abs(got - ref).max()) / max(float(np.abs(ref).max()), 1e-8), k))
+        opt.step()
+        ema_update(ema, model, float(gd["ema_decay"]))
+        lr = float(gd["lr"])
+        flips = 0
+        names, enames = dict(model.named_parameters()), dict(ema.named_parameters())
+        for k in names:
+            idx = gd["pi/" + k]
+            gref = gd["gp/" + k]
+            gmax = float(np.abs(gd["gs/" + k] if "gs/" + k in gd else gd["g/" + k]).max())
+            unsure = np.abs(gref) <= 1e-4 * max(gmax, 1e-12)
+            tol = np.where(unsure, 2 * lr + 1e-6, 1e-6)
+            p1 = names[k].detach().double().cpu().reshape(-1).numpy()[idx]
+            e1 = enames[k].detach().double().cpu().reshape(-1).numpy()[idx]
+            d = np.abs(p1 - gd["p1/" + k])
+            de = np.abs(e1 - gd["ema1/" + k])
+            assert np.all(d <= tol), (k, float(d.max()))
+            assert np.all(de <= 0.1 * tol + 1e-7), (k, float(de.max()))
+            flips += int(np.sum(d > 1e-6))
+        print(f"base96 {'split' if split else 'fp32'} convs: loss {float(loss):.6f} vs {float(gd['loss']):.6f}; "
+              f"worst sampled gradient {worst[0]:.2e} ({worst[1]}); Adam samples beyond 1e-6: {flips}")
+    finally:
+        _lib.set_conv_precision(old)
+
+
 def test_adam_matches_torch_adam():
     """Fused Adam vs torch.optim.Adam (CPU, fp32) over 5 steps with weight decay."""
     from toycrystals_amd.optim import Adam

@@ -150,6 +150,27 @@ def test_oracle_loss(golden):
     assert abs(loss - float(g["loss"])) < 1e-6 * max(1.0, float(g["loss"]))
 
 
+def test_oracle_loss_base96_training_golden(golden):
+    """the base-96 training golden (config 3's width): the host mirror's seeded init with the perturbed norms
+    reproduces the reference's parameters (checksums), and the oracle's loss on the recorded draws equals the
+    reference's loss, so the GPU test's gradients are compared on exactly the reference's inputs"""
+    from toycrystals_amd.models.sde_score_model import CondUNetTiny
+    g = golden("train96_b3")
+    torch.manual_seed(0)
+    m = CondUNetTiny(4, 4, 96)
+    gen = torch.Generator().manual_seed(5)  # tests/golden/make_goldens.py perturb_norms(model, 5)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, (torch.nn.GroupNorm, torch.nn.LayerNorm)):
+                mod.weight.copy_(1.0 + 0.2 * torch.randn(mod.weight.shape, generator=gen))
+                mod.bias.copy_(0.2 * torch.randn(mod.bias.shape, generator=gen))
+    check_checksums(m, g)
+    o = ScoreUNet({k: v.numpy() for k, v in m.state_dict().items()})
+    loss = diffusion_loss_eps(o, VPSDE(0.1, 30.0), g["x0"], g["y_cat"], g["y_cont"], g["u"], g["eps"], g["drop"],
+                              p_uncond=float(g["p_uncond"]))
+    assert abs(loss - float(g["loss"])) < 1e-6 * max(1.0, float(g["loss"]))
+
+
 @pytest.mark.parametrize("name,cond", [("condvae_b4", True), ("vae_b4", False)])
 def test_oracle_vae(golden, name, cond):
     from toycrystals_amd.models.vae import CondVAE, VAE

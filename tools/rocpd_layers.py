@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Per-position kernel timing of one U-Net evaluation from a rocprofv3 rocpd database (kernel trace
-of a one-lane sampling pass): evaluations start at k_first_acf; median duration per position.
-usage: rocpd_layers.py run_results.db [out.txt]"""
+"""Per-position kernel timing of U-Net evaluations from a rocprofv3 rocpd database (kernel trace of a
+one-lane sampling pass): a pass starts at k_first_acf.  Passes are grouped by their kernel count and
+the grid of their first kernel, so an evaluation split into passes of different sizes (config 5's 2 GiB
+cap: an 84-image and a 44-image pass per Bt = 128 evaluation) is reported pass by pass, never as one
+median over both.  usage: rocpd_layers.py run_results.db [out.txt]"""
 import collections
 import sqlite3
 import statistics
@@ -25,15 +27,27 @@ def main() -> int:
         cur.append(r)
     seq.append(cur)
     L = collections.Counter(len(s) for s in seq).most_common(1)[0][0]
-    ev = [s for s in seq if len(s) == L][5:]
+    groups = collections.defaultdict(list)
+    for s in seq:
+        if len(s) == L:
+            groups[s[0][3]].append(s)
     out = open(sys.argv[2], "w") if len(sys.argv) > 2 else sys.stdout
-    tot = 0.0
-    for i in range(L):
-        d = statistics.median((s[i][2] - s[i][1]) / 1e3 for s in ev)
-        tot += d
-        print(f"{i:2d} {short(ev[0][i][0]):60s} grid={ev[0][i][3]:>8d} {d:9.1f} us", file=out)
-    span = statistics.median((s[-1][2] - s[0][1]) / 1e3 for s in ev)
-    print(f"sum of kernel medians {tot:.1f} us; first-start..last-end {span:.1f} us per eval ({len(ev)} evals)", file=out)
+    total_span = 0.0
+    for gk in sorted(groups, reverse=True):
+        ev = groups[gk]
+        ev = ev[min(5, len(ev) // 2):]  # skip warm-up passes
+        tot = 0.0
+        print(f"== pass kind: first-kernel grid {gk} ({len(ev)} passes)", file=out)
+        for i in range(L):
+            d = statistics.median((s[i][2] - s[i][1]) / 1e3 for s in ev)
+            tot += d
+            print(f"{i:2d} {short(ev[0][i][0]):60s} grid={ev[0][i][3]:>8d} {d:9.1f} us", file=out)
+        span = statistics.median((s[-1][2] - s[0][1]) / 1e3 for s in ev)
+        total_span += span
+        print(f"sum of kernel medians {tot:.1f} us; first-start..last-end {span:.1f} us per pass ({len(ev)} passes)",
+              file=out)
+    if len(groups) > 1:
+        print(f"per evaluation (one pass of each kind): {total_span:.1f} us", file=out)
     return 0
 
 

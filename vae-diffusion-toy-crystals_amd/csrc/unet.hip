@@ -12,6 +12,8 @@
 //   k_step   — out conv's 9-tap circular gather of r + bias, CFG combine eps_u + s(eps_c - eps_u),
 //              and the sampler update (EM / Heun stage / final x0 projection) in one pass;
 //              noise either host-injected or Philox4x32-10 in-kernel.
+#include <map>
+#include <mutex>
 #include "common.hpp"
 #include "h2.hpp"
 
@@ -1186,6 +1188,11 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
         if ((H * W) % FIRST_PX == 0 && C % 16 == 0 && C <= 128 && c0.kpad == 32) {
             const size_t shm = ((size_t)FIRST_PX * (C + 4) + 9 * (size_t)C) * sizeof(float) +
                                8 * (size_t)C * sizeof(double);
+            // b2 (fmt 2) tensors are written only by the tile-free record kernel: a shape that would reach
+            // k_conv_first<2> (4-byte records) or the fp32 first conv with fmt 2 fails here, loudly
+            TCX_REQUIRE(fmt != 2 || (h2.on && first_fuse && (H * W) % FIRST_ACF_PX == 0 && C % 8 == 0 &&
+                                     (H * W) % FR_PX == 0 && (FR_PX % W == 0 || W % FR_PX == 0)),
+                        "tcx_unet: the 2-byte bf16 format needs the record first conv (H*W %% %d, W vs %d)", FR_PX, FR_PX);
             if (h2.on && first_fuse && (H * W) % FIRST_ACF_PX == 0 && C % 8 == 0) {
                 const int chunk = FIRST_ACF_PX;
                 const int nchunk = H * W / chunk;
@@ -1219,6 +1226,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                 ns = H * W / FIRST_PX;
             }
         } else {
+            TCX_REQUIRE(fmt != 2, "tcx_unet: the 2-byte bf16 format needs the record first conv");
             if (ct.bias_img) {
                 hipLaunchKernelGGL(k_fold_bias, dim3(cdiv(Bt * C, 256)), dim3(256), 0, st, ct, C, B, cfg, Bt, P.bias0);
                 TCX_TRY(check_launch("k_fold_bias"));
@@ -1341,6 +1349,11 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     {
         TCX_TRY(gn_tab(net, P, 10, P.P0, C, gn, ns, st));
         TCX_REQUIRE(C % 4 == 0, "head: C %% 4");
+        // up1_1 wrote its output as 2-byte bf16 (pre_b2) at fmt 2, which only k_head8r<3, true> reads: a
+        // caller's out_w without 16-B alignment (that kernel's constant loads) is an error, never a
+        // fall-through to a head that reads the tensor as fp32
+        TCX_REQUIRE(fmt != 2 || (P.P0 % HPR == 0 && C == 96 && aligned16(net->out_w)),
+                    "tcx_unet: the 2-byte bf16 head needs out_w 16-byte aligned and H*W %% %d == 0", HPR);
         // register-weight head (r03_ag: 124 -> 118 us at 64^2); k_head8 for other widths / shapes
         if (P.P0 % HPR == 0 && (C == 96 || C == 64 || C == 32) && aligned16(net->out_w)) {  // (16-B constant loads)
             const dim3 gr(Bt * P.P0 / HPR);
@@ -1416,7 +1429,10 @@ int chunk_images(int B, int cap_images) {
 // together) advanced step by step on its own HIP stream, so the HBM-bound passes of one lane
 // (GroupNorm apply, upsample, head) can run beside the MFMA-bound convs of another.  The noise
 // counters use absolute element offsets: the result is identical to one lane.
-int g_lanes = 0;  // set by tcx_set_sample_lanes; 0: TCX_LANES from the environment
+// Per host thread (round 6: no process-global sampler state besides the thread-local error string):
+// tcx_set_sample_lanes sets the calling thread's lane count, which its later workspace queries and
+// sampler calls use; 0 means TCX_LANES from the environment.
+thread_local int g_lanes = 0;
 int lanes_setting() {
     static const int env = [] {
         const char* e = getenv("TCX_LANES");
@@ -1432,11 +1448,18 @@ struct LaneSync {
     bool ok = false;
 };
 
+// The lane streams and events of the CURRENT device, created on first use on that device (keyed by
+// hipGetDevice, so a process sampling on two devices never enqueues one device's lane work on the
+// other's streams) and kept for the process's life; guarded by a mutex for concurrent first calls.
 LaneSync* lane_sync() {
-    static LaneSync ls;
-    static bool tried = false;
-    if (!tried) {
-        tried = true;
+    static std::mutex mu;
+    static std::map<int, LaneSync> per_dev;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = per_dev.find(dev);
+    if (it == per_dev.end()) {
+        LaneSync ls;
         bool ok = true;
         // lane 0 runs on the caller's stream, so L lanes use L streams (the box has 4 hardware queues:
         // a fifth stream would share one and serialise)
@@ -1444,8 +1467,9 @@ LaneSync* lane_sync() {
         for (int i = 1; i < 4; ++i) ok = ok && hipStreamCreateWithFlags(&ls.s[i], hipStreamNonBlocking) == hipSuccess;
         for (int i = 0; i < 5; ++i) ok = ok && hipEventCreateWithFlags(&ls.ev[i], hipEventDisableTiming) == hipSuccess;
         ls.ok = ok;
+        it = per_dev.emplace(dev, ls).first;
     }
-    return ls.ok ? &ls : nullptr;
+    return it->second.ok ? &it->second : nullptr;
 }
 
 // workspace of one lane (rows 2*ceil(Bt/(2L)) >= ceil(Bt/L): an upper bound for B or 2B rows)
@@ -1484,8 +1508,9 @@ namespace tcx {
 namespace {
 
 // Fault injection for the sampler's error paths (tcx_debug_fail_eval): the k-th U-Net evaluation
-// after arming returns TCX_EINVAL before launching anything (one shot).
-int g_fail_eval = 0;
+// after arming returns TCX_EINVAL before launching anything (one shot).  Thread-local: arming it on
+// one host thread never fails another thread's evaluations.
+thread_local int g_fail_eval = 0;
 int injected_failure() {
     if (g_fail_eval <= 0) return TCX_OK;
     if (--g_fail_eval > 0) return TCX_OK;

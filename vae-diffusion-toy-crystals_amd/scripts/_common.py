@@ -11,7 +11,7 @@ if _PKG_ROOT not in sys.path:
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from toycrystals_amd.dist import all_reduce_, broadcast_, dist_backend, local_device  # noqa: E402
+from toycrystals_amd.dist import all_reduce_, broadcast_, dist_backend, dp_forced, local_device  # noqa: E402
 
 
 def pick_device(name: str) -> torch.device:
@@ -25,15 +25,22 @@ def pick_device(name: str) -> torch.device:
 
 def init_dp():
     """One process per GPU under torchrun (backend nccl = RCCL over xGMI; TCX_DIST_BACKEND=gloo lets
-    ranks share one GPU, toycrystals_amd.dist); (rank, world, device)."""
+    ranks share one GPU, toycrystals_amd.dist); (rank, world, device).  Under RCCL the group is bound
+    to this rank's device (device_id: the communicator is created eagerly on it, not on whatever
+    device is current at the first collective).  TCX_DP_FORCE=1 builds the group at world 1 too, so
+    a one-GPU run executes the collectives of the N-GPU path."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world <= 1:
+    if world <= 1 and not (dp_forced() and "RANK" in os.environ):
         return 0, 1, None
-    rank = int(os.environ["RANK"])
+    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", rank))
     device = local_device(local)
     torch.cuda.set_device(device)
-    dist.init_process_group(dist_backend(), rank=rank, world_size=world)
+    backend = dist_backend()
+    if backend == "nccl":
+        dist.init_process_group(backend, rank=rank, world_size=world, device_id=device)
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     return rank, world, device
 
 
@@ -50,7 +57,7 @@ def sync_rng_from_lead(world: int, device) -> None:
     For work rank 0 does ALONE whose draws the one-GPU run also makes (the latent-cache build with
     --z-target sample): the one-GPU run's generators have advanced by those draws, so the ranks
     must continue from rank 0's advanced state, not roll it back."""
-    if world <= 1:
+    if not dist.is_initialized():  # (world 1 under TCX_DP_FORCE=1 still runs the collective)
         return
     st = [None]
     if dist.get_rank() == 0:
@@ -61,13 +68,13 @@ def sync_rng_from_lead(world: int, device) -> None:
 
 
 def shutdown_dp(world: int) -> None:
-    if world > 1 and dist.is_initialized():
+    if dist.is_initialized():  # world > 1, or world 1 under TCX_DP_FORCE=1
         dist.barrier()
         dist.destroy_process_group()
 
 
 def allreduce_scalar_mean(v: float, world: int, device) -> float:
-    if world <= 1:
+    if not dist.is_initialized():
         return v
     t = torch.tensor([v], dtype=torch.float64, device=device)
     all_reduce_(t)
@@ -75,9 +82,10 @@ def allreduce_scalar_mean(v: float, world: int, device) -> float:
 
 
 def broadcast_from_lead(tensors, world: int, device):
-    """Rank 0's list of CPU tensors on every rank (shapes and dtypes travel first); identity at
-    world 1.  Returned as CPU tensors."""
-    if world <= 1:
+    """Rank 0's list of CPU tensors on every rank (shapes and dtypes travel first); identity without
+    a process group.  Rank 0 keeps its own tensors (so its arithmetic is the one-GPU run's); the
+    other ranks receive CPU copies."""
+    if not dist.is_initialized():
         return tensors
     meta = [None]
     if dist.get_rank() == 0:
@@ -87,5 +95,5 @@ def broadcast_from_lead(tensors, world: int, device):
     for i, (shape, dtype) in enumerate(meta[0]):
         buf = tensors[i].to(device).contiguous() if dist.get_rank() == 0 else torch.empty(shape, dtype=dtype, device=device)
         broadcast_(buf, src=0)
-        out.append(buf.cpu())
+        out.append(tensors[i].cpu() if dist.get_rank() == 0 else buf.cpu())
     return out

@@ -19,7 +19,7 @@ from tqdm import tqdm
 
 from toycrystals_amd import functional as TF
 from toycrystals_amd._lib import check, lib, ptr, stream_ptr
-from toycrystals_amd.dist import BucketedGradAllReduce
+from toycrystals_amd.dist import BucketedGradAllReduce, ZeroAdam, dp_active
 from toycrystals_amd.disk_data import DeviceBatches, ToyCrystalsDiskDataset
 from toycrystals_amd.models.diffusion_prior import DiffusionPriorFiLM, DiffusionSchedule
 from toycrystals_amd.models.vae import CondVAE
@@ -101,6 +101,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--global-draws", type=int, default=1, choices=[0, 1],
                    help="1: every rank draws u/eps for the WHOLE global batch from one shared device generator and "
                         "keeps its slice (N GPUs = 1 GPU); 0: per-rank draws of the local shard")
+    p.add_argument("--zero", type=int, default=1, choices=[0, 1],
+                   help="batch-DP only: 1 = ZeRO-1 (gradient reduce-scatter, fused Adam on this rank's 1/N shard, "
+                        "parameter all-gather); 0 = bucketed all-reduce + whole-model Adam on every rank")
     return p
 
 
@@ -163,10 +166,18 @@ def main() -> int:
             print("sample-only: saved results/diffusion_samples.png")
         _common.shutdown_dp(world)
         return 0
-    opt = Adam(prior.parameters(), lr=args.lr)
     params = [p for p in prior.parameters() if p.requires_grad]
-    # gradient averaging overlapped with backward (bucketed RCCL all-reduces; no-op on one GPU)
-    grad_ar = BucketedGradAllReduce(params)
+    zero = bool(args.zero) and dp_active()
+    if zero:
+        # ZeRO-1: the gradients reduce-scattered per bucket while backward runs, Adam
+        # on this rank's shard (1/N of the moments and of the update's HBM traffic), the updated
+        # shards all-gathered; the same Adam arithmetic as torch.optim.Adam element for element
+        opt = ZeroAdam(params, lr=args.lr)
+        grad_ar = None
+    else:
+        opt = Adam(prior.parameters(), lr=args.lr)
+        # gradient averaging overlapped with backward (bucketed RCCL all-reduces; no-op on one GPU)
+        grad_ar = BucketedGradAllReduce(params)
     loss_hist = []
     if lead:
         print("starting diffusion training loop.")
@@ -206,16 +217,23 @@ def main() -> int:
                 q = torch.clamp((t.float() / args.T * 4).long(), 0, 3)
                 bucket_sum.index_add_(0, q, per_s)
                 bucket_n.index_add_(0, q, torch.ones_like(per_s))
-            grad_ar.zero_grad()  # grads = zeroed views into the all-reduce buckets
-            loss.backward()
-            grad_ar.finish()
-            opt.step()
+            if zero:
+                opt.zero_grad()  # grads = zeroed views into the reduce-scatter buckets
+                loss.backward()
+                opt.step()  # reduce-scatter wait, shard Adam, all-gather
+            else:
+                grad_ar.zero_grad()  # grads = zeroed views into the all-reduce buckets
+                loss.backward()
+                grad_ar.finish()
+                opt.step()
             total += loss.detach()
         avg = _common.allreduce_scalar_mean(float(total.item()) / max(nb, 1), world, device)
         loss_hist.append(avg)
         if lead:
             print(f"epoch {epoch + 1:02d}/{args.epochs} diffusion_loss={avg:.6f}")
-            torch.save(prior.state_dict(), "checkpoints/diffusion_prior_last.pt")
+            # (cloned: under ZeRO-1 the parameters are views into the flat buckets, whose whole storage a
+            # view would drag into the file)
+            torch.save({k: v.clone() for k, v in prior.state_dict().items()}, "checkpoints/diffusion_prior_last.pt")
             with _common.lead_only_rng(device):  # the other ranks do not draw: keep the streams in step
                 save_diffusion_samples(vae=vae, prior=prior, sched=sched, out_path="results/diffusion_samples.png",
                                        device=device, z_mean=z_mean, z_std=z_std, ddim_steps=args.ddim_steps)

@@ -15,7 +15,19 @@ from typing import Iterable
 
 import torch
 
+from torch.autograd.graph import increment_version
+
 from ._lib import TcxAdamTensor, check, lib, stream_ptr
+
+
+def mark_updated(tensors) -> None:
+    """Bump the autograd version counter of tensors a libtcx kernel rewrote through raw pointers (the
+    fused Adam / EMA / ZeRO all-gather).  The models' packed-weight caches key on (data_ptr, _version)
+    (sde_score_model.CondUNetTiny.tcx_pack, diffusion_prior.DiffusionPriorFiLM._tcx); without the bump
+    an eval-mode forward after an optimiser step would reuse the pack of the previous weights (a sample
+    grid after epoch 2 drawn with epoch-1 weights), as torch's in-place optimiser updates bump it."""
+    for t in tensors:
+        increment_version(t)
 
 
 def _host_table(entries):
@@ -72,6 +84,7 @@ class Adam(torch.optim.Optimizer):
                 check(L.tcx_adam(table, len(entries), max_n, float(group["lr"]), float(beta1),
                                  float(beta2), float(group["eps"]), float(group["weight_decay"]), step,
                                  stream_ptr(device)), "tcx_adam")
+                mark_updated(p for p, _, _ in items)
         return loss
 
 
@@ -85,6 +98,7 @@ def ema_update(ema_model: torch.nn.Module, model: torch.nn.Module, decay: float)
     entries = [TcxAdamTensor(pe.data_ptr(), p.data_ptr(), None, None, p.numel()) for pe, p in pairs]
     check(lib().tcx_ema(_host_table(entries), len(entries), max(p.numel() for _, p in pairs), float(decay),
                         stream_ptr(device)), "tcx_ema")
+    mark_updated(pe for pe, _ in pairs)
 
 
 def params_to(params: Iterable[torch.nn.Parameter]):  # pragma: no cover - convenience
