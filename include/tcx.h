@@ -198,7 +198,9 @@ int tcx_attention_split_b2(const void* qkv, void* out, int Bt, int N, int C, int
  * wfrag the call is tcx_conv2d_h2.  bf16: 0 f16x3 records, 1 bf16 records, 2 two-byte bf16; + 16: source 1
  * is chunk-major ([C1/8][bsrc*H*W][32 B] record planes, tcx_gn_apply_tab_h2_cm; 4x4/s2 shapes of k_conv4s2g),
  * + 32: source 2 is chunk-major (3x3 shapes of k_conv3m); f16x3 records without prologue only, else
- * TCX_EINVAL. */
+ * TCX_EINVAL.  With bf16 = 2 (config 5, round 6) the chunk-major planes are 2-byte bf16
+ * ([C/8][bsrc*H*W][16 B], tcx_gn_apply_tab_b2_cm): + 16 on k_conv4s2g's slim 4x4/s2 shapes, + 32 on
+ * k_conv3lb's 3x3 shapes (rows of 64 / 128 / 256 px). */
 int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmod, int H, int W, int C1, int C2,
                       const void* wh, const void* wfrag, const float* wscale, const float* bias,
                       const float* bias_b,
@@ -215,6 +217,12 @@ int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const fl
  * (sde_score_model.py:248-263: h1, h2 and their concats), read by tcx_conv2d_h2_pro with the chunk-major bits. */
 int tcx_gn_apply_tab_h2_cm(const float* x, void* y, int Bt, int HW, int C, const float* scale,
                            const float* shift, unsigned* ovf, void* stream);
+/* Config 5 (round 6): GroupNorm + SiLU of a 2-byte bf16 tensor x [Bt][HW][C] (a conv's pre-norm b2 output)
+ * into CHUNK-MAJOR 2-byte bf16 planes y = [C/8][Bt*HW][16 B] (x != y; the tcx_gn_apply_tab_h2_cm shape
+ * conditions) — the 256^2 net's skip tensors h1 / h2 (sde_score_model.py:248-263), the same values as the
+ * in-place tcx_gn_apply_tab_b2 bit for bit, read by tcx_conv2d_h2_pro with bf16 = 2 + 16 / 32. */
+int tcx_gn_apply_tab_b2_cm(const void* x, void* y, int Bt, int HW, int C, const float* scale,
+                           const float* shift, void* stream);
 /* tcx_upsample2x with the output written as h2. */
 int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
                       const float* shift, unsigned* ovf, void* stream);

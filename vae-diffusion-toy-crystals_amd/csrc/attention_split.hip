@@ -89,9 +89,15 @@ __host__ __device__ constexpr int attn_ksb(int D, bool BF) { return (BF ? D * 2 
 
 // FMT 0: h2 records; 1 (BF): bf16 records (h2.hpp), one v_mfma_f32_32x32x16_bf16 (hi x hi) per product,
 // P in bf16; 2 (BF, B2): the same on 2-byte bf16 qkv and output (h2.hpp "b2": the records' hi halves)
+// XCD-aware workgroup order (round 6, TCX_ATTN_XCD=0: off): the hardware deals consecutive workgroups to the
+// 8 XCDs round-robin, so the N / 256 query blocks of one (image, head) — which all stream the same K / V
+// rows — were spread over every XCD's L2 and each fetched the (image, head)'s K / V from HBM (config 5:
+// 1,711 MB read per launch for 302 MB of qkv, profiles/r05_t_cfg5_pmc_traffic.txt).  With xcd_remap the
+// query blocks of an (image, head), and the heads of an image (whose K / V share cache lines of the token
+// rows), run on one XCD at about the same time.
 template <int D, int FMT>
 __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict__ qkv, char* __restrict__ out, int N,
-                                                         int C, float scale) {
+                                                         int C, float scale, int xcd) {
     constexpr bool BF = FMT >= 1, B2 = FMT == 2;
     constexpr int ESZ = B2 ? 2 : 4;  // bytes per element of qkv / out
     static_assert(D % 16 == 0 && D <= 64, "split attention: head dim multiple of 16, <= 64");
@@ -106,13 +112,21 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     // compute, is written to the other): [2][K | V^T hi | V^T lo]
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int STAGE = KT * KSB + 2 * DP * VSW * 4;
-    const int b = blockIdx.z, h = blockIdx.y;
+    int b = blockIdx.z, h = blockIdx.y, qb = blockIdx.x;
+    if (xcd) {
+        const int nq = gridDim.x, nh = gridDim.y;
+        const int flat = blockIdx.x + nq * (blockIdx.y + nh * blockIdx.z);
+        const int t = xcd_remap(flat, nq * nh * gridDim.z);
+        qb = t % nq;
+        h = (t / nq) % nh;
+        b = t / (nq * nh);
+    }
     const int tid = threadIdx.x;
     const size_t rs = 3 * ESZ * (size_t)C;  // bytes per token row of qkv (3C channels)
     const char* base = qkv + (size_t)b * N * rs;
     const int lane = tid & 63, w = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
-    const int q = blockIdx.x * 256 + w * 32 + li;
+    const int q = qb * 256 + w * 32 + li;
     const float scale2 = scale * 1.4426950408889634f;  // log2(e) / sqrt(D)
     h8 qh[DS], ql[DS];
     {
@@ -300,8 +314,12 @@ int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hi
         }
         attr_set = true;
     }
+    static const int xcd = [] {
+        const char* e = getenv("TCX_ATTN_XCD");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
     hipLaunchKernelGGL((k_attention_split<D, FMT>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
-                       (char*)out, N, C, scale);
+                       (char*)out, N, C, scale, xcd);
     return check_launch("tcx_attention_split");
 }
 

@@ -669,14 +669,23 @@ extern "C" int tcx_conv2d_h2_pro(const void* x1, const void* x2, int Bt, int bmo
                         "k_conv4s2g (4x4/s2) or k_lin1x1 (1x1) shapes");
     }
     if (cmf) {
-        // chunk-major sources: the 4x4/s2 LDS-DMA kernel (source 1) or k_conv3m (source 2) only
+        // chunk-major sources: the 4x4/s2 LDS-DMA kernel (source 1) or k_conv3m (source 2) for f16x3 records;
+        // config 5's 2-byte bf16 planes (round 6): k_conv4s2g's slim form (source 1) or k_conv3lb (source 2)
         p.cm1 = cmf & 1;
         p.cm2 = cmf >> 1;
-        TCX_REQUIRE(bf16 == 0 && !pro_scale1 && !pro_scale2 && (!p.cm2 || C2 > 0),
-                    "tcx_conv2d_h2: chunk-major sources are f16x3 records without a prologue");
+        TCX_REQUIRE((bf16 == 0 || bf16 == 2) && !pro_scale1 && !pro_scale2 && (!p.cm2 || C2 > 0) && cmf != 3,
+                    "tcx_conv2d_h2: chunk-major sources are f16x3 records or 2-byte bf16, without a prologue, on one "
+                    "source");
         if (p.cm1) {
             TCX_REQUIRE(conv4s2g_applies(p, cout_pad), "tcx_conv2d_h2: a chunk-major source 1 needs a k_conv4s2g shape");
             return launch_conv4s2g(p, cout_pad, (hipStream_t)stream);
+        }
+        if (bf16 == 2) {
+            ConvParams q = p;
+            q.n_nblk = cout_pad / 96;
+            TCX_REQUIRE(conv3g_applies(p, cout_pad) && conv3lb_takes(q),
+                        "tcx_conv2d_h2: a chunk-major 2-byte bf16 source 2 needs a k_conv3lb shape");
+            return launch_conv3g(p, cout_pad, (hipStream_t)stream);
         }
         TCX_REQUIRE(conv3g_applies(p, cout_pad) && conv3m_takes(p),
                     "tcx_conv2d_h2: a chunk-major source 2 needs a k_conv3m shape");

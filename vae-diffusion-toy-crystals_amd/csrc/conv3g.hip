@@ -63,13 +63,18 @@ int launch_conv3m(const ConvParams& p, hipStream_t st);
 // conv3lb.hip: the bf16 LDS-DMA form for rows of 64 / 128 / 256 pixels (h2 / bf16 record sources)
 bool conv3lb_takes(const ConvParams& p);
 int launch_conv3lb(const ConvParams& p, hipStream_t st);
+// conv3mb.hip (round 6): config 5's b2 3x3 convs on 16x16x32 bf16 tap pairs, three-slot weight ring
+bool conv3mb_takes(const ConvParams& p);
+int launch_conv3mb(const ConvParams& p, hipStream_t st);
 
 int launch_conv3g(ConvParams& p, int cout_pad, hipStream_t st) {
     p.n_nblk = cout_pad / 96;
     if (p.M == 0) return TCX_OK;
     prof_begin(st);
     int rc;
-    if (p.cm2) rc = launch_conv3m(p, st);  // chunk-major source 2 (tcx_conv2d_h2_pro checked conv3m_takes)
+    if (p.bf == 2 && conv3mb_takes(p)) rc = launch_conv3mb(p, st);  // b2 sources (chunk-major source 2 too)
+    else if (p.cm2 && p.bf == 2) rc = launch_conv3lb(p, st);  // chunk-major b2 source 2 (conv3lb_takes checked)
+    else if (p.cm2) rc = launch_conv3m(p, st);  // chunk-major source 2 (tcx_conv2d_h2_pro checked conv3m_takes)
     else if (conv3lb_takes(p)) rc = launch_conv3lb(p, st);
     else if (conv3l_takes(p)) rc = launch_conv3l(p, st);
     else if (p.W == 64) rc = launch3g_w64(p, st);

@@ -41,15 +41,22 @@ constexpr int B_PAIR = 2 * B_NT * 1024;   // hi fragments of a tap pair (6 KB)
 
 __host__ __device__ constexpr int b_npx(int W) { return (B_TP / W + 2) * (W + 2); }
 __host__ __device__ constexpr int b_ni(int W) { return (b_npx(W) + 31) / 32; }  // 1-KB DMA pieces per chunk
-constexpr size_t conv3lb_lds_bytes(int W) { return (size_t)2 * b_ni(W) * 1024 + 2 * (size_t)B_PAIR; }
+constexpr size_t conv3lb_lds_bytes(int W, int NR = 2) { return (size_t)2 * b_ni(W) * 1024 + NR * (size_t)B_PAIR; }
 
 __device__ __forceinline__ void lds_dma16b(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
 constexpr int WAIT_VM0_B = 0x0F70;    // s_waitcnt vmcnt(0)
+constexpr int WAIT_VM3_B = 0x0F73;    // s_waitcnt vmcnt(3): all but the last pair's 3 DMAs
 constexpr int WAIT_LGKM0_B = 0xC07F;  // s_waitcnt lgkmcnt(0)
 
-template <int W>
+// NR (round 6): weight-ring slots.  NR = 2: pair k is DMA'd at the start of odd tap 2k - 3 and waited for at
+// the barrier ending tap 2k - 2 — ONE tap pair (12 bf16 MFMAs per wave, ~0.3 us) to cover an L2 round trip,
+// which the weight waves then stall on while the other waves wait at the barrier (PMC r06_a: MFMA busy 43 %,
+// 0.26 of peak at 256-px rows).  NR = 3: pair k is issued at tap 2k - 5 into slot k % 3 (the slot of pair
+// k - 3, whose last B reads were during tap 2k - 6) and each barrier waits with vmcnt(3) (every pair but the
+// one issued last), so a pair has two tap pairs of cover.  Same arithmetic and order: bit-identical output.
+template <int W, int NR>
 __global__ __launch_bounds__(64 * B_NW, 2) void k_conv3lb(ConvParams p) {
     constexpr int RT = 2, NT = B_NT, NTHR = 64 * B_NW;
     constexpr int W2 = W + 2;
@@ -97,38 +104,46 @@ __global__ __launch_bounds__(64 * B_NW, 2) void k_conv3lb(ConvParams p) {
     const int rowb = p.C1 * esz;
     const int img0 = bs * H;
     const int ls = lane >> 1;
-    auto halo_voff = [&](int i) {
+    // chunk-major source 2 (p.cm2, config 5's concat convs, round 6): b2 planes [C2/8][pixels][16 B]
+    // (gn_apply_b2cm); a 16-channel chunk is two planes, so the slot's piece selects the plane
+    const int plane2 = p.cm2 ? (int)(p.bytes2 / (unsigned)(p.C2 / 8)) : 0;
+    // rb: bytes per pixel (row stride of a plane or of the pixel-major row); ph: bytes between the chunk's
+    // two 8-channel pieces
+    auto halo_voff = [&](int i, int rb, int ph) {
         const int hr0 = (32 * i) / W2;           // compile-time after unrolling
         const int th = W2 * (hr0 + 1) - 32 * i;  // lanes with ls >= th are in row hr0 + 1
         const int y0 = wrap_idx(r0 + hr0 - 1, H), y1 = wrap_idx(r0 + hr0, H);
-        const int yo0 = (img0 + y0) * W * rowb, yo1 = (img0 + y1) * W * rowb;
+        const int yo0 = (img0 + y0) * W * rb, yo1 = (img0 + y1) * W * rb;
         const bool nx = ls >= th;
         int hc = 32 * i - hr0 * W2 + ls - (nx ? W2 : 0);
         const int sl = 32 * i + ls;
         const int hcs = hc;
         if (sl >= NPX) hc = (NPX - 1) % W2;  // padding slots read a valid pixel
         const int x = hc == 0 ? W - 1 : (hc == W + 1 ? 0 : hc - 1);
-        const int yo = (sl >= NPX) ? (img0 + wrap_idx(r0 + (NPX - 1) / W2 - 1, H)) * W * rowb : (nx ? yo1 : yo0);
-        return yo + x * rowb + 8 * esz * ((lane & 1) ^ sw(hcs));
+        const int yo = (sl >= NPX) ? (img0 + wrap_idx(r0 + (NPX - 1) / W2 - 1, H)) * W * rb : (nx ? yo1 : yo0);
+        return yo + x * rb + ph * ((lane & 1) ^ sw(hcs));
     };
     auto halo_issue = [&](int j, int buf, int q0, int q1) {
         const int ci0 = j * B_KC;
         const bool s1 = ci0 < p.C1;
-        const int cc = (s1 ? ci0 : ci0 - p.C1) * esz;
+        const bool cm = !s1 && p.cm2;
+        const int cc = cm ? ((ci0 - p.C1) / 8) * plane2 : (s1 ? ci0 : ci0 - p.C1) * esz;
+        const int rb = cm ? 16 : rowb, ph = cm ? plane2 : 8 * esz;
         const __amdgpu_buffer_rsrc_t rs = s1 ? r1 : r2;
 #pragma unroll
         for (int q = 0; q < NIH; ++q) {
             if (q < q0 || q >= q1) continue;
             const int i = 2 * q + hw;
-            if (i < NI) lds_dma16b(rs, smd + buf * HB + i * 1024, halo_voff(i), cc);
+            if (i < NI) lds_dma16b(rs, smd + buf * HB + i * 1024, halo_voff(i, rb, ph), cc);
         }
     };
     // weight waves: pair k -> ring slot k & 1 as [tap][n][lane][16 B]; wave w moves pieces 3w .. 3w+2
     // (the hi KB of fragment (2k + tap, n) lies at ((nblk nch + 2k + tap) NT + n) 2048)
     auto pair_issue = [&](int k) {
+        const int slot = NR == 2 ? (k & 1) : k % 3;  // the slot of pair k (also when clamped below)
         k = k < npair ? k : npair - 1;
         const int base = (nblk * nch + 2 * k) * NT * 2048;
-        char* const d = smd + RING + (k & 1) * B_PAIR;
+        char* const d = smd + RING + slot * B_PAIR;
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             const int idx = 3 * wv + q;  // = tap * NT + n
@@ -156,7 +171,7 @@ __global__ __launch_bounds__(64 * B_NW, 2) void k_conv3lb(ConvParams p) {
     };
     const int bl = lane * 16;
     auto rd_b = [&](int s, int c) {
-        const char* B = smc + RING + ((c >> 1) & 1) * B_PAIR + (c & 1) * (B_PAIR / 2) + bl;
+        const char* B = smc + RING + (NR == 2 ? ((c >> 1) & 1) : (c >> 1) % 3) * B_PAIR + (c & 1) * (B_PAIR / 2) + bl;
 #pragma unroll
         for (int n = 0; n < NT; ++n) bb[s][n] = __builtin_bit_cast(bf8, *reinterpret_cast<const float4*>(B + n * 1024));
     };
@@ -174,6 +189,7 @@ __global__ __launch_bounds__(64 * B_NW, 2) void k_conv3lb(ConvParams p) {
     if (wv < 2) {
         pair_issue(0);
         pair_issue(1);
+        if constexpr (NR == 3) pair_issue(2);
     } else {
         halo_issue(0, 0, 0, NIH);
     }
@@ -189,7 +205,7 @@ __global__ __launch_bounds__(64 * B_NW, 2) void k_conv3lb(ConvParams p) {
         const int c = 9 * j + t;
         const bool more = j + 1 < cpt;
         if (wv < 2) {
-            if constexpr (s == 1) pair_issue((c + 3) >> 1);
+            if constexpr (s == 1) pair_issue((c + (NR == 2 ? 3 : 5)) >> 1);
         } else if constexpr (t < 4) {
             constexpr int q0 = (NIH * t) / 4, q1 = (NIH * (t + 1)) / 4;
             if (more) halo_issue(j + 1, hb ^ 1, q0, q1);
@@ -208,7 +224,8 @@ __global__ __launch_bounds__(64 * B_NW, 2) void k_conv3lb(ConvParams p) {
         if (t == 7) rd_a(1, 8, hb);
         if constexpr (s == 0) {  // even tap: publishes pair c/2 + 1 and (tap 6 / 7) halo j + 1
             constexpr bool halo_wait = t == (hb ? 7 : 6);
-            if (wv < 2 || halo_wait) __builtin_amdgcn_s_waitcnt(WAIT_VM0_B);
+            if (wv < 2) __builtin_amdgcn_s_waitcnt(NR == 2 ? WAIT_VM0_B : WAIT_VM3_B);
+            else if (halo_wait) __builtin_amdgcn_s_waitcnt(WAIT_VM0_B);
             barrier();
         }
     };
@@ -241,19 +258,29 @@ __global__ __launch_bounds__(64 * B_NW, 2) void k_conv3lb(ConvParams p) {
     }
 }
 
+// TCX_LB_RING=2: the two-slot weight ring (A/B); default three slots
+int lb_ring() {
+    static const int r = [] {
+        const char* e = getenv("TCX_LB_RING");
+        return (e && e[0] == '2') ? 2 : 3;
+    }();
+    return r;
+}
+
 template <int W>
 int launch3lb(const ConvParams& p, hipStream_t st) {
-    static bool attr = false;
-    void (*const k)(ConvParams) = &k_conv3lb<W>;
-    constexpr size_t shm = conv3lb_lds_bytes(W);
-    static_assert(shm <= 80 * 1024, "two workgroups per CU");
-    if (!attr) {
+    static bool attr[2] = {};
+    const int nr = lb_ring();
+    void (*const k)(ConvParams) = nr == 2 ? &k_conv3lb<W, 2> : &k_conv3lb<W, 3>;
+    const size_t shm = conv3lb_lds_bytes(W, nr);
+    static_assert(conv3lb_lds_bytes(W, 3) <= 80 * 1024, "two workgroups per CU");
+    if (!attr[nr - 2]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) !=
             hipSuccess) {
             set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", shm);
             return TCX_EHIP;
         }
-        attr = true;
+        attr[nr - 2] = true;
     }
     const int grid = (p.M / B_TP) * p.n_nblk;
     hipLaunchKernelGGL(k, dim3(grid), dim3(64 * B_NW), shm, st, p);
@@ -270,6 +297,7 @@ bool conv3lb_takes(const ConvParams& p) {
     }();
     if (!on || !p.bf || !p.circular || !(p.W == 64 || p.W == 128 || p.W == 256)) return false;
     if (p.M % B_TP != 0 || p.HoWo % B_TP != 0 || p.Cin % 32 != 0) return false;
+    if (p.cm1 || (p.cm2 && (p.bf != 2 || p.C2 % 16 != 0))) return false;  // chunk-major: b2 source 2 only
     return p.sc1 == nullptr && !(p.C2 > 0 && p.sc2 != nullptr);  // h2 / bf16 record sources only
 }
 

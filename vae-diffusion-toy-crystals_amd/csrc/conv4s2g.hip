@@ -98,10 +98,12 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
     // pixel's 2-byte row; both DMA lanes of a slot read it (the lo slot half is never read by BF)
     const bool b2 = BF && p.bf == 2;
     // chunk-major source (p.cm1, ConvParams): the 8-channel chunk j is the plane at byte j * plane, a
-    // pixel's record at 32 * pixel inside it
-    const bool cm = !BF && p.cm1;
-    const int rowb = cm ? 32 : p.C1 * (b2 ? 2 : 4);
+    // pixel's record at 32 * pixel inside it (h2 records), or its 16-B b2 piece at 16 * pixel (config 5,
+    // round 6: gn_apply_b2cm's planes)
+    const bool cm = (!BF || b2) && p.cm1;
+    const int rowb = cm ? (b2 ? 16 : 32) : p.C1 * (b2 ? 2 : 4);
     const int plane = cm ? (int)(p.bytes1 / (unsigned)(p.C1 / 8)) : 32;
+    const int cstride = cm ? plane : (b2 ? 16 : plane);  // byte distance of consecutive chunks
     auto halo_voff = [&](int i) {
         // RT = 2: recomputed at every issue from an opaque copy of the lane index (hoisted out of the chunk
         // loop, the offsets of all NI instructions spilled beside the doubled accumulators; k_conv3m's note)
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void k_conv4s2g(ConvParams p) {
         for (int q = 0; q < NIH; ++q) {
             if (q < q0 || q >= q1) continue;
             const int i = 2 * q + hw;
-            if (i < NI) q_dma16(r1, smd + buf * HB + i * 1024, halo_voff(i), (b2 ? 16 : plane) * j);
+            if (i < NI) q_dma16(r1, smd + buf * HB + i * 1024, halo_voff(i), cstride * j);
         }
     };
     // ---- weight pairs (waves 0-1): pair k = k-steps 2k, 2k + 1 -> ring slot k & 1; wave w moves KB [6 w, 6 w + 6)
@@ -356,7 +358,7 @@ bool conv4s2g_applies(const ConvParams& p, int cout_pad) {
            p.H == 2 * p.Ho &&
            p.W == 2 * p.Wo && p.HoWo % Q_TP == 0 && cout_pad % 96 == 0 && p.Cin % 8 == 0 && p.C2 == 0 &&
            p.x2 == nullptr && p.kpad == 16 * p.Cin && p.osy == 1 && p.osx == 1 && p.sc1 == nullptr &&
-           !(p.cm1 && p.bf) && !p.cm2;
+           !(p.cm1 && p.bf == 1) && !p.cm2;
 }
 
 int launch_conv4s2g(ConvParams& p, int cout_pad, hipStream_t st) {

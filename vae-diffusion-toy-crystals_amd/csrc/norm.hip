@@ -1184,6 +1184,58 @@ int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const fl
     return check_launch("tcx_upsample2x_h2");
 }
 
+// Config 5's skip tensors chunk-major (round 6): GroupNorm + SiLU of a 2-byte bf16 (b2) pre-norm conv output
+// into CHUNK-MAJOR b2 planes y = [C/8][Bt * HW][16 B] (8 channels x 2 B per pixel per plane), out of place.
+// The readers are config 5's 4x4/s2 downsamples (k_conv4s2g's slim slots, source 1) and the up-path concat
+// convs (k_conv3lb, source 2): from a pixel-major b2 row (C * 2 = 192 / 384 B per pixel) their halo DMA
+// fetched 16 B per pixel and chunk, and the downsample re-read every line 4.6-5.8x from HBM
+// (profiles/r05_t_cfg5_pmc_traffic.txt); a plane is contiguous.  One workgroup per CM_NR * 256 16-B
+// records (tpx pixels of one image): coalesced pixel-major loads, the same arithmetic as k_gn_apply_b2<true>
+// (so the values are bit-identical to the in-place apply), an LDS transpose, contiguous plane stores.
+__global__ __launch_bounds__(256) void k_gn_apply_b2cm(const char* __restrict__ x, char* __restrict__ y, int HW,
+                                                       int C, const float* __restrict__ tsc,
+                                                       const float* __restrict__ tsh) {
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    const int C8 = C / 8;
+    const int tpx = 256 * CM_NR / C8;  // pixels per workgroup
+    const int rs = tpx * 16 + 16;      // LDS bytes per plane row (+16: consecutive planes on other banks)
+    float* sc = lsm;
+    float* sh = lsm + C;
+    char* rec = reinterpret_cast<char*>(lsm + 2 * C);
+    const int b = blockIdx.y, tid = threadIdx.x;
+    for (int c = tid; c < C; c += 256) {
+        sc[c] = tsc[(size_t)b * C + c];
+        sh[c] = tsh[(size_t)b * C + c];
+    }
+    const size_t pix0 = (size_t)b * HW + (size_t)blockIdx.x * tpx;
+    const char* src = x + pix0 * C * 2;
+    uint4 u[CM_NR];
+#pragma unroll
+    for (int k = 0; k < CM_NR; ++k) u[k] = *reinterpret_cast<const uint4*>(src + (size_t)(tid + 256 * k) * 16);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CM_NR; ++k) {
+        const int idx = tid + 256 * k;
+        const int px = idx / C8, c8 = idx - px * C8, c0 = 8 * c8;
+        const uint4 a = u[k];
+        float v[8] = {bf_lo(a.x), bf_hi(a.x), bf_lo(a.y), bf_hi(a.y), bf_lo(a.z), bf_hi(a.z), bf_lo(a.w), bf_hi(a.w)};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = silu_hw(fmaf(v[e], sc[c0 + e], sh[c0 + e]));
+        *reinterpret_cast<uint4*>(rec + c8 * rs + px * 16) =
+            make_uint4(pack2_bf(v[0], v[1]), pack2_bf(v[2], v[3]), pack2_bf(v[4], v[5]), pack2_bf(v[6], v[7]));
+    }
+    __syncthreads();
+    const size_t npix = (size_t)gridDim.y * HW;  // pixels per plane
+#pragma unroll
+    for (int k = 0; k < CM_NR; ++k) {
+        const int idx = tid + 256 * k;
+        const int c8 = idx / tpx, px = idx - c8 * tpx;
+        *reinterpret_cast<uint4*>(y + ((size_t)c8 * npix + pix0 + px) * 16) =
+            *reinterpret_cast<const uint4*>(rec + c8 * rs + px * 16);
+    }
+}
+
+
 bool gn_apply_cm_ok(int HW, int C) {
     if (C % 8 != 0) return false;
     const int c8 = C / 8;
@@ -1201,10 +1253,24 @@ int gn_apply_cm(const float* x, void* y, int Bt, int HW, int C, const float* sca
     return check_launch("gn_apply_cm");
 }
 
+int gn_apply_b2cm(const void* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift,
+                  hipStream_t st) {
+    TCX_REQUIRE(x && y && scale && shift && x != y && aligned16(x) && aligned16(y) && gn_apply_cm_ok(HW, C),
+                "gn_apply_b2cm: needs distinct 16-B aligned buffers, C %% 8 == 0 and whole workgroup tiles");
+    if (Bt == 0) return TCX_OK;
+    const int tpx = 256 * CM_NR / (C / 8);
+    const size_t shm = (size_t)2 * C * sizeof(float) + (size_t)(C / 8) * (tpx * 16 + 16);
+    hipLaunchKernelGGL(k_gn_apply_b2cm, dim3(HW / tpx, Bt), dim3(256), shm, st, (const char*)x, (char*)y, HW, C, scale,
+                       shift);
+    return check_launch("gn_apply_b2cm");
+}
+
 int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
                     unsigned* ovf, int bf, hipStream_t st) {
     TCX_REQUIRE(x && y && scale && shift && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_gn_apply_tab_h2: bad args");
-    TCX_REQUIRE((const void*)x == y || (const char*)y + (size_t)Bt * HW * C * 4 <= (const char*)x ||
+    // (the output is 2 B per element for bf == 2: its extent, not the source's, bounds the overlap test)
+    const size_t ybytes = (size_t)Bt * HW * C * (bf == 2 ? 2 : 4);
+    TCX_REQUIRE((const void*)x == y || (const char*)y + ybytes <= (const char*)x ||
                 (const char*)x + (size_t)Bt * HW * C * 4 <= (const char*)y, "tcx_gn_apply_tab_h2: partial overlap");
     if (Bt == 0) return TCX_OK;
     const int ppb = std::max(1, 32768 / C);
@@ -1278,6 +1344,11 @@ extern "C" int tcx_upsample2x_bf16(const float* x, void* y, int Bt, int H, int W
 extern "C" int tcx_gn_apply_tab_h2_cm(const float* x, void* y, int Bt, int HW, int C, const float* scale,
                                       const float* shift, unsigned* ovf, void* stream) {
     return gn_apply_cm(x, y, Bt, HW, C, scale, shift, ovf, (hipStream_t)stream);
+}
+
+extern "C" int tcx_gn_apply_tab_b2_cm(const void* x, void* y, int Bt, int HW, int C, const float* scale,
+                                      const float* shift, void* stream) {
+    return gn_apply_b2cm(x, y, Bt, HW, C, scale, shift, (hipStream_t)stream);
 }
 
 extern "C" int tcx_gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale,

@@ -31,6 +31,8 @@ int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float*
 int gn_apply_b2_inplace(void* x, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
                         hipStream_t st);
 bool gn_apply_cm_ok(int HW, int C);  // norm.hip: chunk-major skip-tensor records
+int gn_apply_b2cm(const void* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift,
+                  hipStream_t st);  // norm.hip: config 5's chunk-major b2 skip planes
 int gn_apply_cm(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift,
                 unsigned* ovf, hipStream_t st);
 int attention_split(const void* qkv, void* out, int Bt, int N, int C, int heads, int bf, hipStream_t st);
@@ -1061,6 +1063,14 @@ bool skip_cm_ok(const tcx_conv& ds, const tcx_conv& cat, int H, int W, int C, bo
            C % 16 == 0 && cat.cout_pad % 96 == 0 && cat.cout % 96 == 0 && (H * W) % 256 == 0;
 }
 
+// config 5 (b2, round 6): a skip tensor can be chunk-major b2 planes when its downsample runs on k_conv4s2g's
+// slim form and its concat conv on k_conv3lb (rows of 128 / 256 px), the apply pass tiles the image
+bool skip_cm_b2_ok(const tcx_conv& ds, const tcx_conv& cat, int H, int W, int C) {
+    return gn_apply_cm_ok(H * W, C) && ds.whf && cat.whf && ds.ks == 4 && cat.ks == 3 && H % 2 == 0 &&
+           (W == 128 || W == 256) && (H * W / 4) % 128 == 0 && ds.cout_pad % 96 == 0 && C % 16 == 0 &&
+           cat.cout_pad % 96 == 0 && (H * W) % 256 == 0;
+}
+
 // TCX_ATTN_SPLIT=0 keeps the split evaluator's attention on fp32 MFMA (A/B measurements)
 bool attn_split_enabled() {
     static const bool on = [] {
@@ -1242,16 +1252,25 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     // [C/8][Bt*HW][32 B] record planes (gn_apply_cm) for their two readers, the 4x4/s2 downsample (source 1,
     // whose halo DMA re-fetched pixel-major lines) and the up-path concat conv on k_conv3m (source 2).  The
     // raw conv output goes to a buffer that is free at that point (b64 / a32) and the apply writes h1 / h2.
-    const bool cm1 = h2.on && fmt == 0 && (skip_cm_mask() & 1) && skip_cm_ok(net->ds1, net->up1_0, H, W, C, pro[1]);
-    const bool cm2 = h2.on && fmt == 0 && (skip_cm_mask() & 2) && skip_cm_ok(net->ds2, net->up2_0, H1, W1, C2, pro[3]);
+    // (config 5, round 6: the b2 skip tensors as chunk-major b2 planes, gn_apply_b2cm, same readers' roles)
+    const bool cm1 = h2.on && (skip_cm_mask() & 1) &&
+                     ((fmt == 0 && skip_cm_ok(net->ds1, net->up1_0, H, W, C, pro[1])) ||
+                      (fmt == 2 && !pro[1] && skip_cm_b2_ok(net->ds1, net->up1_0, H, W, C)));
+    const bool cm2 = h2.on && (skip_cm_mask() & 2) &&
+                     ((fmt == 0 && skip_cm_ok(net->ds2, net->up2_0, H1, W1, C2, pro[3])) ||
+                      (fmt == 2 && !pro[3] && skip_cm_b2_ok(net->ds2, net->up2_0, H1, W1, C2)));
+    auto apply_cm = [&](const float* raw, float* dst, int HWn, int Cn, int i) -> int {
+        TCX_TRY(gn_tab(net, P, i, HWn, Cn, gn, ns, st));
+        if (fmt == 2) return gn_apply_b2cm(raw, dst, Bt, HWn, Cn, P.sc(i), P.sh(i), st);
+        return gn_apply_cm(raw, dst, Bt, HWn, Cn, P.sc(i), P.sh(i), h2.ovf, st);
+    };
     H2Ctx h2cs = h2, h2cc = h2;  // h2 with the chunk-major bits: source 1 (downsample), source 2 (concat)
     h2cs.fmt |= 16;
     h2cc.fmt |= 32;
     TCX_TRY(conv_gn(net->down1_1, P.a64, nullptr, C, 0, Bt, 0, H, W, 1, 1, nullptr, nullptr, cm1 ? P.b64 : P.h1, gn,
                     &ns, st, SC(0), SH(0), nullptr, nullptr, h2, pre_b2));
     if (cm1) {
-        TCX_TRY(gn_tab(net, P, 1, P.P0, C, gn, ns, st));
-        TCX_TRY(gn_apply_cm(P.b64, P.h1, Bt, P.P0, C, P.sc(1), P.sh(1), h2.ovf, st));
+        TCX_TRY(apply_cm(P.b64, P.h1, P.P0, C, 1));
     } else {
         TCX_TRY(norm(1, P.h1, P.P0, C));  // h1 stays raw; its two consumers apply table 1
     }
@@ -1265,8 +1284,7 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     TCX_TRY(conv_gn(net->down2_1, P.b32, nullptr, C2, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, cm2 ? P.a32 : P.h2, gn,
                     &ns, st, SC(2), SH(2), nullptr, nullptr, h2, pre_b2));
     if (cm2) {
-        TCX_TRY(gn_tab(net, P, 3, P.P1, C2, gn, ns, st));
-        TCX_TRY(gn_apply_cm(P.a32, P.h2, Bt, P.P1, C2, P.sc(3), P.sh(3), h2.ovf, st));
+        TCX_TRY(apply_cm(P.a32, P.h2, P.P1, C2, 3));
     } else {
         TCX_TRY(norm(3, P.h2, P.P1, C2));  // h2 raw; consumers apply table 3
     }

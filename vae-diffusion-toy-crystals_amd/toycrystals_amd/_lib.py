@@ -109,6 +109,7 @@ _SIGS = {
     "tcx_pack_conv_weight_h2_frag4": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp]),
     "tcx_gn_apply_tab_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_fp, c_fp]),
     "tcx_gn_apply_tab_h2_cm": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
+    "tcx_gn_apply_tab_b2_cm": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
     "tcx_upsample2x_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp]),
     "tcx_attention_h2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp]),
     "tcx_attention_split": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
