@@ -108,7 +108,7 @@ def test_zero_adam_world1_equals_fused_adam():
     m0, m1 = mk(), mk()
     m1.load_state_dict(m0.state_dict())
     o0 = Adam(m0.parameters(), lr=1e-2, weight_decay=0.01)
-    o1 = ZeroAdam(list(m1.parameters()), lr=1e-2, weight_decay=0.01, bucket_mb=0.02)  # several buckets
+    o1 = ZeroAdam(list(m1.parameters()), lr=1e-2, weight_decay=0.01, bucket_mb=0.01)  # several buckets
     assert len(o1.buckets) > 1
     x = torch.randn(64, 37, device="cuda")
     for _ in range(4):
