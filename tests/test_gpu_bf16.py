@@ -647,7 +647,15 @@ def test_b2_256px_forward_chunk_major_skips_bit_identical(tmp_path):
     (2, 192, 0, 64, 192),    # 64-px rows (the mid block)
     (2, 192, 0, 128, 192),   # Cin 192: an even number of 9-pair periods (down2_1, us2)
 ])
-def test_b2_conv3mb_vs_float64_on_rounded_operands(B, C1, C2, H, co):
+@pytest.fixture
+def conv3mb_everywhere():
+    """k_conv3mb on every b2 3x3 shape it covers (the default takes it at Cin >= 192 with a b2 output only)"""
+    prev = L().tcx_debug_conv3mb(2)
+    yield
+    L().tcx_debug_conv3mb(prev)
+
+
+def test_b2_conv3mb_vs_float64_on_rounded_operands(B, C1, C2, H, co, conv3mb_everywhere):
     """k_conv3mb (round 6: config 5's 3x3 convs on v_mfma_f32_16x16x32_bf16 tap pairs, three-slot weight
     ring) on b2 sources against float64 on the same bf16-rounded operands: only the fp32 accumulation
     differs (5e-6 of the output scale, as the k_conv3lb gate); GroupNorm partials against float64 sums of
@@ -672,7 +680,7 @@ def test_b2_conv3mb_vs_float64_on_rounded_operands(B, C1, C2, H, co):
 
 @pytest.mark.parametrize("Bt,H,C1,C2,co", [(8, 256, 96, 0, 96), (4, 256, 96, 96, 96), (16, 128, 96, 0, 192),
                                             (32, 64, 192, 0, 192)])
-def test_b2_conv3mb_repeats_bit_for_bit(Bt, H, C1, C2, co):
+def test_b2_conv3mb_repeats_bit_for_bit(Bt, H, C1, C2, co, conv3mb_everywhere):
     """k_conv3mb repeats bit for bit (b2 output and GroupNorm partials) into a NaN-filled output, six times"""
     g = torch.Generator(device="cuda").manual_seed(0)
     s1 = to_b2(torch.randn((Bt, H, H, C1), device="cuda", generator=g))
@@ -701,3 +709,24 @@ def test_b2_conv3mb_repeats_bit_for_bit(Bt, H, C1, C2, co):
         bad += int((y1 != y0).sum()) + int((g1 != g0).sum())
     print(f"k_conv3mb Bt={Bt} {H}^2 {C1}+{C2}->{co}: 6 repeats, {bad} differing values")
     assert bad == 0
+
+
+
+@pytest.mark.parametrize("B,C1,C2,H,co,ob2", [(1, 96, 0, 256, 96, 1), (1, 96, 96, 256, 96, 1), (2, 192, 0, 128, 192, 1),
+                                              (1, 192, 192, 128, 96, 1), (2, 96, 0, 128, 96, 0), (2, 192, 0, 64, 192, 0)])
+def test_b2_conv3mb_equals_conv3lb_bit_for_bit(B, C1, C2, H, co, ob2):
+    """k_conv3mb (16x16x32 tap pairs) and k_conv3lb (32x32x16 taps) on the same b2 sources: the MFMAs sum the
+    same bf16 products in the same k order (tap, then channel) into fp32, so outputs and GroupNorm partials are
+    bit-identical — which is what lets the library pick either per layer"""
+    x1 = dev(nhwc(rng.standard_normal((B, C1, H, H))))
+    x2 = dev(nhwc(rng.standard_normal((B, C2, H, H)))) if C2 else None
+    w = (rng.standard_normal((co, C1 + C2, 3, 3)) / np.sqrt(9 * (C1 + C2))).astype(np.float32)
+    b = rng.standard_normal(co).astype(np.float32)
+    out = {}
+    for mode in (2, 0):
+        prev = L().tcx_debug_conv3mb(mode)
+        try:
+            out[mode] = _conv_fmt(x1, x2, w, b, 3, 1, 2, bool(ob2), gn=True)
+        finally:
+            L().tcx_debug_conv3mb(prev)
+    assert torch.equal(out[2][0], out[0][0]) and torch.equal(out[2][1], out[0][1])

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 T=${1:-r06_c}
 P="python -u -m pytest -x -v -s --timeout 600 --timeout-method thread"
 timeout -k 10 600 $P tests/test_gpu_bf16.py -k "conv3mb or b2_conv_equals or chunk_major or conv3lb_repeats" > gpurun_out/${T}_t1.log 2>&1 || exit 1
-for v in "TCX_CONV3MB=1" "TCX_CONV3MB=0 TCX_LB_RING=3" "TCX_CONV3MB=0 TCX_LB_RING=2"; do
+for v in "TCX_CONV3MB=2" "TCX_CONV3MB=0 TCX_LB_RING=3" "TCX_CONV3MB=0 TCX_LB_RING=2"; do
   env $v timeout -k 10 300 python -u tools/mbbench.py >> gpurun_out/${T}_layers.log 2>&1 || exit 1
 done
 for v in "TCX_CONV3MB=1" "TCX_CONV3MB=0" "TCX_CONV3MB=1"; do

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time config 5's 3x3 convs on 2-byte bf16 (b2) sources and outputs at their 256^2 / 128^2 / 64^2 layer shapes
 (HIP events, median of REPS), on the kernel the library picks (k_conv3mb by default, k_conv3lb with
-TCX_CONV3MB=0), with the fraction of the 2.5 PFLOP/s dense bf16 peak.  usage (GPU box): python tools/mbbench.py"""
+TCX_CONV3MB=0; TCX_CONV3MB=2 forces k_conv3mb on every shape), with the fraction of the 2.5 PFLOP/s dense bf16 peak.  usage (GPU box): python tools/mbbench.py"""
 import os
 import statistics
 import sys

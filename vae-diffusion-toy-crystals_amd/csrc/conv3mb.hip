@@ -345,13 +345,24 @@ int launch3mb(const ConvParams& p, hipStream_t st) {
 
 }  // namespace
 
-// TCX_CONV3MB=0 keeps config 5's 3x3 convs on k_conv3lb (A/B measurements)
-bool conv3mb_takes(const ConvParams& p) {
-    static const bool on = [] {
+// Where it runs (measured per layer against k_conv3lb with its 3-slot ring, tools/mbbench.py at Bt = 84,
+// profiles/r06_c_cfg5_conv_layers_mb_vs_lb.txt): faster at Cin >= 192 with a b2 output (down2.net.3 879 vs
+// 926 us, up2.net.0 824 vs 855, mid.net.0 211 vs 218), slower at Cin = 96 (down1.net.3 1336 vs 1269 us,
+// up1.net.0 1954 vs 1908) and with an fp32 output (up2.net.3 318 vs 284, mid.net.3 234 vs 219) — so the
+// default takes those layers only.  Same products, same k order: the two kernels' outputs are bit-identical
+// (tests/test_gpu_bf16.py test_b2_conv_equals_the_record_conv).  TCX_CONV3MB=0: never, 2: every b2 shape.
+thread_local int g_conv3mb_force = -1;  // tcx_debug_conv3mb (tests): overrides the environment on this thread
+int conv3mb_mode() {
+    static const int m = [] {
         const char* e = getenv("TCX_CONV3MB");
-        return !(e && e[0] == '0');
+        return (e && (e[0] == '0' || e[0] == '2')) ? e[0] - '0' : 1;
     }();
-    if (!on || p.bf != 2 || !p.circular || !(p.W == 64 || p.W == 128 || p.W == 256) || p.wf == nullptr) return false;
+    return g_conv3mb_force >= 0 ? g_conv3mb_force : m;
+}
+bool conv3mb_takes(const ConvParams& p) {
+    const int mode = conv3mb_mode();
+    if (mode == 0 || (mode == 1 && (p.Cin < 192 || !p.out_h2))) return false;
+    if (p.bf != 2 || !p.circular || !(p.W == 64 || p.W == 128 || p.W == 256) || p.wf == nullptr) return false;
     if (p.M % MB_TP != 0 || p.HoWo % MB_TP != 0 || p.Cin % 32 != 0 || p.Cout % MB_BN != 0) return false;
     if (p.cm1 || (p.cm2 && p.C2 % 16 != 0) || p.sc1 != nullptr || p.sc2 != nullptr) return false;
     return p.act == 0 && p.bias_b == nullptr && p.resid == nullptr && p.osy == 1 && p.osx == 1 && p.H == p.Ho &&
@@ -365,3 +376,11 @@ int launch_conv3mb(const ConvParams& p, hipStream_t st) {
 }
 
 }  // namespace tcx
+
+// Test hook: k_conv3mb's selection on this host thread (0 never, 1 the measured default, 2 every b2 3x3 shape
+// it covers; -1 back to TCX_CONV3MB).  Returns the previous override.
+extern "C" int tcx_debug_conv3mb(int mode) {
+    const int prev = tcx::g_conv3mb_force;
+    tcx::g_conv3mb_force = mode < -1 ? -1 : (mode > 2 ? 2 : mode);
+    return prev;
+}

@@ -579,23 +579,56 @@ __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int
     const int c0 = sub * CL;
     float4 v[HR_PASS][Q];  // pass k's channels; only HR_LA + 1 passes are live at a time
     const size_t src0 = (size_t)(p0 + pl) * C + c0;
+    // config 5's b2 head (B2, C = 96, round 6): lane sub takes channels [8 sub, 8 sub + 8) — one 16-B load, the 8
+    // lanes of a pixel its first 128 contiguous bytes — and [64 + 4 sub, 64 + 4 sub + 4) — one 8-B load, the
+    // last 64 B — instead of 12 contiguous channels as three 8-B loads at a 24-B lane stride (the 1.06 GB read
+    // ran at 2.3 TB/s, r06_b layers).  The lane's channel j is 8 sub + j (j < 8) or 64 + 4 sub + j - 8.
+    constexpr bool CM = B2 && Q == 3;
+    auto ld_pass = [&](int k) __attribute__((always_inline)) {
+        if constexpr (CM) {
+            const char* hp = reinterpret_cast<const char*>(h) + ((size_t)(p0 + pl + k * 32) * C) * 2;
+            const uint4 a = *reinterpret_cast<const uint4*>(hp + 16 * sub);
+            const uint2 c = *reinterpret_cast<const uint2*>(hp + 128 + 8 * sub);
+            v[k][0] = make_float4(bf_lo(a.x), bf_hi(a.x), bf_lo(a.y), bf_hi(a.y));
+            v[k][1] = make_float4(bf_lo(a.z), bf_hi(a.z), bf_lo(a.w), bf_hi(a.w));
+            v[k][2 % Q] = make_float4(bf_lo(c.x), bf_hi(c.x), bf_lo(c.y), bf_hi(c.y));
+        } else {
 #pragma unroll
-    for (int k = 0; k < HR_LA && k < HR_PASS; ++k)
+            for (int q = 0; q < Q; ++q) v[k][q] = head_ld4<B2>(h, src0 + (size_t)k * 32 * C + 4 * q);
+        }
+    };
 #pragma unroll
-        for (int q = 0; q < Q; ++q) v[k][q] = head_ld4<B2>(h, src0 + (size_t)k * 32 * C + 4 * q);
+    for (int k = 0; k < HR_LA && k < HR_PASS; ++k) ld_pass(k);
     // the lane's constants as 16-B loads (its 9 CL weights are contiguous in w_out[c][tap], its CL scale /
     // shift entries in the image's table rows): 9 Q + 2 Q vector loads instead of 11 CL scalar ones, which
     // were 5x the data loads' instruction count per block
     float wr[CL][9], scl[CL], shf[CL];
     {
         float4 wq[9 * Q], sq[Q], hq[Q];
-        const float4* wp = reinterpret_cast<const float4*>(w_out + (size_t)c0 * 9);
+        if constexpr (CM) {  // channels 8 sub .. + 7 (18 float4 of w_out), then 64 + 4 sub .. + 3 (9 float4)
+            const float4* wa = reinterpret_cast<const float4*>(w_out + (size_t)(8 * sub) * 9);
+            const float4* wb = reinterpret_cast<const float4*>(w_out + (size_t)(64 + 4 * sub) * 9);
 #pragma unroll
-        for (int i = 0; i < 9 * Q; ++i) wq[i] = wp[i];
+            for (int i = 0; i < 18; ++i) wq[i] = wa[i];
 #pragma unroll
-        for (int i = 0; i < Q; ++i) {
-            sq[i] = reinterpret_cast<const float4*>(tsc + (size_t)b * C + c0)[i];
-            hq[i] = reinterpret_cast<const float4*>(tsh + (size_t)b * C + c0)[i];
+            for (int i = 0; i < 9; ++i) wq[18 + i] = wb[i];
+            const float* ts = tsc + (size_t)b * C;
+            const float* th = tsh + (size_t)b * C;
+            sq[0] = reinterpret_cast<const float4*>(ts + 8 * sub)[0];
+            sq[1] = reinterpret_cast<const float4*>(ts + 8 * sub)[1];
+            sq[2 % Q] = reinterpret_cast<const float4*>(ts + 64 + 4 * sub)[0];
+            hq[0] = reinterpret_cast<const float4*>(th + 8 * sub)[0];
+            hq[1] = reinterpret_cast<const float4*>(th + 8 * sub)[1];
+            hq[2 % Q] = reinterpret_cast<const float4*>(th + 64 + 4 * sub)[0];
+        } else {
+            const float4* wp = reinterpret_cast<const float4*>(w_out + (size_t)c0 * 9);
+#pragma unroll
+            for (int i = 0; i < 9 * Q; ++i) wq[i] = wp[i];
+#pragma unroll
+            for (int i = 0; i < Q; ++i) {
+                sq[i] = reinterpret_cast<const float4*>(tsc + (size_t)b * C + c0)[i];
+                hq[i] = reinterpret_cast<const float4*>(tsh + (size_t)b * C + c0)[i];
+            }
         }
 #pragma unroll
         for (int f = 0; f < 36 * Q; ++f) {
@@ -612,10 +645,7 @@ __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int
 #pragma unroll
     for (int pass = 0; pass < HR_PASS; ++pass) {
         const int pg = p0 + pass * 32 + pl;
-        if (pass + HR_LA < HR_PASS) {
-#pragma unroll
-            for (int q = 0; q < Q; ++q) v[pass + HR_LA][q] = head_ld4<B2>(h, src0 + (size_t)(pass + HR_LA) * 32 * C + 4 * q);
-        }
+        if (pass + HR_LA < HR_PASS) ld_pass(pass + HR_LA);
         float acc[9];
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[t] = 0.f;
@@ -656,12 +686,16 @@ __global__ __launch_bounds__(256) void k_head8r(const float* __restrict__ h, int
 // 32-B records, as the tile form's store phase) from 9 broadcast x reads and 18 b128 weight reads.
 // No fp32 tile, one barrier, ~5-8 KB of LDS (the tile form held 35 KB: 4 workgroups per CU).
 // Needs HW % FR_PX == 0, and FR_PX % W == 0 or W % FR_PX == 0; C0 % 8 == 0.
+// fpx (round 6): pixels per workgroup, FR_PX at 64^2; at config 5's 256^2 rows FR_PX_WIDE: the 128-pixel blocks
+// (43,008 workgroups per 84-image pass) spent their time on the per-block prologue — three staged x rows,
+// the 9 x C0 weight transpose, the bias / table rows — and wrote 1.06 GB at 2.0 TB/s (r06_b layers).
 constexpr int FR_PX = 128;
+constexpr int FR_PX_WIDE = 1024;
 __global__ __launch_bounds__(256) void k_conv_first_rec(const float* __restrict__ x, int bmod, int H, int W, int C0,
                                                         const float* __restrict__ w0, int kpad,
                                                         const float* __restrict__ bias_b, char* __restrict__ y,
                                                         CondTab ct, int Bimg, int cfg, const float* __restrict__ tsc,
-                                                        const float* __restrict__ tsh, unsigned* ovf, int bf) {
+                                                        const float* __restrict__ tsh, unsigned* ovf, int bf, int fpx) {
     extern __shared__ __attribute__((aligned(16))) float fr[];  // w[9][C0] | bias[C0] | sc[C0] | sh[C0] | xr[nr][W]
     float* w = fr;
     float* bs = w + 9 * C0;
@@ -671,9 +705,9 @@ __global__ __launch_bounds__(256) void k_conv_first_rec(const float* __restrict_
     const int HW = H * W;
     const int b = blockIdx.y;
     const int tid = threadIdx.x;
-    const int p0 = blockIdx.x * FR_PX;
+    const int p0 = blockIdx.x * fpx;
     const int y0 = p0 / W;                                  // first row of the block's pixels
-    const int nrow = (FR_PX >= W ? FR_PX / W : 1) + 2;     // staged rows y0-1 .. y0+rows
+    const int nrow = (fpx >= W ? fpx / W : 1) + 2;         // staged rows y0-1 .. y0+rows
     const float* xb = x + (size_t)(b % bmod) * HW;
     for (int i = tid; i < nrow * W; i += 256) {
         const int r = i / W, c = i - (i / W) * W;
@@ -693,7 +727,7 @@ __global__ __launch_bounds__(256) void k_conv_first_rec(const float* __restrict_
     const int G8 = C0 / 8;
     char* dst = y + ((size_t)b * HW + p0) * C0 * 4;
     bool bad = false;
-    for (int item = tid; item < FR_PX * G8; item += 256) {
+    for (int item = tid; item < fpx * G8; item += 256) {
         const int pl = item / G8, g = item - (item / G8) * G8;
         const int p = p0 + pl;
         const int yy = p / W, xx = p - (p / W) * W;
@@ -1216,11 +1250,17 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
                 TCX_TRY(gn_tab(net, P, 0, P.P0, C, gn, ns, st));
                 // tile-free record kernel (r03_af: 143 -> 114 us at 64^2); the LDS-tile form for other shapes
                 if ((H * W) % FR_PX == 0 && (FR_PX % W == 0 || W % FR_PX == 0)) {
-                    const int nrow = (FR_PX >= W ? FR_PX / W : 1) + 2;
+                    static const int fr_wide = [] {  // TCX_FR_PX: pixels per block at W >= 256 (A/B)
+                        const char* e = getenv("TCX_FR_PX");
+                        const int v = e ? atoi(e) : FR_PX_WIDE;
+                        return (v >= FR_PX && v <= 4096 && (v & (v - 1)) == 0) ? v : FR_PX_WIDE;
+                    }();
+                    const int fpx = (W >= 256 && (H * W) % fr_wide == 0 && fr_wide % W == 0) ? fr_wide : FR_PX;
+                    const int nrow = (fpx >= W ? fpx / W : 1) + 2;
                     const size_t shr = ((size_t)12 * C + (size_t)nrow * W) * sizeof(float);
-                    hipLaunchKernelGGL(k_conv_first_rec, dim3(H * W / FR_PX, Bt), dim3(256), shr, st, x, B, H, W, C,
+                    hipLaunchKernelGGL(k_conv_first_rec, dim3(H * W / fpx, Bt), dim3(256), shr, st, x, B, H, W, C,
                                        c0.w, c0.kpad, P.bias0, (char*)P.a64, ct, B, cfg, P.sc(0), P.sh(0), h2.ovf,
-                                       fmt);
+                                       fmt, fpx);
                 } else {
                     hipLaunchKernelGGL(k_conv_first<2>, dim3(H * W / FIRST_PX, Bt), dim3(256), shm, st, x, B, H, W,
                                        C, c0.w, c0.kpad, P.bias0, P.a64, nullptr, ct, B, cfg, P.sc(0), P.sh(0),

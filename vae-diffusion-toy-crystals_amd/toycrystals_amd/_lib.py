@@ -119,6 +119,7 @@ _SIGS = {
     "tcx_f32_to_h2_scaled": (c_int, [c_fp, c_fp, c_size, c_fp, c_fp, c_fp, c_fp]),
     "tcx_unet_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int]),
     "tcx_set_sample_lanes": (c_int, [c_int]),
+    "tcx_debug_conv3mb": (c_int, [c_int]),
     "tcx_sde_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int, c_int, c_float]),
     "tcx_ode_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int, c_int, c_float]),
     "tcx_debug_fail_eval": (c_int, [c_int]),

@@ -26,8 +26,11 @@ def mark_updated(tensors) -> None:
     (sde_score_model.CondUNetTiny.tcx_pack, diffusion_prior.DiffusionPriorFiLM._tcx); without the bump
     an eval-mode forward after an optimiser step would reuse the pack of the previous weights (a sample
     grid after epoch 2 drawn with epoch-1 weights), as torch's in-place optimiser updates bump it."""
-    for t in tensors:
-        increment_version(t)
+    # one call for the whole list: per tensor the same call costs ~7 us each (0.7 ms per prior step), the list
+    # form ~6 us in total
+    ts = list(tensors)
+    if ts:
+        increment_version(ts)
 
 
 def _host_table(entries):
@@ -48,44 +51,103 @@ class Adam(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        """One fused tcx_adam launch per (param group, step count, device).
+
+        The host path is kept short (round 6): the prior's training step (100+ parameters) left the GPU idle
+        0.5-0.8 ms per step between the last backward kernel and the Adam launch while this loop ran a CPU
+        tensor add, an .item() and a ctypes struct per parameter (profiles/r06_d_*).  Now the per-parameter
+        `step` tensors of a group are 0-dim views of ONE CPU tensor (so state_dict() still holds one `step`
+        tensor per parameter, as torch.optim.Adam's) advanced by a single add, the counts are mirrored in a
+        Python list, and the kernel-argument table is rebuilt only when a storage pointer changes."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
         L = lib()
-        for group in self.param_groups:
+        if not hasattr(self, "_tcx_steps"):
+            self._tcx_steps, self._tcx_counts, self._tcx_masks = {}, {}, {}
+        for gi, group in enumerate(self.param_groups):
             beta1, beta2 = group["betas"]
-            by_step = {}
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
-                if p.grad.is_sparse:
-                    raise RuntimeError("Adam does not support sparse gradients")
-                if not p.is_cuda:
-                    raise RuntimeError("the fused Adam runs on the MI355X only (params must be on 'cuda')")
+            params = group["params"]
+            stor = self._tcx_steps.get(gi)
+            if stor is None or stor.numel() != len(params):
+                stor = self._tcx_steps[gi] = torch.zeros(len(params), dtype=torch.float32)
+                self._tcx_counts[gi] = [0] * len(params)
+            counts = self._tcx_counts[gi]
+            items, has = [], []
+            for i, p in enumerate(params):
+                g = p.grad
                 st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                if len(st) == 0 and g is not None:
+                    if g.is_sparse:
+                        raise RuntimeError("Adam does not support sparse gradients")
+                    if not p.is_cuda:
+                        raise RuntimeError("the fused Adam runs on the MI355X only (params must be on 'cuda')")
+                    if p.dtype != torch.float32 or not p.is_contiguous():
+                        raise RuntimeError("fused Adam is fp32-only and needs contiguous params")
+                    stor[i] = 0.0
+                    counts[i] = 0
+                    st["step"] = stor[i]
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                if not (p.is_contiguous() and st["exp_avg"].is_contiguous() and st["exp_avg_sq"].is_contiguous()):
-                    raise RuntimeError("fused Adam needs contiguous params and state")
-                if p.dtype != torch.float32:
-                    raise RuntimeError("fused Adam is fp32-only")
-                key = (int(st["step"].item()), p.device)
-                by_step.setdefault(key, []).append((p, g, st))
-            for (step, device), items in by_step.items():
-                entries = [TcxAdamTensor(p.data_ptr(), g.data_ptr(), s["exp_avg"].data_ptr(),
-                                         s["exp_avg_sq"].data_ptr(), p.numel()) for p, g, s in items]
-                table = _host_table(entries)
-                max_n = max(p.numel() for p, _, _ in items)
-                check(L.tcx_adam(table, len(entries), max_n, float(group["lr"]), float(beta1),
+                elif "step" in st and st["step"]._base is not stor:  # state loaded from a checkpoint
+                    v = float(st["step"])
+                    stor[i] = v
+                    counts[i] = int(v)
+                    st["step"] = stor[i]
+                has.append(g is not None)
+                if g is not None:
+                    items.append((p, g if g.is_contiguous() else g.contiguous(), st))
+                    counts[i] += 1
+            if not items:
+                continue
+            pattern = tuple(has)
+            if all(has):
+                stor.add_(1.0)
+            else:
+                mask = self._tcx_masks.get((gi, pattern))
+                if mask is None:
+                    mask = self._tcx_masks[(gi, pattern)] = torch.tensor(pattern, dtype=torch.float32)
+                stor.add_(mask)
+            steps = [counts[i] for i, h in enumerate(has) if h]
+            by_step = {}
+            if min(steps) == max(steps):
+                by_step[(steps[0], items[0][0].device)] = items
+            else:  # counts differ (a parameter skipped in some steps): one launch per count
+                for it, c in zip(items, steps):
+                    by_step.setdefault((c, it[0].device), []).append(it)
+            for (step, device), its in by_step.items():
+                table, n, max_n = self._table(gi, step, its)
+                check(L.tcx_adam(table, n, max_n, float(group["lr"]), float(beta1),
                                  float(beta2), float(group["eps"]), float(group["weight_decay"]), step,
                                  stream_ptr(device)), "tcx_adam")
-                mark_updated(p for p, _, _ in items)
+                mark_updated([p for p, _, _ in its])
         return loss
+
+    def _table(self, gi, step, items):
+        """The ctypes {p, g, m, v, n} table of these parameters, cached while every pointer is unchanged."""
+        key = tuple((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr())
+                    for p, g, st in items)
+        cache = getattr(self, "_tcx_tables", None)
+        if cache is None:
+            cache = self._tcx_tables = {}
+        ck = (gi, id(items[0][0]), len(items))  # (the step count is a launch argument, not in the table)
+        hit = cache.get(ck)
+        if hit is None or hit[0] != key:
+            for p, g, st in items:
+                if not (p.is_contiguous() and st["exp_avg"].is_contiguous() and st["exp_avg_sq"].is_contiguous()):
+                    raise RuntimeError("fused Adam needs contiguous params and state")
+            entries = [TcxAdamTensor(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                                     st["exp_avg_sq"].data_ptr(), p.numel()) for p, g, st in items]
+            hit = (key, _host_table(entries), len(entries), max(p.numel() for p, _, _ in items))
+            if len(cache) > 64:
+                cache.clear()
+            cache[ck] = hit
+        return hit[1], hit[2], hit[3]
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._tcx_tables = {}  # (the loaded `step` tensors are re-bound to the group views at the next step)
 
 
 @torch.no_grad()
