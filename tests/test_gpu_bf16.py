@@ -639,14 +639,6 @@ def test_b2_256px_forward_chunk_major_skips_bit_identical(tmp_path):
 
 
 
-@pytest.mark.parametrize("B,C1,C2,H,co", [
-    (1, 96, 0, 256, 96),     # 256-px rows, one row per tile (down1_1 / up1_1 / us1)
-    (1, 96, 96, 256, 96),    # two b2 sources (up1.net.0)
-    (3, 96, 0, 128, 192),    # 128-px rows, two n blocks, odd batch (down2.net.0)
-    (1, 192, 192, 128, 96),  # Cin 384 over two sources (up2.net.0)
-    (2, 192, 0, 64, 192),    # 64-px rows (the mid block)
-    (2, 192, 0, 128, 192),   # Cin 192: an even number of 9-pair periods (down2_1, us2)
-])
 @pytest.fixture
 def conv3mb_everywhere():
     """k_conv3mb on every b2 3x3 shape it covers (the default takes it at Cin >= 192 with a b2 output only)"""
@@ -655,6 +647,14 @@ def conv3mb_everywhere():
     L().tcx_debug_conv3mb(prev)
 
 
+@pytest.mark.parametrize("B,C1,C2,H,co", [
+    (1, 96, 0, 256, 96),     # 256-px rows, one row per tile (down1_1 / up1_1 / us1)
+    (1, 96, 96, 256, 96),    # two b2 sources (up1.net.0)
+    (3, 96, 0, 128, 192),    # 128-px rows, two n blocks, odd batch (down2.net.0)
+    (1, 192, 192, 128, 96),  # Cin 384 over two sources (up2.net.0)
+    (2, 192, 0, 64, 192),    # 64-px rows (the mid block)
+    (2, 192, 0, 128, 192),   # Cin 192: an even number of 9-pair periods (down2_1, us2)
+])
 def test_b2_conv3mb_vs_float64_on_rounded_operands(B, C1, C2, H, co, conv3mb_everywhere):
     """k_conv3mb (round 6: config 5's 3x3 convs on v_mfma_f32_16x16x32_bf16 tap pairs, three-slot weight
     ring) on b2 sources against float64 on the same bf16-rounded operands: only the fp32 accumulation
@@ -730,3 +730,24 @@ def test_b2_conv3mb_equals_conv3lb_bit_for_bit(B, C1, C2, H, co, ob2):
         finally:
             L().tcx_debug_conv3mb(prev)
     assert torch.equal(out[2][0], out[0][0]) and torch.equal(out[2][1], out[0][1])
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 128, 128, 96), (1, 64, 128, 96)])
+def test_b2_upsample_from_b2_source_equals_fp32_source(B, H, W, C):
+    """config 5's us1 with up2.net.3's output stored as b2 (round 6): the segmented band upsample reading the 2-byte
+    source (GroupNorm + SiLU tables applied while staging) equals the same kernel on an fp32 source holding the
+    same bf16 values, bit for bit; a shape outside the segmented band form is refused"""
+    x = torch.from_numpy(bf(rng.standard_normal((B, H, W, C)).astype(np.float32) * 2)).cuda()
+    xb = to_b2(x)
+    sc = torch.rand(B, C, device="cuda") + 0.5
+    sh = torch.randn(B, C, device="cuda")
+    y32 = torch.empty((B, 2 * H, 2 * W, C), dtype=torch.int16, device="cuda")
+    yb2 = torch.full((B, 2 * H, 2 * W, C), -1, dtype=torch.int16, device="cuda")
+    chk(L().tcx_upsample2x_b2(x.data_ptr(), y32.data_ptr(), B, H, W, C, sc.data_ptr(), sh.data_ptr(), st()))
+    chk(L().tcx_upsample2x_b2_from_b2(xb.data_ptr(), yb2.data_ptr(), B, H, W, C, sc.data_ptr(), sh.data_ptr(), st()))
+    torch.cuda.synchronize()
+    assert torch.equal(y32, yb2)
+    small = to_b2(torch.randn(1, 16, 16, 96, device="cuda"))
+    out = torch.empty((1, 32, 32, 96), dtype=torch.int16, device="cuda")
+    assert L().tcx_upsample2x_b2_from_b2(small.data_ptr(), out.data_ptr(), 1, 16, 16, 96, sc.data_ptr(), sh.data_ptr(),
+                                         st()) != 0
