@@ -314,6 +314,7 @@ def test_weight_scale_extremes():
     (2, 192, 192, 16, True, False),   # proj: residual, fp32 out (k_lin1x1)
     (2, 192, 576, 16, False, True),   # qkv: h2 out (k_lin1x1)
     (4, 96, 288, 8, False, False),    # 3 chunks (odd count), 3 column blocks
+    (2, 192, 384, 16, True, True),    # two 192-column tiles (8-wave form), residual and h2 out
     (1, 32, 96, 16, False, True),     # one chunk
     (3, 64, 96, 8, True, False),      # M = 192, not whole 128-row tiles: im2col kernel
 ])
