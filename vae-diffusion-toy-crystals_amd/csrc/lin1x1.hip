@@ -18,24 +18,20 @@
 namespace tcx {
 namespace {
 
-constexpr int X_TM = 128;                 // rows (pixels) per tile: 4 row blocks x 32
+constexpr int X_TM = 128;                 // rows (pixels) per tile: 4 waves x 32
 constexpr int X_ABYTES = X_TM * 128;      // A chunk: 128 rows x 32 channels h2
-// B chunk: 96 NG weight rows x 32 channels h2.  NG = 1: 4 waves, one 96-column group; NG = 2 (round 6): 8 waves,
-// waves 4-7 take columns 96-191 of the same A tile, so qkv (576) and proj (192) re-read their A tile from L2 once
-// per 192 output columns instead of per 96 (each wave's work and registers are the 4-wave form's)
-__host__ __device__ constexpr int x_stage(int NG) { return X_ABYTES + NG * 96 * 128; }
-// s_waitcnt vmcnt(n): one stage in flight — per wave 4 A + 3 B DMA instructions (NG = 1) or 2 A + 3 B (NG = 2)
-__host__ __device__ constexpr int x_wait_stage(int NG) { return 0x0F70 | (NG == 1 ? 7 : 5); }
+constexpr int X_BBYTES = 96 * 128;        // B chunk: 96 weight rows x 32 channels h2
+constexpr int X_STAGE = X_ABYTES + X_BBYTES;
+constexpr int X_WAIT_VM7 = 0x0F77;        // s_waitcnt vmcnt(7): one stage (4 + 3 DMA per wave) in flight
 constexpr int X_WAIT_VM0 = 0x0F70;
 
 __device__ __forceinline__ void x_dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
 
-template <bool BF, int NG>
-__global__ __launch_bounds__(256 * NG, 2 / NG) void k_lin1x1(ConvParams p) {
+template <bool BF>
+__global__ __launch_bounds__(256, 2) void k_lin1x1(ConvParams p) {
     constexpr int NT = 3;
-    constexpr int X_STAGE = x_stage(NG);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     char* const smc = reinterpret_cast<char*>(sm);
     int lz;  // LDS-DMA destinations from a base the optimiser cannot fold to a constant (conv3l.hip)
@@ -44,43 +40,39 @@ __global__ __launch_bounds__(256 * NG, 2 / NG) void k_lin1x1(ConvParams p) {
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, li = lane & 31, lh = lane >> 5;
-    const int wg = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave of the workgroup (0 .. 4 NG - 1)
-    const int wv = wg & 3;                                       // its row block
-    const int cg = wg >> 2;                                      // its 96-column group
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int mblk = tile / p.n_nblk;
     const int nblk = tile - mblk * p.n_nblk;
-    const int m0 = mblk * X_TM, n0 = nblk * 96 * NG;
+    const int m0 = mblk * X_TM, n0 = nblk * 96;
     const int nch = p.Cin / 32;
     const __amdgpu_buffer_rsrc_t ra = mk_rsrc(p.x1, p.bytes1);
     const __amdgpu_buffer_rsrc_t rw = mk_rsrc(p.w, p.bytesw);
 
-    // DMA plan: A instructions (8 rows each) 4 wg .. 4 wg + 3 (NG = 1) / 2 wg .. 2 wg + 1 (NG = 2), B instructions
-    // 3 wg .. 3 wg + 2 (the B tile's 96 NG rows)
-    constexpr int AQ = 4 / NG;
+    // DMA plan: A instructions 4 wv .. 4 wv + 3 (8 rows each), B instructions 3 wv .. 3 wv + 2
     const int lr = lane >> 3, lp = lane & 7;
-    int aoff[AQ], boff[3];
+    int aoff[4], boff[3];
     // b2 source (BF, p.bf == 2, h2.hpp): a 32-channel chunk is 64 B of hi halves; lane lp of a row
     // fills physical piece lp with logical piece L = lp ^ swizzle, whose hi data (L even) sits at 16 (L / 2)
     // (an odd L, a lo piece, is never read by BF: it gets the same bytes)
     const bool b2 = BF && p.bf == 2;
 #pragma unroll
-    for (int q = 0; q < AQ; ++q) {
-        const int r = 8 * (AQ * wg + q) + lr;
+    for (int q = 0; q < 4; ++q) {
+        const int r = 8 * (4 * wv + q) + lr;
         const int L = lp ^ ((r >> 1) & 7);
         aoff[q] = b2 ? (m0 + r) * p.Cin * 2 + 16 * (L >> 1) : (m0 + r) * p.Cin * 4 + 16 * L;
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-        const int r = 8 * (3 * wg + q) + lr;
+        const int r = 8 * (3 * wv + q) + lr;
         boff[q] = (n0 + r) * p.kpad * 4 + 16 * (lp ^ ((r >> 1) & 7));
     }
     auto issue = [&](int c, int buf) {
         char* const d = smd + buf * X_STAGE;
 #pragma unroll
-        for (int q = 0; q < AQ; ++q) x_dma16(ra, d + (AQ * wg + q) * 1024, aoff[q], c * (b2 ? 64 : 128));
+        for (int q = 0; q < 4; ++q) x_dma16(ra, d + (4 * wv + q) * 1024, aoff[q], c * (b2 ? 64 : 128));
 #pragma unroll
-        for (int q = 0; q < 3; ++q) x_dma16(rw, d + X_ABYTES + (3 * wg + q) * 1024, boff[q], c * 128);
+        for (int q = 0; q < 3; ++q) x_dma16(rw, d + X_ABYTES + (3 * wv + q) * 1024, boff[q], c * 128);
     };
 
     f32x16 acc[NT];
@@ -96,7 +88,7 @@ __global__ __launch_bounds__(256 * NG, 2 / NG) void k_lin1x1(ConvParams p) {
     if (nch > 1) issue(1, 1);
     for (int c = 0; c < nch; ++c) {
         const int buf = c & 1;
-        if (c + 1 < nch) __builtin_amdgcn_s_waitcnt(x_wait_stage(NG));
+        if (c + 1 < nch) __builtin_amdgcn_s_waitcnt(X_WAIT_VM7);
         else __builtin_amdgcn_s_waitcnt(X_WAIT_VM0);
         __builtin_amdgcn_s_barrier();
         h8 ah[2], al[2], bh[2][NT], bl[2][NT];
@@ -107,8 +99,8 @@ __global__ __launch_bounds__(256 * NG, 2 / NG) void k_lin1x1(ConvParams p) {
             if (!BF) al[s] = rd(buf, 0, ra0, ph + 1);
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
-                bh[s][n] = rd(buf, X_ABYTES, 96 * cg + 32 * n + li, ph);
-                if (!BF) bl[s][n] = rd(buf, X_ABYTES, 96 * cg + 32 * n + li, ph + 1);
+                bh[s][n] = rd(buf, X_ABYTES, 32 * n + li, ph);
+                if (!BF) bl[s][n] = rd(buf, X_ABYTES, 32 * n + li, ph + 1);
             }
         }
 #pragma unroll
@@ -137,11 +129,7 @@ __global__ __launch_bounds__(256 * NG, 2 / NG) void k_lin1x1(ConvParams p) {
         }
     }
     __syncthreads();  // LDS -> the epilogue's reduction scratch
-    if constexpr (NG == 1) {
-        conv_epilogue<NT, BF ? 2 : 1, 4>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
-    } else {  // (no GroupNorm partials: lin1x1_applies keeps p.gn null for NG = 2)
-        conv_epi_store<NT, BF ? 2 : 1, 4>(p, acc, m0, n0 + 96 * cg, wv, lane, reinterpret_cast<double*>(sm));
-    }
+    conv_epilogue<NT, BF ? 2 : 1, 4>(p, acc, m0, n0, wv, tid, reinterpret_cast<double*>(sm));
 }
 
 }  // namespace
@@ -153,42 +141,23 @@ bool lin1x1_applies(const ConvParams& p, int cout_pad) {
            p.HoWo % X_TM == 0 && p.osy == 1 && p.osx == 1 && p.sc1 == nullptr && p.bmod <= 0;
 }
 
-// 192-column tiles (8 waves) where the padded width allows and no GroupNorm partials are asked for (qkv 576,
-// proj 192); TCX_LIN_NG=1 keeps the 96-column 4-wave form (A/B)
-int lin_ng(const ConvParams& p, int cout_pad) {
-    static const int forced = [] {
-        const char* e = getenv("TCX_LIN_NG");
-        return (e && e[0] == '1') ? 1 : 2;
-    }();
-    return (forced == 2 && cout_pad % 192 == 0 && p.Cout % 192 == 0 && p.gn == nullptr) ? 2 : 1;
-}
-
-template <bool BF, int NG>
-int launch_lin_one(ConvParams& p, hipStream_t st) {
-    constexpr size_t shm = 2 * (size_t)x_stage(NG);
-    static_assert(shm <= 80 * 1024, "two 4-wave / one 8-wave workgroup(s) per CU at 80 KB");
-    static bool attr = false;
-    auto kc = &k_lin1x1<BF, NG>;
-    if (!attr) {
+int launch_lin1x1(ConvParams& p, int cout_pad, hipStream_t st) {
+    p.n_nblk = cout_pad / 96;
+    if (p.M == 0) return TCX_OK;
+    prof_begin(st);
+    constexpr size_t shm = 2 * (size_t)X_STAGE;
+    static bool attr[2] = {false, false};
+    auto kc = p.bf ? &k_lin1x1<true> : &k_lin1x1<false>;
+    if (!attr[p.bf ? 1 : 0]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kc), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)shm) != hipSuccess) {
             set_error("tcx_conv2d_h2: cannot enable %zu B of dynamic LDS", shm);
             return TCX_EHIP;
         }
-        attr = true;
+        attr[p.bf ? 1 : 0] = true;
     }
-    hipLaunchKernelGGL(kc, dim3((p.M / X_TM) * p.n_nblk), dim3(256 * NG), shm, st, p);
-    return check_launch("tcx_conv2d_h2(1x1)");
-}
-
-int launch_lin1x1(ConvParams& p, int cout_pad, hipStream_t st) {
-    const int ng = lin_ng(p, cout_pad);
-    p.n_nblk = cout_pad / (96 * ng);
-    if (p.M == 0) return TCX_OK;
-    prof_begin(st);
-    int rc;
-    if (ng == 2) rc = p.bf ? launch_lin_one<true, 2>(p, st) : launch_lin_one<false, 2>(p, st);
-    else rc = p.bf ? launch_lin_one<true, 1>(p, st) : launch_lin_one<false, 1>(p, st);
+    hipLaunchKernelGGL(kc, dim3((p.M / X_TM) * p.n_nblk), dim3(256), shm, st, p);
+    const int rc = check_launch("tcx_conv2d_h2(1x1)");
     prof_end(st, 2.0 * (double)p.M * p.Cout * p.Cin);
     return rc;
 }
