@@ -378,8 +378,8 @@ int tcx_debug_fail_eval(int k);
 /* Test hook (round 6): which 3x3 kernel runs config 5's 2-byte bf16 convs on this host thread — 0 k_conv3lb
  * only, 1 the measured default (k_conv3mb at Cin >= 192 with a 2-byte output), 2 k_conv3mb on every shape it
  * covers, -1 back to the TCX_CONV3MB environment default.  Returns the previous override.  Both kernels sum
- * the same bf16 products in the same k order: the outputs are bit-identical (the fp64 GroupNorm partials
- * to fp64 rounding). */
+ * the same bf16 products in the same k order: the outputs are bit-identical (the GroupNorm partials to the
+ * fp32 rounding of their per-lane sums). */
 int tcx_debug_conv3mb(int mode);
 
 /* (Workspace: tcx_sde_workspace_size(net, B, H, W, n_steps, guidance) bytes — see the breaking-change

@@ -738,8 +738,9 @@ def test_b2_conv3mb_repeats_bit_for_bit(Bt, H, C1, C2, co, conv3mb_everywhere):
 def test_b2_conv3mb_equals_conv3lb_bit_for_bit(B, C1, C2, H, co, ob2):
     """k_conv3mb (16x16x32 tap pairs) and k_conv3lb (32x32x16 taps) on the same b2 sources: the MFMAs sum the
     same bf16 products in the same k order (tap, then channel) into fp32, so the outputs are bit-identical —
-    which is what lets the library pick either per layer; the fp64 GroupNorm partials are summed over the
-    accumulator layouts in different orders (16x16 vs 32x32 blocks): equal to fp64 rounding"""
+    which is what lets the library pick either per layer; the GroupNorm partials are summed per lane in fp32 over
+    different accumulator layouts (16x16 vs 32x32 blocks) before the fp64 fold: equal to fp32 rounding of those
+    partial sums (the gate of test_b2_conv_equals_the_record_conv)"""
     x1 = dev(nhwc(rng.standard_normal((B, C1, H, H))))
     x2 = dev(nhwc(rng.standard_normal((B, C2, H, H)))) if C2 else None
     w = (rng.standard_normal((co, C1 + C2, 3, 3)) / np.sqrt(9 * (C1 + C2))).astype(np.float32)
@@ -752,7 +753,7 @@ def test_b2_conv3mb_equals_conv3lb_bit_for_bit(B, C1, C2, H, co, ob2):
         finally:
             L().tcx_debug_conv3mb(prev)
     assert torch.equal(out[2][0], out[0][0])
-    np.testing.assert_allclose(out[2][1].cpu().numpy(), out[0][1].cpu().numpy(), rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(out[2][1].cpu().numpy(), out[0][1].cpu().numpy(), rtol=1e-5, atol=1e-3)
 
 
 @pytest.mark.parametrize("B,H,W,C", [(2, 128, 128, 96), (1, 64, 128, 96)])

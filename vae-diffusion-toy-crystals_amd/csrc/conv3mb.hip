@@ -350,8 +350,8 @@ int launch3mb(const ConvParams& p, hipStream_t st) {
 // 926 us, up2.net.0 824 vs 855, mid.net.0 211 vs 218), slower at Cin = 96 (down1.net.3 1336 vs 1269 us,
 // up1.net.0 1954 vs 1908) and with an fp32 output (up2.net.3 318 vs 284, mid.net.3 234 vs 219) — so the
 // default takes those layers only.  Same products, same k order: the two kernels' outputs are bit-identical
-// (tests/test_gpu_bf16.py test_b2_conv3mb_equals_conv3lb_bit_for_bit; the fp64 GroupNorm partials agree to
-// fp64 rounding: they are summed over the 16x16 vs 32x32 accumulator layouts).  TCX_CONV3MB=0: never, 2: every b2 shape.
+// (tests/test_gpu_bf16.py test_b2_conv3mb_equals_conv3lb_bit_for_bit; the GroupNorm partials agree to the fp32
+// rounding of their per-lane sums, taken over the 16x16 vs 32x32 accumulator layouts).  TCX_CONV3MB=0: never, 2: every b2 shape.
 thread_local int g_conv3mb_force = -1;  // tcx_debug_conv3mb (tests): overrides the environment on this thread
 int conv3mb_mode() {
     static const int m = [] {
