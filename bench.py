@@ -294,9 +294,9 @@ def main() -> int:
         peak = F16_PEAK_TFLOPS / SPLIT_PRODUCTS
         peak_basis = "2500 TFLOP/s dense f16 MFMA / 3 products per fp32 MAC; achieved in fp32-equivalent FLOPs"
     elif args.precision == "bf16":
-        kname = ("bf16 single-product convs (config 5): k_conv3lb (LDS-DMA 3x3 at 64/128/256-px rows), k_conv3g, "
-                 "k_conv4s2g, k_lin1x1, k_conv<SPL=2> — one v_mfma_f32_32x32x16_bf16 per MAC; all conv launches "
-                 "of the pass")
+        kname = ("bf16 single-product convs (config 5): k_conv3lb (LDS-DMA 3x3 at 64/128/256-px rows, "
+                 "v_mfma_f32_32x32x16_bf16) and k_conv3mb (16x16x32 tap pairs, Cin >= 192), k_conv4s2g (chunk-major "
+                 "skip planes), k_lin1x1 — one bf16 MFMA per MAC; all conv launches of the pass")
         peak = F16_PEAK_TFLOPS
         peak_basis = "2500 TFLOP/s dense bf16 MFMA"
     else:

@@ -186,12 +186,6 @@ int tcx_gn_apply_tab_b2(const void* x, void* y, int Bt, int HW, int C, const flo
                         int silu, int in_b2, void* stream);
 int tcx_upsample2x_b2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
                       void* stream);
-/* Config 5 (round 6): tcx_upsample2x_b2 from a 2-byte bf16 SOURCE x (up2.net.3's pre-GroupNorm output stored
- * as b2), GroupNorm + SiLU of the source from the tables, 2-byte bf16 output; the segmented band shapes only
- * (source rows wider than one LDS band, e.g. 128 x 96) — otherwise TCX_EINVAL.  The same values as
- * tcx_upsample2x_b2 on an fp32 source holding the same bf16 values, bit for bit. */
-int tcx_upsample2x_b2_from_b2(const void* x, void* y, int Bt, int H, int W, int C, const float* scale,
-                              const float* shift, void* stream);
 int tcx_attention_split_b2(const void* qkv, void* out, int Bt, int N, int C, int heads, void* stream);
 
 /* tcx_conv2d_h2 with the fragment-ordered weights (wfrag, or NULL) and a GroupNorm+SiLU prologue per

@@ -754,24 +754,3 @@ def test_b2_conv3mb_equals_conv3lb_bit_for_bit(B, C1, C2, H, co, ob2):
             L().tcx_debug_conv3mb(prev)
     assert torch.equal(out[2][0], out[0][0])
     np.testing.assert_allclose(out[2][1].cpu().numpy(), out[0][1].cpu().numpy(), rtol=1e-5, atol=1e-3)
-
-
-@pytest.mark.parametrize("B,H,W,C", [(2, 128, 128, 96), (1, 64, 128, 96)])
-def test_b2_upsample_from_b2_source_equals_fp32_source(B, H, W, C):
-    """config 5's us1 with up2.net.3's output stored as b2 (round 6): the segmented band upsample reading the 2-byte
-    source (GroupNorm + SiLU tables applied while staging) equals the same kernel on an fp32 source holding the
-    same bf16 values, bit for bit; a shape outside the segmented band form is refused"""
-    x = torch.from_numpy(bf(rng.standard_normal((B, H, W, C)).astype(np.float32) * 2)).cuda()
-    xb = to_b2(x)
-    sc = torch.rand(B, C, device="cuda") + 0.5
-    sh = torch.randn(B, C, device="cuda")
-    y32 = torch.empty((B, 2 * H, 2 * W, C), dtype=torch.int16, device="cuda")
-    yb2 = torch.full((B, 2 * H, 2 * W, C), -1, dtype=torch.int16, device="cuda")
-    chk(L().tcx_upsample2x_b2(x.data_ptr(), y32.data_ptr(), B, H, W, C, sc.data_ptr(), sh.data_ptr(), st()))
-    chk(L().tcx_upsample2x_b2_from_b2(xb.data_ptr(), yb2.data_ptr(), B, H, W, C, sc.data_ptr(), sh.data_ptr(), st()))
-    torch.cuda.synchronize()
-    assert torch.equal(y32, yb2)
-    small = to_b2(torch.randn(1, 16, 16, 96, device="cuda"))
-    out = torch.empty((1, 32, 32, 96), dtype=torch.int16, device="cuda")
-    assert L().tcx_upsample2x_b2_from_b2(small.data_ptr(), out.data_ptr(), 1, 16, 16, 96, sc.data_ptr(), sh.data_ptr(),
-                                         st()) != 0

@@ -35,11 +35,11 @@ def main():
         tot[k] = (n, rf, rw)
         print(f"{k[:60]:60s} {n:6d} {rf:20.2f} {rw:16.2f}")
     # the launches bench.py's roofline times: the implicit-GEMM convs (k_conv<...>, k_conv3g<...>, ...)
-    conv = [v for k, v in tot.items() if re.match(r"tcx::(k_conv(3g|3p|3l|3lg|3lb|3m|4s2h|4s2g)?|k_lin1x1)<", k)]
+    conv = [v for k, v in tot.items() if re.match(r"tcx::(k_conv(3g|3p|3l|3lg|3lb|3m|3mb|4s2h|4s2g)?|k_lin1x1)<", k)]
     n = sum(v[0] for v in conv)
     if n:
         avg = sum(v[0] * (v[1] + v[2]) for v in conv) / n
-        print(f"\nconv launches (k_conv<>, k_conv3g<>, k_conv3l<>, k_conv3lg<>, k_conv3lb<>, k_conv3m<>, k_conv3p<>, k_conv4s2h<>, k_conv4s2g<>, k_lin1x1<>): {n}, average HBM bytes per launch (read x2 + write) = "
+        print(f"\nconv launches (k_conv<>, k_conv3g<>, k_conv3l<>, k_conv3lg<>, k_conv3lb<>, k_conv3m<>, k_conv3mb<>, k_conv3p<>, k_conv4s2h<>, k_conv4s2g<>, k_lin1x1<>): {n}, average HBM bytes per launch (read x2 + write) = "
               f"{avg:.1f} MB")
 
 

@@ -30,15 +30,15 @@ typedef unsigned u4 __attribute__((ext_vector_type(4)));
     do { \
 _Pragma("unroll") \
         for (int u = 0; u < KI; ++u) {  /* BF: the hi pieces only (global piece 2 pc) */ \
-            const int i = tid + NTHR * u; \
+            const int i = tid + 512 * u; \
             const int j = i / KPL, pc = i - (i / KPL) * KPL; \
-            if (KT * KPL % NTHR == 0 || i < KT * KPL) \
+            if (KT * KPL % 512 == 0 || i < KT * KPL) \
                 kreg[u] = *reinterpret_cast<const f4*>(base + (size_t)(k0 + j) * rs + (size_t)(C + h * D) * ESZ + \
                                                        (B2 ? pc : BF ? 2 * pc : pc) * 16); \
         } \
 _Pragma("unroll") \
         for (int u = 0; u < VI; ++u) { \
-            const int i = tid + NTHR * u; \
+            const int i = tid + 512 * u; \
             if (i < (KT / 2) * G) { \
                 const int g = i / (KT / 2), jp = i - g * (KT / 2);  /* key pair (2 jp, 2 jp + 1), dim group g */ \
                 const char* src = base + (size_t)(k0 + 2 * jp) * rs + (size_t)(2 * C + h * D) * ESZ + g * 8 * ESZ; \
@@ -56,13 +56,13 @@ _Pragma("unroll") \
         unsigned* Vl = Vlb(st); \
 _Pragma("unroll") \
         for (int u = 0; u < KI; ++u) { \
-            const int i = tid + NTHR * u; \
+            const int i = tid + 512 * u; \
             const int j = i / KPL, pc = i - (i / KPL) * KPL; \
-            if (KT * KPL % NTHR == 0 || i < KT * KPL) *reinterpret_cast<f4*>(Ks + j * KSB + pc * 16) = kreg[u]; \
+            if (KT * KPL % 512 == 0 || i < KT * KPL) *reinterpret_cast<f4*>(Ks + j * KSB + pc * 16) = kreg[u]; \
         } \
 _Pragma("unroll") \
         for (int u = 0; u < VI; ++u) { \
-            const int i = tid + NTHR * u; \
+            const int i = tid + 512 * u; \
             if (i < (KT / 2) * G) { \
                 const int g = i / (KT / 2), jp = i - g * (KT / 2); \
                 const int j = 2 * jp; \
@@ -95,22 +95,13 @@ __host__ __device__ constexpr int attn_ksb(int D, bool BF) { return (BF ? D * 2 
 // 1,711 MB read per launch for 302 MB of qkv, profiles/r05_t_cfg5_pmc_traffic.txt).  With xcd_remap the
 // query blocks of an (image, head), and the heads of an image (whose K / V share cache lines of the token
 // rows), run on one XCD at about the same time.
-// QW (round 6): waves per workgroup (32 queries each), KT: keys per staged tile.  QW = 8, KT = 128 is the
-// round-1..5 form (one 98-KB workgroup per CU: two waves per SIMD whatever the registers allow).  The bf16 forms
-// stage no lo V^T, so QW = 4, KT = 64 needs 16 KB per stage: at 165 VGPRs three 4-wave workgroups fit a CU
-// (three waves per SIMD), the latency of one workgroup's tile loads and barrier hidden by the others.
-__host__ __device__ constexpr size_t attn_lds_bytes(int D, int FMT, int KT) {
-    return 2 * ((size_t)KT * ((FMT >= 1 ? D * 2 : D * 4) + 16) + (FMT >= 1 ? 1 : 2) * (size_t)((D + 31) / 32 * 32) *
-                (KT / 2 + 4) * 4);
-}
-template <int D, int FMT, int QW = 8, int KT = 128>
-__global__ __launch_bounds__(64 * QW) void k_attention_split(const char* __restrict__ qkv, char* __restrict__ out, int N,
+template <int D, int FMT>
+__global__ __launch_bounds__(512) void k_attention_split(const char* __restrict__ qkv, char* __restrict__ out, int N,
                                                          int C, float scale, int xcd) {
-    constexpr int NTHR = 64 * QW;
-    constexpr int QB = 32 * QW;  // queries per workgroup
     constexpr bool BF = FMT >= 1, B2 = FMT == 2;
     constexpr int ESZ = B2 ? 2 : 4;  // bytes per element of qkv / out
     static_assert(D % 16 == 0 && D <= 64, "split attention: head dim multiple of 16, <= 64");
+    constexpr int KT = 128;            // keys per staged tile
     constexpr int NST = KT / 32;       // 32-key subtiles
     constexpr int DS = D / 16;         // 16-deep steps of Q.K
     constexpr int DT = (D + 31) / 32;  // 32-row tiles of O^T
@@ -120,7 +111,7 @@ __global__ __launch_bounds__(64 * QW) void k_attention_split(const char* __restr
     // two LDS stages (tile t computed from one while tile t+1, loaded into registers during that
     // compute, is written to the other): [2][K | V^T hi | V^T lo]
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int STAGE = KT * KSB + (BF ? 1 : 2) * DP * VSW * 4;  // (BF: no lo V^T plane)
+    constexpr int STAGE = KT * KSB + 2 * DP * VSW * 4;
     int b = blockIdx.z, h = blockIdx.y, qb = blockIdx.x;
     if (xcd) {
         const int nq = gridDim.x, nh = gridDim.y;
@@ -135,7 +126,7 @@ __global__ __launch_bounds__(64 * QW) void k_attention_split(const char* __restr
     const char* base = qkv + (size_t)b * N * rs;
     const int lane = tid & 63, w = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
-    const int q = qb * QB + w * 32 + li;
+    const int q = qb * 256 + w * 32 + li;
     const float scale2 = scale * 1.4426950408889634f;  // log2(e) / sqrt(D)
     h8 qh[DS], ql[DS];
     {
@@ -155,11 +146,11 @@ __global__ __launch_bounds__(64 * QW) void k_attention_split(const char* __restr
     constexpr bool ONES = BF && DP > D;  // measured: 256^2 bf16 1390 -> 1313 us; the f16x3 form at N = 256 (two key tiles) lost 7 %
     constexpr unsigned ONE2 = 0x3F803F80u;  // two bf16 ones per dword
     if (DP > D) {
-        for (int i = tid; i < (DP - D) * VSW; i += NTHR) {
+        for (int i = tid; i < (DP - D) * VSW; i += 512) {
 #pragma unroll
             for (int st = 0; st < 2; ++st) {
                 Vhb(st)[D * VSW + i] = ONES && i < VSW ? ONE2 : 0u;
-                if (!BF) Vlb(st)[D * VSW + i] = 0u;
+                Vlb(st)[D * VSW + i] = 0u;
             }
         }
     }
@@ -170,8 +161,8 @@ __global__ __launch_bounds__(64 * QW) void k_attention_split(const char* __restr
     constexpr int KP = D / 4;  // 16-B pieces per K row
     constexpr int KPL = BF ? KP / 2 : KP;  // pieces staged per K row (BF: the hi pieces)
     constexpr int G = D / 8;   // 8-dim groups per V row
-    constexpr int KI = (KT * KPL + NTHR - 1) / NTHR;      // K pieces per thread (guarded when ragged)
-    constexpr int VI = ((KT / 2) * G + NTHR - 1) / NTHR;  // V (key pair, dim group) items per thread
+    constexpr int KI = (KT * KPL + 511) / 512;       // K pieces per thread (guarded when ragged)
+    constexpr int VI = ((KT / 2) * G + 511) / 512;   // V (key pair, dim group) items per thread
     f4 kreg[KI];        // native vectors: arrays of HIP's float4/uint4 structs stayed in scratch here
     u4 vreg[VI][4];
     TCX_ATT_LOAD(0);
@@ -309,23 +300,14 @@ __global__ __launch_bounds__(64 * QW) void k_attention_split(const char* __restr
         }
 }
 
-// TCX_ATTN_Q4=0: config 5's b2 attention on the 8-wave 128-key form instead of 4 waves x 64 keys (A/B)
-bool attn_q4_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("TCX_ATTN_Q4");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-template <int D, int FMT, int QW, int KT>
-int launch_split_form(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
+template <int D, int FMT>
+int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
     const float scale = (float)(1.0 / std::sqrt((double)D));
-    constexpr size_t shm = attn_lds_bytes(D, FMT, KT);
-    static_assert(shm <= 160 * 1024, "LDS");
+    constexpr int DP = (D + 31) / 32 * 32;
+    constexpr size_t shm = 2 * ((size_t)128 * attn_ksb(D, FMT >= 1) + 2 * (size_t)DP * (128 / 2 + 4) * 4);
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D, FMT, QW, KT>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D, FMT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) {
             set_error("tcx_attention_split: cannot enable %zu B of dynamic LDS", shm);
             return TCX_EHIP;
@@ -336,16 +318,9 @@ int launch_split_form(const void* qkv, void* out, int Bt, int N, int C, int head
         const char* e = getenv("TCX_ATTN_XCD");
         return (e && e[0] == '0') ? 0 : 1;
     }();
-    hipLaunchKernelGGL((k_attention_split<D, FMT, QW, KT>), dim3(N / (32 * QW), heads, Bt), dim3(64 * QW), shm, st,
-                       (const char*)qkv, (char*)out, N, C, scale, xcd);
+    hipLaunchKernelGGL((k_attention_split<D, FMT>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
+                       (char*)out, N, C, scale, xcd);
     return check_launch("tcx_attention_split");
-}
-
-template <int D, int FMT>
-int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
-    if (FMT == 2 && attn_q4_enabled() && N % 128 == 0)
-        return launch_split_form<D, FMT, 4, 64>(qkv, out, Bt, N, C, heads, st);
-    return launch_split_form<D, FMT, 8, 128>(qkv, out, Bt, N, C, heads, st);
 }
 
 #undef TCX_ATT_LOAD

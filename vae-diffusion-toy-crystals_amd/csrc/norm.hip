@@ -459,9 +459,7 @@ __global__ __launch_bounds__(256, 2) void k_upsample2x_band(const float* __restr
 // output rows, segment of SW source columns).  The segment's SW columns and one clamped halo column
 // either side (the bilinear taps of its 2 SW output columns) are staged; the arithmetic per output is
 // that of k_upsample2x_band / k_upsample2x_g8 (same clamped coordinates, same fmaf order).
-// SB2 (round 6, config 5's us1): the source is 2-byte bf16 (up2.net.3's pre-GroupNorm output stored as b2, as
-// every other pre-norm tensor of config 5): half the source bytes; staged in LDS as fp32 as before.
-template <int ROWS, bool SB2 = false>
+template <int ROWS>
 __global__ __launch_bounds__(256, 2) void k_upsample2x_bandseg(const float* __restrict__ x, char* __restrict__ y,
                                                               int H, int W, int C, int SW,
                                                               const float* __restrict__ tsc,
@@ -486,13 +484,7 @@ __global__ __launch_bounds__(256, 2) void k_upsample2x_bandseg(const float* __re
             const int col = e / C4, c4 = e - (e / C4) * C4;
             const int ysrc = min(max(ys0 + r, 0), H - 1);
             const int xsrc = min(max(xs0 + col, 0), W - 1);
-            const size_t el = (((size_t)b * H + ysrc) * W + xsrc) * C + 4 * c4;
-            if constexpr (SB2) {
-                const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(x) + el * 2);
-                v[k] = (f4v){bf_lo(u.x), bf_hi(u.x), bf_lo(u.y), bf_hi(u.y)};
-            } else {
-                v[k] = *reinterpret_cast<const f4v*>(x + el);
-            }
+            v[k] = *reinterpret_cast<const f4v*>(x + (((size_t)b * H + ysrc) * W + xsrc) * C + 4 * c4);
         }
     }
 #pragma unroll
@@ -1146,15 +1138,10 @@ int upsample_seg_width(int H, int W, int C) {
 bool upsample_fused_ok(int H, int W, int C) { return upsample_band_ok(H, W, C) || upsample_seg_width(H, W, C) > 0; }
 
 // h2 (f16x3) or bf16 (bf != 0) records out of the upsample / GroupNorm apply (unet.hip, and the C ABI below)
-// a 2-byte bf16 source is read by the segmented band form only (config 5's us1 at 128^2 x 96 source rows)
-bool upsample_b2src_ok(int H, int W, int C) { return !upsample_band_ok(H, W, C) && upsample_seg_width(H, W, C) > 0; }
-
 int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
-                  unsigned* ovf, int bf, hipStream_t st, int src_b2) {
+                  unsigned* ovf, int bf, hipStream_t st) {
     TCX_REQUIRE(x && y && C % 8 == 0 && aligned16(x) && aligned16(y), "tcx_upsample2x_h2: bad args");
     TCX_REQUIRE((scale == nullptr) == (shift == nullptr), "tcx_upsample2x_h2: scale/shift pair");
-    TCX_REQUIRE(!src_b2 || upsample_b2src_ok(H, W, C),
-                "tcx_upsample2x_h2: a 2-byte bf16 source needs the segmented band shape");
     if ((size_t)Bt * H * W * C == 0) return TCX_OK;
     if (upsample_band_ok(H, W, C)) {  // the banded LDS form (the 64^2 U-Net's us1 / us2)
         // 4 output rows per band: 48 KB of LDS, 3 workgroups per CU (r03_n: the 8-row bands and 4-channel
@@ -1178,15 +1165,15 @@ int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const fl
     if (const int sw = seg_on ? upsample_seg_width(H, W, C) : 0) {  // config 5's wide rows
         constexpr int rows = 4;
         const size_t shm = (size_t)(rows / 2 + 2) * (sw + 2) * C * sizeof(float);
-        const auto k = src_b2 ? &k_upsample2x_bandseg<4, true> : &k_upsample2x_bandseg<4, false>;
-        static bool attr[2] = {};
-        if (!attr[src_b2 ? 1 : 0]) {
+        const auto k = &k_upsample2x_bandseg<4>;
+        static bool attr = false;
+        if (!attr) {
             if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(4 * UB_MAXWC * sizeof(float))) != hipSuccess) {
                 set_error("tcx_upsample2x_h2: cannot enable %zu B of dynamic LDS", 4 * UB_MAXWC * sizeof(float));
                 return TCX_EHIP;
             }
-            attr[src_b2 ? 1 : 0] = true;
+            attr = true;
         }
         hipLaunchKernelGGL(k, dim3(Bt * (2 * H / rows) * (W / sw)), dim3(256), shm, st, x, (char*)y, H, W, C, sw, scale,
                            shift, ovf, bf);
@@ -1346,23 +1333,17 @@ int attn_prep_h2(float* a, void* y, int Bt, int HW, int C, const float* sc, cons
 
 extern "C" int tcx_upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
                                  const float* shift, unsigned* ovf, void* stream) {
-    return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, ovf, 0, (hipStream_t)stream, 0);
+    return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, ovf, 0, (hipStream_t)stream);
 }
 
 extern "C" int tcx_upsample2x_bf16(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
                                    const float* shift, void* stream) {
-    return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, nullptr, 1, (hipStream_t)stream, 0);
+    return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, nullptr, 1, (hipStream_t)stream);
 }
 
 extern "C" int tcx_gn_apply_tab_h2_cm(const float* x, void* y, int Bt, int HW, int C, const float* scale,
                                       const float* shift, unsigned* ovf, void* stream) {
     return gn_apply_cm(x, y, Bt, HW, C, scale, shift, ovf, (hipStream_t)stream);
-}
-
-extern "C" int tcx_upsample2x_b2_from_b2(const void* x, void* y, int Bt, int H, int W, int C, const float* scale,
-                                         const float* shift, void* stream) {
-    return upsample2x_h2(reinterpret_cast<const float*>(x), y, Bt, H, W, C, scale, shift, nullptr, 2,
-                         (hipStream_t)stream, 1);
 }
 
 extern "C" int tcx_gn_apply_tab_b2_cm(const void* x, void* y, int Bt, int HW, int C, const float* scale,
@@ -1391,7 +1372,7 @@ extern "C" int tcx_gn_apply_tab_b2(const void* x, void* y, int Bt, int HW, int C
 
 extern "C" int tcx_upsample2x_b2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale,
                                  const float* shift, void* stream) {
-    return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, nullptr, 2, (hipStream_t)stream, 0);
+    return upsample2x_h2(x, y, Bt, H, W, C, scale, shift, nullptr, 2, (hipStream_t)stream);
 }
 
 extern "C" int tcx_f32_to_h2(const float* x, void* y, size_t n, unsigned* ovf, void* stream) {

@@ -25,8 +25,7 @@ bool attn_prep_ok(int HW, int C, int groups, int bf);  // norm.hip: the attentio
 int attn_prep_h2(float* a, void* y, int Bt, int HW, int C, const float* sc, const float* sh, const float* gamma,
                  const float* beta, int groups, unsigned* ovf, int bf, hipStream_t st);
 int upsample2x_h2(const float* x, void* y, int Bt, int H, int W, int C, const float* scale, const float* shift,
-                  unsigned* ovf, int bf, hipStream_t st, int src_b2 = 0);
-bool upsample_b2src_ok(int H, int W, int C);  // norm.hip: a 2-byte source takes the segmented band form
+                  unsigned* ovf, int bf, hipStream_t st);
 int gn_apply_tab_h2(const float* x, void* y, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
                     unsigned* ovf, int bf, hipStream_t st);
 int gn_apply_b2_inplace(void* x, int Bt, int HW, int C, const float* scale, const float* shift, int silu,
@@ -1382,24 +1381,16 @@ int unet_body(const tcx_unet* net, const Plan& P, const float* x, int B, const f
     TCX_TRY(conv_gn(net->up2_0, P.a32, P.h2, C2, C2, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.b32, gn, &ns, st,
                     nullptr, nullptr, SC(3), SH(3), cm2 ? h2cc : h2, pre_b2));
     TCX_TRY(norm(7, P.b32, P.P1, C));
-    // config 5 (round 6): up2.net.3's pre-GroupNorm output as b2 too when the fused upsample reads it (its
-    // segmented band form takes a 2-byte source): half the bytes of the conv's stores and the upsample's loads
-    static const bool up21_on = [] {  // TCX_UP21_B2=0: fp32 as before (A/B)
-        const char* e = getenv("TCX_UP21_B2");
-        return !(e && e[0] == '0');
-    }();
-    const int up21_b2 = (up21_on && fmt == 2 && upsample_b2src_ok(H1, W1, C) && !pro[8]) ? 1 : 0;
     TCX_TRY(conv_gn(net->up2_1, P.b32, nullptr, C, 0, Bt, 0, H1, W1, 1, 1, nullptr, nullptr, P.a32, gn, &ns, st,
-                    SC(7), SH(7), nullptr, nullptr, h2, up21_b2));
+                    SC(7), SH(7), nullptr, nullptr, h2));
     // us1: GN+SiLU of up2's output, bilinear x2 into the free b64, conv.  Split path: the banded
     // upsample applies the GroupNorm+SiLU once per source element while staging (no apply pass);
     // fp32 path: the apply pass in place, then the plain upsample
     // (r03_o, one lane, alternating: 72.7 vs 72.3 images/s against the separate apply pass)
     if (h2.on && upsample_fused_ok(H1, W1, C)) {
         TCX_TRY(gn_tab(net, P, 8, P.P1, C, gn, ns, st));
-        TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, P.sc(8), P.sh(8), h2.ovf, fmt, st, up21_b2));
+        TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, P.sc(8), P.sh(8), h2.ovf, fmt, st));
     } else {
-        TCX_REQUIRE(!up21_b2, "tcx_unet: a 2-byte up2 output needs the fused upsample");
         TCX_TRY(norm(8, P.a32, P.P1, C, false));
         if (h2.on) TCX_TRY(upsample2x_h2(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, h2.ovf, fmt, st));
         else TCX_TRY(tcx_upsample2x(P.a32, P.b64, Bt, H1, W1, C, nullptr, nullptr, st));

@@ -103,7 +103,6 @@ _SIGS = {
     "tcx_attention_split_b2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_gn_apply_tab_b2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp, c_fp, c_int, c_int, c_fp]),
     "tcx_upsample2x_b2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
-    "tcx_upsample2x_b2_from_b2": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp]),
     "tcx_conv_weight_h2_frag_bytes": (c_size, [c_int, c_int]),
     "tcx_pack_conv_weight_h2_frag": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_fp]),
     "tcx_conv_weight_h2_frag4_bytes": (c_size, [c_int, c_int]),
