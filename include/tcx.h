@@ -527,6 +527,13 @@ int tcx_pack_conv_dgrad_weight(const float* w, float* wpk, int Cout, int Cin, in
 int tcx_conv_transpose2x(const float* x, int Bt, int H, int W, int Cin, const float* wpk4, const float* bias,
                          float* y, int Cout, int cout_pad, int kpad, int act, int circular, void* stream);
 
+/* The same on the f16x3 split path (round 6): xh = h2 records of x (tcx_f32_to_h2_scaled, scale s_x),
+ * wh4 = h2 records of tcx_pack_convT_weight's [4][cout_pad][kpad] (scale s_w), *wscale = 1 / (s_w s_x);
+ * Cin % 32 == 0, kpad == 4 Cin.  fp32 output.  The training step's ds1 / ds2 data gradients. */
+int tcx_conv_transpose2x_h2(const void* xh, int Bt, int H, int W, int Cin, const void* wh4, const float* wscale,
+                            const float* bias, float* y, int Cout, int cout_pad, int kpad, int act, int circular,
+                            void* stream);
+
 /* GroupNorm forward statistics from fp64 partials: scale/shift tables [Bt][C] and per-(batch,
  * group) mean / rstd [Bt][groups] saved for the backward (nn.GroupNorm, sde_score_model.py:103). */
 int tcx_gn_stats(const double* part, int Bt, int HW, int C, int groups, int nsplit, const float* gamma,

@@ -18,6 +18,7 @@
 // the A load, bias / per-batch bias / residual / activation epilogue, and GroupNorm partial
 // statistics of the output (fp64) for the following GroupNorm.
 #include "conv_common.hpp"
+#include "thin.hpp"
 
 namespace tcx {
 bool conv3m_takes(const ConvParams& p);  // conv3m.hip
@@ -774,6 +775,11 @@ extern "C" int tcx_conv2d(const float* x1, const float* x2, int Bt, int bmod, in
                     "no bmod/upsample, Ho*Wo %% 128 == 0, C <= 384, extents < 2 GiB");
     }
     TCX_REQUIRE(aligned16(wpk), "tcx_conv2d: packed weight must be 16-B aligned");
+    if (!upsample && !gn_stats && !pro_scale1 && !pro_scale2 && bmod == 0 && C2 == 0 && stride == 1) {
+        // one-channel side (the score net's first / out convs and the out conv's data gradient): thin.hip
+        ThinConv a{x1, wpk, bias, bias_b, resid, y, Bt, H, W, C1, Cout, kpad, ks, pad, circular, p.Ho, p.Wo, act};
+        if (thin_conv_takes(a)) return launch_thin_conv(a, (hipStream_t)stream);
+    }
     return launch_conv(p, cout_pad, mode, (hipStream_t)stream);
 }
 
@@ -807,6 +813,40 @@ extern "C" int tcx_conv_transpose2x(const float* x, int Bt, int H, int W, int Ci
             p.bytesw = bw < lim && aligned16(p.w) ? (unsigned)bw : 0u;
         }
         TCX_TRY(launch_conv(p, cout_pad, vec_ok ? 0 : 1, (hipStream_t)stream));
+    }
+    return TCX_OK;
+}
+
+// The same four sub-pixel 2x2 convs on the f16x3 split path (round 6): the training step's data gradient
+// of the 4x4/s2 downsamples (the adjoint of sde_score_model.py:215-216's ds1 / ds2) on h2 records of dY
+// and of the phase weights (tcx_f32_to_h2_scaled of tcx_pack_convT_weight's [4][cout_pad][kpad]), the
+// combined scale *wscale = 1 / (s_w s_dy) applied in k_conv's epilogue (MODE 3 staging, SPL 1)
+extern "C" int tcx_conv_transpose2x_h2(const void* xh, int Bt, int H, int W, int Cin, const void* wh4,
+                                       const float* wscale, const float* bias, float* y, int Cout, int cout_pad,
+                                       int kpad, int act, int circular, void* stream) {
+    TCX_REQUIRE(xh && wh4 && wscale && y, "tcx_convT2x_h2: null pointer");
+    TCX_REQUIRE(Bt >= 0 && H > 0 && W > 0 && Cin % BK == 0 && Cout > 0 && cout_pad >= Cout && cout_pad % 32 == 0 &&
+                    kpad == 4 * Cin && act >= 0 && act <= 3,
+                "tcx_convT2x_h2: needs Cin %% 32 == 0, kpad == 4 Cin, cout_pad %% 32 == 0");
+    TCX_REQUIRE(aligned16(xh) && aligned16(wh4) && aligned16(y), "tcx_convT2x_h2: pointers must be 16-B aligned");
+    const size_t lim = (size_t)1 << 31;
+    const size_t b1 = (size_t)Bt * H * W * Cin * 4, bw = (size_t)cout_pad * kpad * 4;
+    TCX_REQUIRE(b1 < lim && 4 * bw < lim, "tcx_convT2x_h2: operands must be < 2 GiB (32-bit buffer offsets)");
+    for (int ph = 0; ph < 4; ++ph) {
+        const int ry = ph >> 1, rx = ph & 1;
+        ConvParams p{};
+        p.x1 = (const float*)xh; p.x2 = nullptr; p.C1 = Cin; p.C2 = 0; p.Cin = Cin;
+        p.bmod = 0; p.H = H; p.W = W; p.Hi = H; p.Wi = W;
+        p.Ho = H; p.Wo = W; p.HoWo = H * W; p.M = Bt * H * W;
+        p.w = (const float*)((const char*)wh4 + (size_t)ph * bw);
+        p.bias = bias; p.bias_b = nullptr; p.resid = nullptr; p.y = y;
+        p.Cout = Cout; p.kpad = kpad; p.nchunks = kpad / BK;
+        p.ks = 2; p.stride = 1; p.pad_y = 1 - ry; p.pad_x = 1 - rx; p.circular = circular;
+        p.Hy = 2 * H; p.Wy = 2 * W; p.osy = 2; p.ooy = ry; p.osx = 2; p.oox = rx;
+        p.act = act; p.gn = nullptr; p.nsplit = 1;
+        p.bytes1 = (unsigned)b1; p.bytesw = (unsigned)bw;
+        p.wscale = wscale; p.out_h2 = 0; p.bf = 0;
+        TCX_TRY(launch_conv(p, cout_pad, 0, (hipStream_t)stream));
     }
     return TCX_OK;
 }

@@ -16,6 +16,7 @@
 #include "common.hpp"
 #include "skinny.hpp"
 #include "h2.hpp"
+#include "thin.hpp"
 
 namespace tcx {
 namespace {
@@ -986,6 +987,24 @@ extern "C" int tcx_conv_wgrad(const float* x1, const float* x2, int Bt, int H, i
     TCX_REQUIRE(need + (base - (char*)ws) <= ws_bytes, "tcx_conv_wgrad: workspace too small (%zu < %zu)", ws_bytes,
                 need + 256);
     p.part = reinterpret_cast<float*>(base);
+    if (C2 == 0 && pad == 1 && aligned16(x1) && aligned16(dy) && aligned16(p.part)) {
+        // one-channel side (the score net's first / out convs): VALU reduction planes, thin.hip
+        ThinWgrad a{};
+        const size_t plane = (size_t)p.K * Cout * sizeof(float);
+        const size_t room = (ws_bytes - (size_t)(base - (char*)ws)) / plane;
+        const int ns = thin_wgrad_plan(Bt, H, W, C1, Cout, ks, stride, (int)std::min<size_t>(room, 256), &a);
+        if (ns > 0 && p.Ho == H && p.Wo == W) {
+            const bool cout1 = Cout == 1;
+            a.wide = cout1 ? x1 : dy;
+            a.thin = cout1 ? dy : x1;
+            a.pad = pad; a.circular = circular; a.sign = cout1 ? -1 : 1; a.part = p.part;
+            TCX_TRY(launch_thin_wgrad(a, ns, (hipStream_t)stream));
+            const size_t n = (size_t)p.K * Cout;
+            hipLaunchKernelGGL(k_wgrad_reduce, dim3((int)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                               (hipStream_t)stream, p.part, ns, p.K, Cout, p.Cin, ks, beta, dw);
+            return check_launch("tcx_conv_wgrad reduce");
+        }
+    }
     const bool asc = (C1 % 4 != 0) || (C2 % 4 != 0) || !aligned16(x1) || (x2 && !aligned16(x2));
     const bool bsc = (Cout % 4 != 0) || !aligned16(dy);
     hipStream_t st = (hipStream_t)stream;

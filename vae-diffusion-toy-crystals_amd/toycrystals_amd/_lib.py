@@ -162,6 +162,8 @@ _SIGS = {
     "tcx_pack_conv_dgrad_weight": (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_fp]),
     "tcx_conv_transpose2x": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int,
                                      c_int, c_fp]),
+    "tcx_conv_transpose2x_h2": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_fp, c_fp, c_int, c_int, c_int,
+                                        c_int, c_int, c_fp]),
     "tcx_gn_stats": (c_int, [c_fp, c_int, c_int, c_int, c_int, c_int, c_fp, c_fp, c_float, c_fp, c_fp, c_fp, c_fp,
                              c_fp]),
     "tcx_gn_bwd_workspace": (c_size, [c_int, c_int, c_int]),

@@ -121,16 +121,25 @@ def _split_ok(x1, x2, C1, C2, ks, kpad, macs) -> bool:
 
 
 _SLOT_INIT = {}
+_SLOT_POOL = {}  # device -> [chunk of fresh slots, next free index]
+_SLOT_CHUNK = 256
 
 
 def _scale_slot(device) -> torch.Tensor:
-    """A fresh [bits = 0][1.0][1/s] slot (int32 x 12, fields 16 B apart): one copy launch."""
-    t = _SLOT_INIT.get(device)
-    if t is None:
-        h = torch.zeros(12, dtype=torch.int32)
-        h[4:5].view(torch.float32).fill_(1.0)
-        t = _SLOT_INIT[device] = h.to(device)
-    return t.clone()
+    """A fresh [bits = 0][1.0][1/s] slot (int32 x 12, fields 16 B apart).  Slots are handed out of
+    chunks of 256 initialised by one launch (a copy per slot cost 58 launches per score step); each
+    slot is used once, and a chunk lives while any slot view of it does."""
+    e = _SLOT_POOL.get(device)
+    if e is None or e[1] >= _SLOT_CHUNK:
+        t = _SLOT_INIT.get(device)
+        if t is None:
+            h = torch.zeros(12, dtype=torch.int32)
+            h[4:5].view(torch.float32).fill_(1.0)
+            t = _SLOT_INIT[device] = h.to(device)
+        e = _SLOT_POOL[device] = [t.repeat(_SLOT_CHUNK), 0]
+    i = e[1]
+    e[1] = i + 1
+    return e[0][12 * i:12 * i + 12]
 
 
 def _absmax_slot_for(x: torch.Tensor, C: int) -> torch.Tensor | None:
@@ -157,24 +166,30 @@ def _tagged_slot(t: torch.Tensor):
     return None
 
 
-def _h2_scaled(ts):
+def _h2_scaled(ts, mul=None):
     """fp32 tensors sharing ONE power-of-two scale s (max |s v| in [2^13, 2^14)) -> their h2 records
     and a 1-element float tensor holding 1/s (tcx_absmax + tcx_f32_to_h2_scaled).  A single tensor
-    whose producer already reported its max |value| (_tag_absmax) skips the absmax pass."""
+    whose producer already reported its max |value| (_tag_absmax) skips the absmax pass.
+    mul: a 1-element float tensor m; the returned scalar is then m / s, written by the conversion
+    itself (the conv epilogue's combined scale without a separate multiply launch)."""
     L = lib()
     st = _st(ts[0])
     sl = _tagged_slot(ts[0]) if len(ts) == 1 else None
     pre = sl is not None
     if not pre:
         sl = _scale_slot(ts[0].device)  # [bits][1.0][1/s], 16 B apart
+    elif mul is not None:
+        # the producer's slot may still be read as 1/s by records made earlier: keep it, multiply apart
+        hs, inv_t = _h2_scaled(ts)
+        return hs, inv_t * mul
     bits, one, inv = ptr(sl), ptr(sl) + 16, ptr(sl) + 32
     for t in ts if not pre else ():
         check(L.tcx_absmax(ptr(t), t.numel(), bits, st), "tcx_absmax")
     hs = []
     for i, t in enumerate(ts):
         h = torch.empty_like(t)
-        check(L.tcx_f32_to_h2_scaled(ptr(t), ptr(h), t.numel(), bits, one if i == 0 else None,
-                                     inv if i == 0 else None, st), "to h2")
+        num = (ptr(mul) if mul is not None else one) if i == 0 else None
+        check(L.tcx_f32_to_h2_scaled(ptr(t), ptr(h), t.numel(), bits, num, inv if i == 0 else None, st), "to h2")
         hs.append(h)
     return hs, sl[8:9].view(torch.float32)
 
@@ -190,8 +205,9 @@ def _conv_fwd_split(x1, x2, wpk, kpad, cpad, b, bias_b, resid, Cout, ks, stride,
         hs, xinv = _h2_scaled([x1] if x2 is None else [x1, x2])
         xh = (hs[0], hs[1] if x2 is not None else None, xinv)
     x1h, x2h, xinv = xh
-    (wh,), winv = _h2_scaled([wpk])  # h2 of the packed weight (the layout of tcx_pack_conv_weight_h2)
-    comb = winv * xinv  # 1 / (s_w s_x), applied by the conv epilogue
+    # h2 of the packed weight (the layout of tcx_pack_conv_weight_h2) and comb = 1 / (s_w s_x), the
+    # scale the conv epilogue applies, written by the weight's conversion launch
+    (wh,), comb = _h2_scaled([wpk], mul=xinv)
     # fragment-ordered copy of the weight (round 3): the 3x3 convs then run on the LDS-DMA kernels of
     # the sampler (k_conv3lg / k_conv3g) and the 4x4/s2 ones on k_conv4s2g instead of the register-
     # staged k_conv3p / k_conv4s2h (the library picks; a shape they do not cover ignores the copy)
@@ -252,8 +268,22 @@ def _conv_dgrad(dy, w, C_lo, n_ci, stride, pad, circular, H, W, keep=None):
         check(L.tcx_pack_convT_weight(ptr(w), ptr(wpk), Cout, Cin, cpad, kpad, st), "pack convT")
         Hy, Wy = dy.shape[1], dy.shape[2]
         dx = _empty((B, 2 * Hy, 2 * Wy, Cin), dy)
-        check(L.tcx_conv_transpose2x(ptr(dy), B, Hy, Wy, Cout, ptr(wpk), None, ptr(dx), Cin, cpad, kpad, 0, circular,
-                                     st), "tcx_conv_transpose2x")
+        if _split_ok(dy, None, Cout, 0, 2, kpad, float(B) * 4 * Hy * Wy * Cin * 4 * Cout):
+            # f16x3 (round 6): dY's records (made here or by an earlier data gradient, and reused by the
+            # weight gradient) and the phase weights' records, comb = 1 / (s_w s_dy) from the conversion
+            if keep:
+                xh = keep[0]
+            else:
+                hs, inv = _h2_scaled([dy])
+                xh = (hs[0], None, inv)
+                if keep is not None:
+                    keep.append(xh)
+            (wh,), comb = _h2_scaled([wpk], mul=xh[2])
+            check(L.tcx_conv_transpose2x_h2(ptr(xh[0]), B, Hy, Wy, Cout, ptr(wh), ptr(comb), None, ptr(dx), Cin, cpad,
+                                            kpad, 0, circular, st), "tcx_conv_transpose2x_h2")
+        else:
+            check(L.tcx_conv_transpose2x(ptr(dy), B, Hy, Wy, Cout, ptr(wpk), None, ptr(dx), Cin, cpad, kpad, 0,
+                                         circular, st), "tcx_conv_transpose2x")
         assert dx.shape[1] == H and dx.shape[2] == W
         return dx
     raise NotImplementedError(f"conv data gradient for stride={stride}, k={ks}, pad={pad}")
@@ -271,10 +301,10 @@ def _conv_wgrad(x1, x2, dy, Cout, ks, stride, pad, circular, xrec=None, dyrec=No
     ws = _ws(dy.device, nb)
     if _WGRAD_SPLIT and xrec is not None and Cout % 8 == 0 and dy.numel() * 4 < (1 << 31):
         if dyrec is None:
-            (dyh,), dyinv = _h2_scaled([dy])
+            (dyh,), comb = _h2_scaled([dy], mul=xrec[2])
         else:
             dyh, _, dyinv = dyrec
-        comb = xrec[2] * dyinv
+            comb = xrec[2] * dyinv
         check(L.tcx_conv_wgrad_h2(ptr(xrec[0]), ptr(xrec[1]), B, H, W, C1, C2, ptr(dyh), Cout, ks, stride, pad,
                                   circular, 0.0, ptr(comb), ptr(dw), ptr(ws), ws.numel(), _st(dy)),
               "tcx_conv_wgrad_h2")
