@@ -376,6 +376,11 @@ int tcx_debug_fail_eval(int k);
  * fp32 rounding of their per-lane sums). */
 int tcx_debug_conv3mb(int mode);
 
+/* Test hook (round 6): the calling thread's choice for the halo-staged 3x3 weight gradient of
+ * tcx_conv_wgrad_h2 (wgrad3h.hip: all nine taps of a 32-channel group per workgroup): -1 default
+ * (on; TCX_WGRAD3H=0 turns it off), 0 = k_wgrad_h2, 1 = the halo kernel.  Returns the previous mode. */
+int tcx_debug_wgrad3h(int mode);
+
 /* (Workspace: tcx_sde_workspace_size(net, B, H, W, n_steps, guidance) bytes — see the breaking-change
  * note above; tcx_ode_sample_ex likewise needs tcx_ode_workspace_size.)
  * tcx_sde_sample_ex on one shard of a larger sampling batch (batch-DP sampling):

@@ -37,6 +37,15 @@ def im2col(x, ks, stride, pad, circular):
     return cols.reshape(B * Ho * Wo, ks * ks * C), Ho, Wo
 
 
+@pytest.fixture(params=[1, 0], ids=["halo", "im2col"])
+def wgrad_mode(request):
+    """1: the halo-staged 3x3 kernel (wgrad3h.hip, round 6) where it applies (3x3 stride 1, W in {16, 32, 64},
+    C1 % 32 == 0, Cout % 96 == 0), 0: k_wgrad_h2 everywhere (tcx_debug_wgrad3h)."""
+    prev = L().tcx_debug_wgrad3h(request.param)
+    yield request.param
+    L().tcx_debug_wgrad3h(prev)
+
+
 @pytest.mark.parametrize("B,H,W,C1,C2,Cout,ks,stride,circ", [
     (2, 16, 16, 32, 0, 96, 3, 1, 1),     # NT = 3, one k block
     (2, 16, 16, 96, 96, 96, 3, 1, 1),    # two sources (the skip concats), 14 k blocks
@@ -45,8 +54,12 @@ def im2col(x, ks, stride, pad, circular):
     (2, 8, 8, 64, 0, 192, 3, 1, 0),      # zero padding (VAE), two co blocks
     (1, 9, 7, 40, 0, 48, 3, 1, 1),       # K = 360 (ragged k block), Cout 48 in a 64-wide block
     (4, 64, 64, 96, 0, 96, 3, 1, 1),     # the score model's 64^2 layer shape
+    (2, 32, 32, 64, 0, 192, 3, 1, 0),    # halo kernel: zero padding at 32^2, two co blocks
+    (2, 32, 32, 192, 192, 96, 3, 1, 1),  # halo kernel: up2.net.0's concat at 32^2 (12 channel groups)
+    (3, 64, 64, 96, 96, 96, 3, 1, 0),    # halo kernel: up1.net.0's concat at 64^2, zero padding
+    (2, 16, 16, 192, 0, 192, 3, 1, 1),   # halo kernel: the mid convs at 16^2 (4-row chunks)
 ])
-def test_wgrad_h2_vs_float64(B, H, W, C1, C2, Cout, ks, stride, circ):
+def test_wgrad_h2_vs_float64(B, H, W, C1, C2, Cout, ks, stride, circ, wgrad_mode):
     pad = 1
     x1 = rng.standard_normal((B, H, W, C1)).astype(np.float32)
     x2 = rng.standard_normal((B, H, W, C2)).astype(np.float32) if C2 else None
@@ -71,6 +84,28 @@ def test_wgrad_h2_vs_float64(B, H, W, C1, C2, Cout, ks, stride, circ):
     mag = (np.abs(cols).T @ np.abs(dyd)).reshape(ks, ks, C1 + C2, Cout).transpose(3, 2, 0, 1)
     err = np.abs(got - ref)
     bound = mag * 2.0 ** -19 + 1e-6 * float(mag.max())
-    print(f"wgrad_h2 B={B} {H}x{W} C={C1}+{C2} Cout={Cout} k={ks} s={stride} circ={circ}: "
+    print(f"wgrad_h2[{wgrad_mode}] B={B} {H}x{W} C={C1}+{C2} Cout={Cout} k={ks} s={stride} circ={circ}: "
           f"max err {float(err.max()):.3e}, max err/bound {float((err / bound).max()):.3f}")
     assert np.all(err <= bound), float((err / bound).max())
+
+
+def test_wgrad3h_deterministic_and_close_to_im2col():
+    """The halo kernel is deterministic (fixed chunk order per split, fixed plane order in the reduce) and agrees
+    with k_wgrad_h2 to the fp32 accumulation-order difference (both sum the same f16x3 products)."""
+    B, H, W, C, Cout = 4, 64, 64, 96, 96
+    x1h = to_h2(dev(rng.standard_normal((B, H, W, C)).astype(np.float32)))
+    dyh = to_h2(dev((rng.standard_normal((B, H, W, Cout)) * 0.1).astype(np.float32)))
+    comb = torch.ones(1, device="cuda")
+    nb = int(L().tcx_conv_wgrad_workspace(B, H, W, C, Cout, 3))
+    ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    outs = []
+    for mode in (1, 1, 0):
+        prev = L().tcx_debug_wgrad3h(mode)
+        dw = torch.empty((Cout, C, 3, 3), device="cuda")
+        chk(L().tcx_conv_wgrad_h2(x1h.data_ptr(), None, B, H, W, C, 0, dyh.data_ptr(), Cout, 3, 1, 1, 1, 0.0,
+                                  comb.data_ptr(), dw.data_ptr(), ws.data_ptr(), nb, st()))
+        L().tcx_debug_wgrad3h(prev)
+        outs.append(dw.cpu())
+    assert torch.equal(outs[0], outs[1])
+    scale = float(outs[2].abs().max())
+    assert float((outs[0] - outs[2]).abs().max()) <= 1e-5 * scale

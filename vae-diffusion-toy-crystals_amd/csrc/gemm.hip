@@ -19,6 +19,25 @@
 #include "thin.hpp"
 
 namespace tcx {
+struct Wg3hArgs {
+    const char* x1;
+    const char* x2;
+    const char* dy;
+    unsigned bx1, bx2, bdy;
+    int B, H, W, C1, C2, Cin, Cout, circular;
+    int RB;
+    int nchunk, cps;
+    int ncob;
+    const float* comb;
+    float* part;
+};
+// wgrad3h.hip: the halo-staged 3x3 weight gradient
+bool wgrad3h_takes(int B, int H, int W, int C1, int C2, int Cout, int ks, int stride, int pad, size_t in1, size_t in2,
+                   size_t ind);
+int launch_wgrad3h(Wg3hArgs& a, int max_split, int* nsplit, hipStream_t st);
+}  // namespace tcx
+
+namespace tcx {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -1052,6 +1071,24 @@ extern "C" int tcx_conv_wgrad_h2(const void* x1, const void* x2, int Bt, int H, 
                 ws_bytes, need + 256);
     p.part = reinterpret_cast<float*>(base);
     hipStream_t st = (hipStream_t)stream;
+    {
+        // 3x3 stride-1 convs: the halo-staged kernel (wgrad3h.hip), all nine taps per workgroup
+        const size_t in1 = (size_t)Bt * H * W * C1 * 4, in2 = (size_t)Bt * H * W * C2 * 4, ind = (size_t)p.M * Cout * 4;
+        if (wgrad3h_takes(Bt, H, W, C1, C2, Cout, ks, stride, pad, in1, in2, ind)) {
+            Wg3hArgs a{};
+            a.x1 = (const char*)x1; a.x2 = (const char*)x2; a.dy = (const char*)dy;
+            a.bx1 = (unsigned)in1; a.bx2 = (unsigned)in2; a.bdy = (unsigned)ind;
+            a.B = Bt; a.H = H; a.W = W; a.C1 = C1; a.C2 = C2; a.Cin = C1 + C2; a.Cout = Cout; a.circular = circular;
+            a.comb = comb; a.part = p.part;
+            const size_t room = (ws_bytes - (size_t)(base - (char*)ws)) / ((size_t)p.K * Cout * sizeof(float));
+            int ns = 0;
+            TCX_TRY(launch_wgrad3h(a, (int)std::min<size_t>(room, 256), &ns, st));
+            const size_t n = (size_t)p.K * Cout;
+            hipLaunchKernelGGL(k_wgrad_reduce, dim3((int)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
+                               p.part, ns, p.K, Cout, p.Cin, ks, beta, dw);
+            return check_launch("tcx_conv_wgrad_h2 reduce");
+        }
+    }
     const dim3 grid(p.nkblk * p.ncblk, p.nsplit);
     // operands past 2 GiB (32-bit buffer offsets) take the round-2 quad-staged k_wgrad_h2_r2 (the knob that
     // selected it for A/B was removed in round 4: 419 vs 613 us, r03)

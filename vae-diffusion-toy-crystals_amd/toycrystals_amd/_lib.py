@@ -120,6 +120,7 @@ _SIGS = {
     "tcx_unet_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int]),
     "tcx_set_sample_lanes": (c_int, [c_int]),
     "tcx_debug_conv3mb": (c_int, [c_int]),
+    "tcx_debug_wgrad3h": (c_int, [c_int]),
     "tcx_sde_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int, c_int, c_float]),
     "tcx_ode_workspace_size": (c_size, [ctypes.POINTER(TcxUnet), c_int, c_int, c_int, c_int, c_float]),
     "tcx_debug_fail_eval": (c_int, [c_int]),
