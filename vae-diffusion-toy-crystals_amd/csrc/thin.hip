@@ -28,38 +28,34 @@ __device__ __forceinline__ float thin_act(float v, int act) {
     return v;
 }
 
-// source pixel of output (oy, ox) at tap (dy, dx), or -1 (zero padding outside the image)
-__device__ __forceinline__ int thin_src(int oy, int ox, int dy, int dx, int pad, int H, int W, int circ) {
-    int iy = oy + dy - pad, ix = ox + dx - pad;
-    if (circ) {
-        iy = wrap_idx(iy, H);
-        ix = wrap_idx(ix, W);
-    } else if (iy < 0 || iy >= H || ix < 0 || ix >= W) {
-        return -1;
-    }
-    return iy * W + ix;
-}
-
 // one workgroup per output row, one thread per (output pixel, 4 output channels) in turn; the weights
-// transposed into LDS as [tap][Cout] once per row (staging them per 256 outputs cost more than the row's
-// arithmetic); 32-bit index math
+// transposed into LDS as [tap][Cout] and the row's ks input rows (with their wrapped / zero halo columns)
+// staged in LDS once per row, so the inner loop reads only LDS; 32-bit index math
 __global__ __launch_bounds__(256) void k_thin_cin1(ThinConv a) {
     extern __shared__ __attribute__((aligned(16))) float wT[];
-    const int T = a.ks * a.ks, Q = a.Cout / 4;
+    const int T = a.ks * a.ks, Q = a.Cout / 4, XW = a.Wo + a.ks - 1;  // staged row width
+    float* xs = wT + T * a.Cout;                                      // [ks][XW]
+    const int row = blockIdx.x, b = row / a.Ho, oy = row - b * a.Ho;
+    const float* xb = a.x + (size_t)b * a.H * a.W;
     for (int i = threadIdx.x; i < T * a.Cout; i += 256) {
         const int tap = i / a.Cout, co = i - tap * a.Cout;
         wT[i] = a.w[(size_t)co * a.kpad + tap];
     }
+    for (int i = threadIdx.x; i < a.ks * XW; i += 256) {
+        const int dy = i / XW, c = i - dy * XW;  // staged column c = input column c - pad
+        int iy = oy + dy - a.pad, ix = c - a.pad;
+        float v = 0.f;
+        if (a.circular) v = xb[wrap_idx(iy, a.H) * a.W + wrap_idx(ix, a.W)];
+        else if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) v = xb[iy * a.W + ix];
+        xs[i] = v;
+    }
     __syncthreads();
-    const int row = blockIdx.x, b = row / a.Ho, oy = row - b * a.Ho;
-    const float* xb = a.x + (size_t)b * a.H * a.W;
     for (int it = threadIdx.x; it < a.Wo * Q; it += 256) {
         const int ox = it / Q, cq = it - ox * Q;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int dy = 0; dy < a.ks; ++dy)
             for (int dx = 0; dx < a.ks; ++dx) {
-                const int s = thin_src(oy, ox, dy, dx, a.pad, a.H, a.W, a.circular);
-                const float v = s >= 0 ? xb[s] : 0.f;
+                const float v = xs[dy * XW + ox + dx];
                 const float4 w4 = *reinterpret_cast<const float4*>(wT + (dy * a.ks + dx) * a.Cout + 4 * cq);
                 acc.x = fmaf(v, w4.x, acc.x); acc.y = fmaf(v, w4.y, acc.y);
                 acc.z = fmaf(v, w4.z, acc.z); acc.w = fmaf(v, w4.w, acc.w);
@@ -146,7 +142,7 @@ size_t cout1_lds(const ThinConv& a) {
 bool thin_conv_takes(const ThinConv& a) {
     static const bool off = getenv("TCX_THIN") && getenv("TCX_THIN")[0] == '0';  // A/B: the MFMA kernels
     if (off || a.ks < 1 || a.ks > 7 || a.B <= 0 || (size_t)a.B * a.Ho >= (1u << 31)) return false;
-    if (a.Cin == 1 && a.Cout % 4 == 0 && a.ks * a.ks * a.Cout <= 8192 && aligned16(a.y) &&
+    if (a.Cin == 1 && a.Cout % 4 == 0 && a.ks * a.ks * a.Cout <= 8192 && a.Wo + a.ks - 1 <= 4096 && aligned16(a.y) &&
         (!a.resid || aligned16(a.resid)))
         return true;
     return a.Cout == 1 && a.Cin % 4 == 0 && cout1_lds(a) <= 48 * 1024 && aligned16(a.x) && aligned16(a.w);
@@ -155,7 +151,7 @@ bool thin_conv_takes(const ThinConv& a) {
 int launch_thin_conv(const ThinConv& a, hipStream_t st) {
     if (a.Cin == 1) {
         hipLaunchKernelGGL(k_thin_cin1, dim3(a.B * a.Ho), dim3(256),
-                           (size_t)a.ks * a.ks * a.Cout * sizeof(float), st, a);
+                           ((size_t)a.ks * a.ks * a.Cout + (size_t)a.ks * (a.Wo + a.ks - 1)) * sizeof(float), st, a);
     } else {
         hipLaunchKernelGGL(k_thin_cout1, dim3(a.B * a.Ho), dim3(256), cout1_lds(a), st, a);
     }

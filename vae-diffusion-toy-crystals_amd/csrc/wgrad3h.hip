@@ -44,18 +44,19 @@ struct Wg3hArgs {
 namespace {
 
 constexpr int W3_WAIT_VM0 = 0x0F70;    // s_waitcnt vmcnt(0)
-constexpr int W3_DYB = 64 * 384;       // dY image: 64 pixels x 96 channels
 
-__host__ __device__ constexpr int w3_halo_px(int W) { return (64 / W + 2) * (W + 2); }
-__host__ __device__ constexpr int w3_halo_bytes(int W) { return (w3_halo_px(W) * 128 + 1023) / 1024 * 1024; }
-// DMA instructions (1 KB each) per chunk, padded to a multiple of 4 so every wave issues the same count
-// (its vmcnt then names one chunk exactly); the padding instructions load zeros into the stage's tail
-__host__ __device__ constexpr int w3_ninst(int W) { return (w3_halo_bytes(W) / 1024 + W3_DYB / 1024 + 3) / 4 * 4; }
-__host__ __device__ constexpr int w3_stage(int W) { return w3_ninst(W) * 1024; }
-constexpr int W3_NSTAGE = 3;  // ring depth: chunk c + 2 streams in while chunk c is multiplied
-constexpr size_t wgrad3h_lds_bytes(int W) { return W3_NSTAGE * (size_t)w3_stage(W); }
-static_assert(wgrad3h_lds_bytes(64) <= 160 * 1024 && wgrad3h_lds_bytes(32) <= 160 * 1024 &&
-                  wgrad3h_lds_bytes(16) <= 160 * 1024, "wgrad3h ring exceeds the CU's LDS");
+// chunk geometry: CP pixels per chunk (32 or 64) as RB rows x SW columns of one image (SW = min(W, CP))
+__host__ __device__ constexpr int w3_sw(int W, int CP) { return W < CP ? W : CP; }
+__host__ __device__ constexpr int w3_rb(int W, int CP) { return CP / w3_sw(W, CP); }
+__host__ __device__ constexpr int w3_halo_px(int W, int CP) { return (w3_rb(W, CP) + 2) * (w3_sw(W, CP) + 2); }
+__host__ __device__ constexpr int w3_nh(int W, int CP) { return (w3_halo_px(W, CP) * 128 + 1023) / 1024; }
+__host__ __device__ constexpr int w3_nt(int W, int CP) { return w3_nh(W, CP) + CP * 384 / 1024; }  // 1-KB DMAs
+__host__ __device__ constexpr int w3_stage(int W, int CP) { return w3_nt(W, CP) * 1024; }
+constexpr int W3_NSTAGE = 3;  // ring depth: chunks c + 1 and c + 2 stream in while chunk c is multiplied
+constexpr size_t wgrad3h_lds_bytes(int W, int CP) { return W3_NSTAGE * (size_t)w3_stage(W, CP); }
+static_assert(wgrad3h_lds_bytes(64, 64) <= 160 * 1024 && wgrad3h_lds_bytes(64, 32) <= 80 * 1024 &&
+                  wgrad3h_lds_bytes(32, 32) <= 80 * 1024 && wgrad3h_lds_bytes(16, 32) <= 80 * 1024,
+              "wgrad3h ring exceeds the CU's LDS");
 
 __device__ __forceinline__ int w3_swz(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 2); }
 
@@ -67,19 +68,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef short v8s __attribute__((ext_vector_type(8)));
 
-template <int W>
-__global__ __launch_bounds__(256, 1) void k_wgrad3h(Wg3hArgs a) {
-    constexpr int RB = 64 / W, W2 = W + 2;
-    constexpr int HPX = w3_halo_px(W);
-    constexpr int HB = w3_halo_bytes(W);
-    constexpr int STG = w3_stage(W);
-    constexpr int NH = HB / 1024;      // halo DMA instructions per chunk (1 KB each)
-    constexpr int ND = W3_DYB / 1024;  // dY DMA instructions per chunk (24)
-    constexpr int NT = NH + ND;
-    constexpr int NTP = w3_ninst(W);   // with the zero-load padding
-    constexpr int PER = NTP / 4;       // DMA instructions per wave and chunk
-    static_assert(PER <= 15, "vmcnt immediate");
-    constexpr int WAIT_ONE = 0x0F70 | PER;  // s_waitcnt vmcnt(PER): all but the newest chunk landed
+// CP = 64: one workgroup per CU (the ring is 3 x 49-52 KB); CP = 32: two per CU (3 x 21-25 KB each), whose
+// waves' DMA / VALU then run beside the other workgroup's MFMAs
+template <int W, int CP>
+__global__ __launch_bounds__(256, CP == 32 ? 2 : 1) void k_wgrad3h(Wg3hArgs a) {
+    constexpr int SW = w3_sw(W, CP), RB = w3_rb(W, CP), NSEG = W / SW, W2 = SW + 2;
+    constexpr int HPX = w3_halo_px(W, CP);
+    constexpr int NH = w3_nh(W, CP);   // halo DMA instructions per chunk (1 KB each)
+    constexpr int HB = NH * 1024;
+    constexpr int NT = w3_nt(W, CP);   // + the dY block's (CP x 384 B)
+    constexpr int STG = NT * 1024;
+    constexpr int PHI = (NT + 3) / 4, PLO = NT / 4;  // DMA instructions of waves wv < NT % 4 / the others
+    static_assert(PHI <= 15, "vmcnt immediate");
     extern __shared__ __attribute__((aligned(1024))) char sm[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int tile = blockIdx.x, split = blockIdx.y;
@@ -96,22 +96,22 @@ __global__ __launch_bounds__(256, 1) void k_wgrad3h(Wg3hArgs a) {
     const int ch0 = split * a.cps;
     const int ch1 = min(ch0 + a.cps, a.nchunk);
 
-    // this wave's DMA instructions of a chunk: i = wv, wv + 4, ... over NT (halo first, then dY)
+    // this wave's DMA instructions of a chunk: i = wv, wv + 4, ... below NT (halo first, then dY)
     auto issue = [&](int c, int buf) {
-        const int row0 = c * RB;  // first image row of the chunk in the B H row space
+        const int rbk = c / NSEG, sg = c - (c / NSEG) * NSEG;
+        const int row0 = rbk * RB;  // first image row of the chunk in the B H row space
+        const int x0 = sg * SW;
         const int b = row0 / H, y0 = row0 - (row0 / H) * H;
         char* st = sm + buf * STG;
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
+        for (int k = 0; k < PHI; ++k) {
             const int i = 4 * k + wv;
-            int voff;
-            if (i >= NT) {
-                w3_dma16(rx, st + i * 1024, OOB);  // padding: zeros into the stage's tail
-            } else if (i < NH) {
+            if (i >= NT) break;
+            if (i < NH) {
                 const int u = i * 64 + lane;  // physical 16-B unit of the halo image
                 const int hp = u >> 3, lp = (u & 7) ^ w3_swz(u >> 3);
                 const int hr = hp / W2, hc = hp - (hp / W2) * W2;
-                int y = y0 + hr - 1, x = hc - 1;
+                int y = y0 + hr - 1, x = x0 + hc - 1;
                 bool ok = hp < HPX;
                 if (a.circular) {
                     y = wrap_idx(y, H);
@@ -119,12 +119,13 @@ __global__ __launch_bounds__(256, 1) void k_wgrad3h(Wg3hArgs a) {
                 } else {
                     ok = ok && y >= 0 && y < H && x >= 0 && x < W;
                 }
-                voff = ok ? ((b * H + y) * W + x) * (Cs * 4) + cbyte + 16 * lp : OOB;
+                const int voff = ok ? ((b * H + y) * W + x) * (Cs * 4) + cbyte + 16 * lp : OOB;
                 w3_dma16(rx, st + i * 1024, voff);
             } else {
                 const int u = (i - NH) * 64 + lane;  // physical unit of the dY image: 24 per pixel
                 const int px = u / 24, lp = (u - (u / 24) * 24) ^ w3_swz(u / 24);
-                voff = ((row0 * W + px) * a.Cout + 96 * cob) * 4 + 16 * lp;
+                const int r = px / SW, xx = px - (px / SW) * SW;
+                const int voff = (((row0 + r) * W + x0 + xx) * a.Cout + 96 * cob) * 4 + 16 * lp;
                 w3_dma16(rd, st + HB + (i - NH) * 1024, voff);
             }
         }
@@ -168,8 +169,9 @@ __global__ __launch_bounds__(256, 1) void k_wgrad3h(Wg3hArgs a) {
     for (int c = ch0; c < ch1; ++c) {
         const int buf = (c - ch0) % W3_NSTAGE;
         // this wave's DMA of chunk c landed (chunk c + 1's may still be in flight)
-        if (c + 1 < ch1) __builtin_amdgcn_s_waitcnt(WAIT_ONE);
-        else __builtin_amdgcn_s_waitcnt(W3_WAIT_VM0);
+        if (c + 1 >= ch1) __builtin_amdgcn_s_waitcnt(W3_WAIT_VM0);
+        else if (wv < NT % 4) __builtin_amdgcn_s_waitcnt(0x0F70 | PHI);
+        else __builtin_amdgcn_s_waitcnt(0x0F70 | PLO);
         // every wave's; the stage of chunk c - 1 is no longer read.  A bare s_barrier: __syncthreads' fence
         // would drain vmcnt, i.e. chunk c + 1's DMA as well
         __builtin_amdgcn_s_barrier();
@@ -177,9 +179,9 @@ __global__ __launch_bounds__(256, 1) void k_wgrad3h(Wg3hArgs a) {
         const int X = lds0 + buf * STG;
         const int D = X + HB;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {  // two k steps of 32 pixels
+        for (int s = 0; s < CP / 32; ++s) {  // k steps of 32 pixels
             const int o = 32 * s + 8 * g;       // this lane group's first chunk pixel
-            const int r = o / W, x = o - (o / W) * W;
+            const int r = o / SW, x = o - (o / SW) * SW;
             v4s Bf[3][4], Af[2][4];             // [hi u0, hi u1, lo u0, lo u1]
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -258,18 +260,31 @@ bool wgrad3h_takes(int B, int H, int W, int C1, int C2, int Cout, int ks, int st
 
 // max_split: the partial planes the caller's workspace holds; *nsplit: the planes written
 int launch_wgrad3h(Wg3hArgs& a, int max_split, int* nsplit, hipStream_t st) {
-    a.RB = 64 / a.W;
-    a.nchunk = a.B * a.H / a.RB;
+    static const int cp = [] {  // chunk pixels: 64 (one workgroup per CU) or 32 (two); A/B
+        const char* e = getenv("TCX_W3_CP");
+        return e && atoi(e) == 32 ? 32 : 64;
+    }();
+    const int per_cu = cp == 32 ? 2 : 1;
+    a.nchunk = a.B * a.H * a.W / cp;
     a.ncob = a.Cout / 96;
     const int tiles = (a.Cin / 32) * a.ncob;
-    int ns = std::max(1, std::min({max_split, std::max(1, 256 / tiles), a.nchunk}));
+    int ns = std::max(1, std::min({max_split, std::max(1, 256 * per_cu / tiles), a.nchunk}));
     a.cps = cdiv(a.nchunk, ns);
     ns = cdiv(a.nchunk, a.cps);
     using K = void (*)(Wg3hArgs);
-    const K k = a.W == 64 ? &k_wgrad3h<64> : (a.W == 32 ? &k_wgrad3h<32> : &k_wgrad3h<16>);
-    const size_t lds = wgrad3h_lds_bytes(a.W);
-    static bool attr[3] = {};
-    const int ki = a.W == 64 ? 0 : (a.W == 32 ? 1 : 2);
+    K k;
+    size_t lds;
+    int ki;
+    if (cp == 64) {
+        k = a.W == 64 ? &k_wgrad3h<64, 64> : (a.W == 32 ? &k_wgrad3h<32, 64> : &k_wgrad3h<16, 64>);
+        lds = wgrad3h_lds_bytes(a.W, 64);
+        ki = a.W == 64 ? 0 : (a.W == 32 ? 1 : 2);
+    } else {
+        k = a.W == 64 ? &k_wgrad3h<64, 32> : (a.W == 32 ? &k_wgrad3h<32, 32> : &k_wgrad3h<16, 32>);
+        lds = wgrad3h_lds_bytes(a.W, 32);
+        ki = 3 + (a.W == 64 ? 0 : (a.W == 32 ? 1 : 2));
+    }
+    static bool attr[6] = {};
     if (!attr[ki]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
             hipSuccess) {
