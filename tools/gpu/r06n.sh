@@ -1,5 +1,5 @@
-# Round 6: the halo weight gradient with 32-pixel chunks (two workgroups per CU, default) vs 64-pixel chunks
-# (TCX_W3_CP=64): its tests under both, then the score step alternating, then the kernel trace.
+# Round 6: the halo weight gradient with 32-pixel chunks (TCX_W3_CP=32, two workgroups per CU) vs 64-pixel
+# chunks (the default): its tests under both, then the score step alternating, then the kernel trace.
 set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp

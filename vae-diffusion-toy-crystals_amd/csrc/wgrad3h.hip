@@ -260,9 +260,9 @@ bool wgrad3h_takes(int B, int H, int W, int C1, int C2, int Cout, int ks, int st
 
 // max_split: the partial planes the caller's workspace holds; *nsplit: the planes written
 int launch_wgrad3h(Wg3hArgs& a, int max_split, int* nsplit, hipStream_t st) {
-    static const int cp = [] {  // chunk pixels: 64 (one workgroup per CU) or 32 (two); A/B
+    static const int cp = [] {  // chunk pixels: 32 (two workgroups per CU) or 64 (one; A/B)
         const char* e = getenv("TCX_W3_CP");
-        return e && atoi(e) == 32 ? 32 : 64;
+        return e && atoi(e) == 64 ? 64 : 32;
     }();
     const int per_cu = cp == 32 ? 2 : 1;
     a.nchunk = a.B * a.H * a.W / cp;
