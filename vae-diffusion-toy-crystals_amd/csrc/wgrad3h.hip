@@ -6,12 +6,14 @@
 // k_wgrad_h2 (gemm.hip) gathers an im2col tile per 128-k block, so every input pixel is fetched once per
 // tap it feeds (9x) and dY once per k block (7-27x): per 32-pixel chunk it moves 28 KB for 32 x 128 x 96
 // MACs, more than the L1 return path sustains (0.26 of the f16x3 ceiling, profiles/r06_d_*).  Here a
-// workgroup owns ALL nine taps of one 32-channel group x 96 output channels and walks 64-pixel chunks
-// (1, 2 or 4 image rows at W = 64, 32, 16):
-//   * the chunk's input halo ((rows + 2) x (W + 2) pixels x 32 channels, h2 records, 128 B per pixel) and
-//     its dY block (64 pixels x 96 channels, 384 B per pixel) land in LDS by LDS-DMA (buffer_load ... lds,
+// workgroup owns ALL nine taps of one 32-channel group x 96 output channels and walks chunks of 32 pixels
+// (half a row at W = 64, a row at 32, two rows at 16; TCX_W3_CP=64: 64-pixel chunks, one workgroup per CU):
+//   * the chunk's input halo ((rows + 2) x (cols + 2) pixels x 32 channels, h2 records, 128 B per pixel) and
+//     its dY block (32 pixels x 96 channels, 384 B per pixel) land in LDS by LDS-DMA (buffer_load ... lds,
 //     no registers), in a three-stage ring: chunks c + 1 and c + 2 stream in while chunk c is multiplied
 //     (with two stages the DMA latency, not the MFMA, set the chunk time: 4.6 us per 64-pixel chunk at 64^2);
+//     at 32-pixel chunks the ring is 3 x 21-25 KB, so two workgroups share a CU and one's DMA issue and
+//     address VALU run beside the other's MFMAs (268 vs 310 us per 64^2 96 -> 96 launch);
 //   * the MFMA operands (8 consecutive pixels of one channel per lane) come from ds_read_b64_tr_b16 on the
 //     pixel-major images, each tap reading the halo at its own (dy, dx) offset — the halo is fetched once
 //     for all nine taps;
