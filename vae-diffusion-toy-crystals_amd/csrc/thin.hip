@@ -28,56 +28,61 @@ __device__ __forceinline__ float thin_act(float v, int act) {
     return v;
 }
 
-// one workgroup per output row, one thread per (output pixel, 4 output channels) in turn; the weights
-// transposed into LDS as [tap][Cout] and the row's ks input rows (with their wrapped / zero halo columns)
-// staged in LDS once per row, so the inner loop reads only LDS; 32-bit index math
+// workgroups stride over the output rows (weights transposed into LDS as [tap][Cout] and the bias staged once
+// per workgroup: staging them per row cost more than the row's arithmetic); per row the ks input rows (with
+// their wrapped / zero halo columns) are staged in LDS and one thread takes (output pixel, 4 output channels)
+// in turn; 32-bit index math
 __global__ __launch_bounds__(256) void k_thin_cin1(ThinConv a) {
     extern __shared__ __attribute__((aligned(16))) float wT[];
     const int T = a.ks * a.ks, Q = a.Cout / 4, XW = a.Wo + a.ks - 1;  // staged row width
-    float* xs = wT + T * a.Cout;                                      // [ks][XW]
-    const int row = blockIdx.x, b = row / a.Ho, oy = row - b * a.Ho;
-    const float* xb = a.x + (size_t)b * a.H * a.W;
+    float* bsh = wT + T * a.Cout;                                     // [Cout] bias
+    float* xs = bsh + a.Cout;                                         // [ks][XW]
     for (int i = threadIdx.x; i < T * a.Cout; i += 256) {
-        const int tap = i / a.Cout, co = i - tap * a.Cout;
-        wT[i] = a.w[(size_t)co * a.kpad + tap];
+        const int co = i / T, tap = i - co * T;  // consecutive lanes read one packed row's taps
+        wT[tap * a.Cout + co] = a.w[(size_t)co * a.kpad + tap];
     }
-    for (int i = threadIdx.x; i < a.ks * XW; i += 256) {
-        const int dy = i / XW, c = i - dy * XW;  // staged column c = input column c - pad
-        int iy = oy + dy - a.pad, ix = c - a.pad;
-        float v = 0.f;
-        if (a.circular) v = xb[wrap_idx(iy, a.H) * a.W + wrap_idx(ix, a.W)];
-        else if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) v = xb[iy * a.W + ix];
-        xs[i] = v;
-    }
-    __syncthreads();
-    for (int it = threadIdx.x; it < a.Wo * Q; it += 256) {
-        const int ox = it / Q, cq = it - ox * Q;
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int dy = 0; dy < a.ks; ++dy)
-            for (int dx = 0; dx < a.ks; ++dx) {
-                const float v = xs[dy * XW + ox + dx];
-                const float4 w4 = *reinterpret_cast<const float4*>(wT + (dy * a.ks + dx) * a.Cout + 4 * cq);
-                acc.x = fmaf(v, w4.x, acc.x); acc.y = fmaf(v, w4.y, acc.y);
-                acc.z = fmaf(v, w4.z, acc.z); acc.w = fmaf(v, w4.w, acc.w);
+    for (int i = threadIdx.x; i < a.Cout; i += 256) bsh[i] = a.bias ? a.bias[i] : 0.f;
+    for (int row = blockIdx.x; row < a.B * a.Ho; row += gridDim.x) {
+        const int b = row / a.Ho, oy = row - b * a.Ho;
+        const float* xb = a.x + (size_t)b * a.H * a.W;
+        __syncthreads();  // the previous row's reads of xs are done (and the weights staged)
+        for (int i = threadIdx.x; i < a.ks * XW; i += 256) {
+            const int dy = i / XW, c = i - dy * XW;  // staged column c = input column c - pad
+            const int iy = oy + dy - a.pad, ix = c - a.pad;
+            float v = 0.f;
+            if (a.circular) v = xb[wrap_idx(iy, a.H) * a.W + wrap_idx(ix, a.W)];
+            else if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) v = xb[iy * a.W + ix];
+            xs[i] = v;
+        }
+        __syncthreads();
+        for (int it = threadIdx.x; it < a.Wo * Q; it += 256) {
+            const int ox = it / Q, cq = it - ox * Q;
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int dy = 0; dy < a.ks; ++dy)
+                for (int dx = 0; dx < a.ks; ++dx) {
+                    const float v = xs[dy * XW + ox + dx];
+                    const float4 w4 = *reinterpret_cast<const float4*>(wT + (dy * a.ks + dx) * a.Cout + 4 * cq);
+                    acc.x = fmaf(v, w4.x, acc.x); acc.y = fmaf(v, w4.y, acc.y);
+                    acc.z = fmaf(v, w4.z, acc.z); acc.w = fmaf(v, w4.w, acc.w);
+                }
+            float4 add = *reinterpret_cast<const float4*>(bsh + 4 * cq);
+            if (a.bias_b) {
+                const float4 bb = *reinterpret_cast<const float4*>(a.bias_b + (size_t)b * a.Cout + 4 * cq);
+                add.x += bb.x; add.y += bb.y; add.z += bb.z; add.w += bb.w;
             }
-        float add[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int e = 0; e < 4; ++e) {
-            const int co = 4 * cq + e;
-            if (a.bias) add[e] += a.bias[co];
-            if (a.bias_b) add[e] += a.bias_b[(size_t)b * a.Cout + co];
+            const size_t oi = ((size_t)row * a.Wo + ox) * a.Cout + 4 * cq;
+            if (a.resid) {
+                const float4 rr = *reinterpret_cast<const float4*>(a.resid + oi);
+                add.x += rr.x; add.y += rr.y; add.z += rr.z; add.w += rr.w;
+            }
+            const float4 out = make_float4(thin_act(acc.x + add.x, a.act), thin_act(acc.y + add.y, a.act),
+                                           thin_act(acc.z + add.z, a.act), thin_act(acc.w + add.w, a.act));
+            *reinterpret_cast<float4*>(a.y + oi) = out;
         }
-        const size_t oi = ((size_t)row * a.Wo + ox) * a.Cout + 4 * cq;
-        if (a.resid) {
-            const float4 rr = *reinterpret_cast<const float4*>(a.resid + oi);
-            add[0] += rr.x; add[1] += rr.y; add[2] += rr.z; add[3] += rr.w;
-        }
-        const float4 out = make_float4(thin_act(acc.x + add[0], a.act), thin_act(acc.y + add[1], a.act),
-                                       thin_act(acc.z + add[2], a.act), thin_act(acc.w + add[3], a.act));
-        *reinterpret_cast<float4*>(a.y + oi) = out;
     }
 }
 
-// one workgroup per output row: the ks input rows are read as contiguous [x][c] float4 streams (lane =
+// workgroups stride over the output rows; per row the ks input rows are read as contiguous [x][c] float4 streams (lane =
 // 4 channels of one pixel, coalesced), each float4 dotted with the ks weight quads of its tap row per dx
 // and the ks partials per (dx, x, quad) left in LDS; the row's outputs then sum them in a fixed order
 // (4 lanes per pixel over quads, then dx).  Row stride QP = Q | 1 floats keeps those reads free of bank
@@ -88,47 +93,49 @@ __global__ __launch_bounds__(256) void k_thin_cout1(ThinConv a) {
     float* wk = sm;                      // [ks ks C]
     float* part = sm + ks * ks * C;      // [ks][W][QP]
     for (int i = threadIdx.x; i < ks * ks * C; i += 256) wk[i] = a.w[i];
-    __syncthreads();
-    const int row = blockIdx.x, b = row / a.Ho, oy = row - b * a.Ho;
-    const float* xb = a.x + (size_t)b * a.H * a.W * C;
-    for (int it = threadIdx.x; it < a.W * Q; it += 256) {
-        const int x = it / Q, cq = it - x * Q;
-        float acc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int dy = 0; dy < ks; ++dy) {
-            int iy = oy + dy - a.pad;
-            if (a.circular) iy = wrap_idx(iy, a.H);
-            else if (iy < 0 || iy >= a.H) continue;
-            const float4 v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + x) * C + 4 * cq);
-            for (int dx = 0; dx < ks; ++dx) {
-                const float4 w4 = *reinterpret_cast<const float4*>(wk + (dy * ks + dx) * C + 4 * cq);
-                acc[dx] = fmaf(v.w, w4.w, fmaf(v.z, w4.z, fmaf(v.y, w4.y, fmaf(v.x, w4.x, acc[dx]))));
+    for (int row = blockIdx.x; row < a.B * a.Ho; row += gridDim.x) {
+        const int b = row / a.Ho, oy = row - b * a.Ho;
+        const float* xb = a.x + (size_t)b * a.H * a.W * C;
+        __syncthreads();  // the weights staged; the previous row's partials read
+        for (int it = threadIdx.x; it < a.W * Q; it += 256) {
+            const int x = it / Q, cq = it - x * Q;
+            float acc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (int dy = 0; dy < ks; ++dy) {
+                int iy = oy + dy - a.pad;
+                if (a.circular) iy = wrap_idx(iy, a.H);
+                else if (iy < 0 || iy >= a.H) continue;
+                const float4 v = *reinterpret_cast<const float4*>(xb + ((size_t)iy * a.W + x) * C + 4 * cq);
+                for (int dx = 0; dx < ks; ++dx) {
+                    const float4 w4 = *reinterpret_cast<const float4*>(wk + (dy * ks + dx) * C + 4 * cq);
+                    acc[dx] = fmaf(v.w, w4.w, fmaf(v.z, w4.z, fmaf(v.y, w4.y, fmaf(v.x, w4.x, acc[dx]))));
+                }
             }
+            for (int dx = 0; dx < ks; ++dx) part[(dx * a.W + x) * QP + cq] = acc[dx];
         }
-        for (int dx = 0; dx < ks; ++dx) part[(dx * a.W + x) * QP + cq] = acc[dx];
-    }
-    __syncthreads();
-    // 4 lanes per output pixel, each summing every 4th quad over the ks dx taps, then two xor shuffles
-    // (a fixed order); all 256 lanes reach the shuffles
-    const int sub = threadIdx.x & 3;
-    for (int o0 = 0; o0 < a.Wo; o0 += 64) {
-        const int ox = o0 + (threadIdx.x >> 2);
-        const bool live = ox < a.Wo;
-        float s = 0.f;
-        for (int dx = 0; dx < ks && live; ++dx) {
-            int ix = ox + dx - a.pad;
-            if (a.circular) ix = wrap_idx(ix, a.W);
-            else if (ix < 0 || ix >= a.W) continue;
-            const float* pp = part + (dx * a.W + ix) * QP;
-            for (int q = sub; q < Q; q += 4) s += pp[q];
+        __syncthreads();
+        // 4 lanes per output pixel, each summing every 4th quad over the ks dx taps, then two xor shuffles
+        // (a fixed order); all 256 lanes reach the shuffles
+        const int sub = threadIdx.x & 3;
+        for (int o0 = 0; o0 < a.Wo; o0 += 64) {
+            const int ox = o0 + (threadIdx.x >> 2);
+            const bool live = ox < a.Wo;
+            float s = 0.f;
+            for (int dx = 0; dx < ks && live; ++dx) {
+                int ix = ox + dx - a.pad;
+                if (a.circular) ix = wrap_idx(ix, a.W);
+                else if (ix < 0 || ix >= a.W) continue;
+                const float* pp = part + (dx * a.W + ix) * QP;
+                for (int q = sub; q < Q; q += 4) s += pp[q];
+            }
+            s += __shfl_xor(s, 1);
+            s += __shfl_xor(s, 2);
+            if (!live || sub != 0) continue;
+            const size_t o = (size_t)row * a.Wo + ox;
+            float v = s + (a.bias ? a.bias[0] : 0.f);
+            if (a.bias_b) v += a.bias_b[b];
+            if (a.resid) v += a.resid[o];
+            a.y[o] = thin_act(v, a.act);
         }
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        if (!live || sub != 0) continue;
-        const size_t o = (size_t)row * a.Wo + ox;
-        float v = s + (a.bias ? a.bias[0] : 0.f);
-        if (a.bias_b) v += a.bias_b[b];
-        if (a.resid) v += a.resid[o];
-        a.y[o] = thin_act(v, a.act);
     }
 }
 
@@ -143,17 +150,18 @@ bool thin_conv_takes(const ThinConv& a) {
     static const bool off = getenv("TCX_THIN") && getenv("TCX_THIN")[0] == '0';  // A/B: the MFMA kernels
     if (off || a.ks < 1 || a.ks > 7 || a.B <= 0 || (size_t)a.B * a.Ho >= (1u << 31)) return false;
     if (a.Cin == 1 && a.Cout % 4 == 0 && a.ks * a.ks * a.Cout <= 8192 && a.Wo + a.ks - 1 <= 4096 && aligned16(a.y) &&
-        (!a.resid || aligned16(a.resid)))
+        (!a.resid || aligned16(a.resid)) && (!a.bias_b || aligned16(a.bias_b)))
         return true;
     return a.Cout == 1 && a.Cin % 4 == 0 && cout1_lds(a) <= 48 * 1024 && aligned16(a.x) && aligned16(a.w);
 }
 
 int launch_thin_conv(const ThinConv& a, hipStream_t st) {
     if (a.Cin == 1) {
-        hipLaunchKernelGGL(k_thin_cin1, dim3(a.B * a.Ho), dim3(256),
-                           ((size_t)a.ks * a.ks * a.Cout + (size_t)a.ks * (a.Wo + a.ks - 1)) * sizeof(float), st, a);
+        hipLaunchKernelGGL(k_thin_cin1, dim3(std::min(a.B * a.Ho, 2048)), dim3(256),
+                           ((size_t)a.ks * a.ks * a.Cout + a.Cout + (size_t)a.ks * (a.Wo + a.ks - 1)) * sizeof(float), st,
+                           a);
     } else {
-        hipLaunchKernelGGL(k_thin_cout1, dim3(a.B * a.Ho), dim3(256), cout1_lds(a), st, a);
+        hipLaunchKernelGGL(k_thin_cout1, dim3(std::min(a.B * a.Ho, 2048)), dim3(256), cout1_lds(a), st, a);
     }
     return check_launch("thin conv");
 }
