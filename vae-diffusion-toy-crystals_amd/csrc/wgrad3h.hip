@@ -27,6 +27,7 @@
 #include "h2.hpp"
 
 #include <algorithm>
+#include <utility>
 
 namespace tcx {
 
@@ -54,11 +55,18 @@ __host__ __device__ constexpr int w3_halo_px(int W, int CP) { return (w3_rb(W, C
 __host__ __device__ constexpr int w3_nh(int W, int CP) { return (w3_halo_px(W, CP) * 128 + 1023) / 1024; }
 __host__ __device__ constexpr int w3_nt(int W, int CP) { return w3_nh(W, CP) + CP * 384 / 1024; }  // 1-KB DMAs
 __host__ __device__ constexpr int w3_stage(int W, int CP) { return w3_nt(W, CP) * 1024; }
-constexpr int W3_NSTAGE = 3;  // ring depth: chunks c + 1 and c + 2 stream in while chunk c is multiplied
-constexpr size_t wgrad3h_lds_bytes(int W, int CP) { return W3_NSTAGE * (size_t)w3_stage(W, CP); }
-static_assert(wgrad3h_lds_bytes(64, 64) <= 160 * 1024 && wgrad3h_lds_bytes(64, 32) <= 80 * 1024 &&
-                  wgrad3h_lds_bytes(32, 32) <= 80 * 1024 && wgrad3h_lds_bytes(16, 32) <= 80 * 1024,
+// NS: ring depth (chunks c + 1 .. c + NS - 1 stream in while chunk c is multiplied)
+constexpr size_t wgrad3h_lds_bytes(int W, int CP, int NS) { return NS * (size_t)w3_stage(W, CP); }
+static_assert(wgrad3h_lds_bytes(64, 64, 3) <= 160 * 1024 && wgrad3h_lds_bytes(64, 32, 3) <= 80 * 1024 &&
+                  wgrad3h_lds_bytes(32, 32, 3) <= 80 * 1024 && wgrad3h_lds_bytes(16, 32, 3) <= 80 * 1024 &&
+                  wgrad3h_lds_bytes(64, 32, 6) <= 160 * 1024 && wgrad3h_lds_bytes(16, 32, 6) <= 160 * 1024,
               "wgrad3h ring exceeds the CU's LDS");
+// s_waitcnt vmcnt(n), n <= 63 (gfx9 split field), no expcnt / lgkmcnt wait
+__host__ __device__ constexpr int w3_vm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
+template <typename F, int... Is>
+__device__ __forceinline__ void w3_for(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
 
 __device__ __forceinline__ int w3_swz(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 2); }
 
@@ -70,10 +78,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef short v8s __attribute__((ext_vector_type(8)));
 
-// CP = 64: one workgroup per CU (the ring is 3 x 49-52 KB); CP = 32: two per CU (3 x 21-25 KB each), whose
-// waves' DMA / VALU then run beside the other workgroup's MFMAs
-template <int W, int CP>
-__global__ __launch_bounds__(256, CP == 32 ? 2 : 1) void k_wgrad3h(Wg3hArgs a) {
+// CP = 64: one workgroup per CU (the ring is 3 x 49-52 KB); CP = 32, NWG = 2: two per CU (3 x 21-25 KB each),
+// whose waves' DMA / VALU then run beside the other workgroup's MFMAs.  Measured and dropped: CP = 32 with a
+// six-deep ring and one workgroup per CU (410 vs 268 us per 64^2 launch: not the DMA latency, the co-resident
+// waves are the lever) and three workgroups per CU (two stages; 168 VGPRs: 80 spilled)
+template <int W, int CP, int NS, int NWG>
+__global__ __launch_bounds__(256, NWG) void k_wgrad3h(Wg3hArgs a) {
     constexpr int SW = w3_sw(W, CP), RB = w3_rb(W, CP), NSEG = W / SW, W2 = SW + 2;
     constexpr int HPX = w3_halo_px(W, CP);
     constexpr int NH = w3_nh(W, CP);   // halo DMA instructions per chunk (1 KB each)
@@ -166,18 +176,26 @@ __global__ __launch_bounds__(256, CP == 32 ? 2 : 1) void k_wgrad3h(Wg3hArgs a) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    if (ch0 < ch1) issue(ch0, 0);
-    if (ch0 + 1 < ch1) issue(ch0 + 1, 1);
+#pragma unroll
+    for (int k = 0; k < NS - 1; ++k)
+        if (ch0 + k < ch1) issue(ch0 + k, k);
+    const bool whi = wv < NT % 4;  // this wave issues PHI DMA instructions per chunk, else PLO
     for (int c = ch0; c < ch1; ++c) {
-        const int buf = (c - ch0) % W3_NSTAGE;
-        // this wave's DMA of chunk c landed (chunk c + 1's may still be in flight)
-        if (c + 1 >= ch1) __builtin_amdgcn_s_waitcnt(W3_WAIT_VM0);
-        else if (wv < NT % 4) __builtin_amdgcn_s_waitcnt(0x0F70 | PHI);
-        else __builtin_amdgcn_s_waitcnt(0x0F70 | PLO);
+        const int buf = (c - ch0) % NS;
+        // this wave's DMA of chunk c landed (the newer chunks' may still be in flight)
+        const int newer = min(NS - 2, ch1 - 1 - c);
+        static_assert((NS - 2) * PHI <= 63, "vmcnt range");
+        w3_for([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            if (newer == k) {
+                if (whi) __builtin_amdgcn_s_waitcnt(w3_vm(k * PHI));
+                else __builtin_amdgcn_s_waitcnt(w3_vm(k * PLO));
+            }
+        }, std::make_integer_sequence<int, NS - 1>{});
         // every wave's; the stage of chunk c - 1 is no longer read.  A bare s_barrier: __syncthreads' fence
         // would drain vmcnt, i.e. chunk c + 1's DMA as well
         __builtin_amdgcn_s_barrier();
-        if (c + 2 < ch1) issue(c + 2, (buf + 2) % W3_NSTAGE);
+        if (c + NS - 1 < ch1) issue(c + NS - 1, (buf + NS - 1) % NS);
         const int X = lds0 + buf * STG;
         const int D = X + HB;
 #pragma unroll
@@ -262,11 +280,11 @@ bool wgrad3h_takes(int B, int H, int W, int C1, int C2, int Cout, int ks, int st
 
 // max_split: the partial planes the caller's workspace holds; *nsplit: the planes written
 int launch_wgrad3h(Wg3hArgs& a, int max_split, int* nsplit, hipStream_t st) {
-    static const int cp = [] {  // chunk pixels: 32 (two workgroups per CU) or 64 (one; A/B)
+    static const int cp = [] {  // chunk pixels: 32 (default) or 64 (one workgroup per CU, three stages; A/B)
         const char* e = getenv("TCX_W3_CP");
         return e && atoi(e) == 64 ? 64 : 32;
     }();
-    const int per_cu = cp == 32 ? 2 : 1;
+    const int per_cu = cp == 64 ? 1 : 2;
     a.nchunk = a.B * a.H * a.W / cp;
     a.ncob = a.Cout / 96;
     const int tiles = (a.Cin / 32) * a.ncob;
@@ -276,15 +294,16 @@ int launch_wgrad3h(Wg3hArgs& a, int max_split, int* nsplit, hipStream_t st) {
     using K = void (*)(Wg3hArgs);
     K k;
     size_t lds;
+    const int wi = a.W == 64 ? 0 : (a.W == 32 ? 1 : 2);
     int ki;
     if (cp == 64) {
-        k = a.W == 64 ? &k_wgrad3h<64, 64> : (a.W == 32 ? &k_wgrad3h<32, 64> : &k_wgrad3h<16, 64>);
-        lds = wgrad3h_lds_bytes(a.W, 64);
-        ki = a.W == 64 ? 0 : (a.W == 32 ? 1 : 2);
+        k = a.W == 64 ? &k_wgrad3h<64, 64, 3, 1> : (a.W == 32 ? &k_wgrad3h<32, 64, 3, 1> : &k_wgrad3h<16, 64, 3, 1>);
+        lds = wgrad3h_lds_bytes(a.W, 64, 3);
+        ki = wi;
     } else {
-        k = a.W == 64 ? &k_wgrad3h<64, 32> : (a.W == 32 ? &k_wgrad3h<32, 32> : &k_wgrad3h<16, 32>);
-        lds = wgrad3h_lds_bytes(a.W, 32);
-        ki = 3 + (a.W == 64 ? 0 : (a.W == 32 ? 1 : 2));
+        k = a.W == 64 ? &k_wgrad3h<64, 32, 3, 2> : (a.W == 32 ? &k_wgrad3h<32, 32, 3, 2> : &k_wgrad3h<16, 32, 3, 2>);
+        lds = wgrad3h_lds_bytes(a.W, 32, 3);
+        ki = 3 + wi;
     }
     static bool attr[6] = {};
     if (!attr[ki]) {
