@@ -27,6 +27,7 @@
 #include "h2.hpp"
 
 #include <algorithm>
+#include <mutex>
 #include <utility>
 
 namespace tcx {
@@ -305,14 +306,16 @@ int launch_wgrad3h(Wg3hArgs& a, int max_split, int* nsplit, hipStream_t st) {
         lds = wgrad3h_lds_bytes(a.W, 32, 3);
         ki = 3 + wi;
     }
-    static bool attr[6] = {};
-    if (!attr[ki]) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-            hipSuccess) {
-            set_error("tcx_conv_wgrad_h2: cannot enable %zu B of dynamic LDS", lds);
-            return TCX_EHIP;
-        }
-        attr[ki] = true;
+    // the dynamic-LDS opt-in once per kernel variant (host threads may race to the first call)
+    static std::once_flag once[6];
+    static hipError_t attr_rc[6];
+    std::call_once(once[ki], [&] {
+        attr_rc[ki] = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds);
+    });
+    if (attr_rc[ki] != hipSuccess) {
+        set_error("tcx_conv_wgrad_h2: cannot enable %zu B of dynamic LDS", lds);
+        return TCX_EHIP;
     }
     hipLaunchKernelGGL(k, dim3(tiles, ns), dim3(256), lds, st, a);
     *nsplit = ns;
