@@ -295,8 +295,8 @@ def main() -> int:
         peak_basis = "2500 TFLOP/s dense f16 MFMA / 3 products per fp32 MAC; achieved in fp32-equivalent FLOPs"
     elif args.precision == "bf16":
         kname = ("bf16 single-product convs (config 5): k_conv3lb (LDS-DMA 3x3 at 64/128/256-px rows, "
-                 "v_mfma_f32_32x32x16_bf16) and k_conv3mb (16x16x32 tap pairs, Cin >= 192), k_conv4s2g (chunk-major "
-                 "skip planes), k_lin1x1 — one bf16 MFMA per MAC; all conv launches of the pass")
+                 "v_mfma_f32_32x32x16_bf16; TCX_CONV3MB=1 adds k_conv3mb's 16x16x32 tap pairs at Cin >= 192), "
+                 "k_conv4s2g (chunk-major skip planes), k_lin1x1 — one bf16 MFMA per MAC; all conv launches of the pass")
         peak = F16_PEAK_TFLOPS
         peak_basis = "2500 TFLOP/s dense bf16 MFMA"
     else:

@@ -370,10 +370,10 @@ size_t tcx_ode_workspace_size(const tcx_unet* net, int B, int H, int W, int n_st
 int tcx_debug_fail_eval(int k);
 
 /* Test hook (round 6): which 3x3 kernel runs config 5's 2-byte bf16 convs on this host thread — 0 k_conv3lb
- * only, 1 the measured default (k_conv3mb at Cin >= 192 with a 2-byte output), 2 k_conv3mb on every shape it
- * covers, -1 back to the TCX_CONV3MB environment default.  Returns the previous override.  Both kernels sum
- * the same bf16 products in the same k order: the outputs are bit-identical (the GroupNorm partials to the
- * fp32 rounding of their per-lane sums). */
+ * only (the default: measured 1.1 % faster end to end), 1 k_conv3mb at Cin >= 192 with a 2-byte output, 2
+ * k_conv3mb on every shape it covers, -1 back to the TCX_CONV3MB environment default.  Returns the previous
+ * override.  Both kernels sum the same bf16 products in the same k order: the outputs are bit-identical (the
+ * GroupNorm partials to the fp32 rounding of their per-lane sums). */
 int tcx_debug_conv3mb(int mode);
 
 /* Test hook (round 6): the calling thread's choice for the halo-staged 3x3 weight gradient of

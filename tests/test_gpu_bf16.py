@@ -470,9 +470,9 @@ def _conv_fmt(x1, x2, w, b, ks, stride, fmt, out_b2, gn=False):
 ])
 def test_b2_conv_equals_the_record_conv(B, C1, C2, H, co, ks, stride):
     """fp32 outputs and GroupNorm partials against the 4-byte record sources: bit for bit where both run one
-    kernel (4x4/s2, 1x1); for the 3x3 convs the b2 sources run k_conv3mb (16x16x32 tap pairs, round 6) and
-    the records k_conv3lb (32x32x16 taps) — the same bf16 products summed in fp32 in another order, so within
-    5e-6 of the output scale.  The b2 output is the round-to-nearest-even of the same kernel's fp32 output."""
+    kernel (4x4/s2, 1x1); for the 3x3 convs both run k_conv3lb by default (TCX_CONV3MB=1/2: the b2 sources on
+    k_conv3mb's 16x16x32 tap pairs — the same bf16 products summed in fp32 in another order), so within 5e-6 of
+    the output scale.  The b2 output is the round-to-nearest-even of the same kernel's fp32 output."""
     g_ = torch.Generator(device="cuda").manual_seed(1)
     x1 = torch.randn((B, H, H, C1), device="cuda", generator=g_)
     x2 = torch.randn((B, H, H, C2), device="cuda", generator=g_) if C2 else None
@@ -484,7 +484,7 @@ def test_b2_conv_equals_the_record_conv(B, C1, C2, H, co, ks, stride):
     if ks == 3:
         scale = max(1.0, float(yr.abs().max()))
         err = float((yr - yb).abs().max()) / scale
-        print(f"b2 (k_conv3mb) vs records (k_conv3lb) {C1}+{C2}->{co} at {H}^2: {err:.2e}")
+        print(f"b2 vs records (3x3) {C1}+{C2}->{co} at {H}^2: {err:.2e}")
         assert err < 5e-6
         np.testing.assert_allclose(gb.cpu().numpy(), gr.cpu().numpy(), rtol=1e-5, atol=1e-3)
     else:
@@ -662,7 +662,7 @@ def test_b2_256px_forward_chunk_major_skips_bit_identical(tmp_path):
 
 @pytest.fixture
 def conv3mb_everywhere():
-    """k_conv3mb on every b2 3x3 shape it covers (the default takes it at Cin >= 192 with a b2 output only)"""
+    """k_conv3mb on every b2 3x3 shape it covers (the default runs k_conv3lb everywhere)"""
     prev = L().tcx_debug_conv3mb(2)
     yield
     L().tcx_debug_conv3mb(prev)

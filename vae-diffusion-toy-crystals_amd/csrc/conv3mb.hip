@@ -348,15 +348,19 @@ int launch3mb(const ConvParams& p, hipStream_t st) {
 // Where it runs (measured per layer against k_conv3lb with its 3-slot ring, tools/mbbench.py at Bt = 84,
 // profiles/r06_c_cfg5_conv_layers_mb_vs_lb.txt): faster at Cin >= 192 with a b2 output (down2.net.3 879 vs
 // 926 us, up2.net.0 824 vs 855, mid.net.0 211 vs 218), slower at Cin = 96 (down1.net.3 1336 vs 1269 us,
-// up1.net.0 1954 vs 1908) and with an fp32 output (up2.net.3 318 vs 284, mid.net.3 234 vs 219) — so the
-// default takes those layers only.  Same products, same k order: the two kernels' outputs are bit-identical
+// up1.net.0 1954 vs 1908) and with an fp32 output (up2.net.3 318 vs 284, mid.net.3 234 vs 219).  Taking the
+// Cin >= 192 b2-output layers (mode 1) measured 1.1 % SLOWER end to end than k_conv3lb everywhere (config 5,
+// three alternating pairs: 9.164 / 9.168 / 9.173 vs 9.264 / 9.276 / 9.287 images/s, profiles/r06_u_cfg5_ab.txt;
+// mode 1 also caught up1.net.0's 256^2 concat, the layer it loses most on), so the default is mode 0 and the
+// kernel stays for A/B.  Same products, same k order: the two kernels' outputs are bit-identical
 // (tests/test_gpu_bf16.py test_b2_conv3mb_equals_conv3lb_bit_for_bit; the GroupNorm partials agree to the fp32
-// rounding of their per-lane sums, taken over the 16x16 vs 32x32 accumulator layouts).  TCX_CONV3MB=0: never, 2: every b2 shape.
+// rounding of their per-lane sums, taken over the 16x16 vs 32x32 accumulator layouts).  TCX_CONV3MB=1: Cin >= 192
+// with a b2 output, 2: every b2 shape, 0 (default): never.
 thread_local int g_conv3mb_force = -1;  // tcx_debug_conv3mb (tests): overrides the environment on this thread
 int conv3mb_mode() {
     static const int m = [] {
         const char* e = getenv("TCX_CONV3MB");
-        return (e && (e[0] == '0' || e[0] == '2')) ? e[0] - '0' : 1;
+        return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
     }();
     return g_conv3mb_force >= 0 ? g_conv3mb_force : m;
 }
