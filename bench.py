@@ -58,7 +58,7 @@ SPLIT_PRODUCTS = 3               # f16x3: hi*hi + hi*lo + lo*hi MFMAs per fp32 m
 # launches of two sampler steps.  A counter pass cannot run inside this process, so the measured
 # value is carried here with its source; it applies to the f16x3 path it was taken on.
 # keyed by (conv precision, image size): the 64x64 headline (f16x3) and config 5 (256x256 bf16)
-TRAFFIC_BYTES_PER_CONV_LAUNCH = {("f16x3", 64): 499.2e6, ("bf16", 256): 1004.7e6}
+TRAFFIC_BYTES_PER_CONV_LAUNCH = {("f16x3", 64): 499.2e6, ("bf16", 256): 997.5e6}
 TRAFFIC_SOURCE = {
     ("f16x3", 64): ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE in separate passes over bench.py --lanes 1 "
                     "(Bt = 256 per launch, the one-lane pass the roofline times), averaged over the 135 split-path "
@@ -66,8 +66,8 @@ TRAFFIC_SOURCE = {
                     "of two sampler steps, profiles/r06_fin_pmc_traffic.txt"),
     ("bf16", 256): ("rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE in separate passes over bench.py --img-size 256 "
                     "--batch 64 --precision bf16 --lanes 1 (64 images per launch: the evaluation runs in two passes "
-                    "under the 2 GiB cap), averaged over the 270 conv launches (k_conv3lb, k_conv3mb, k_conv4s2g, "
-                    "k_lin1x1) of two sampler steps, profiles/r06_fin_cfg5_pmc_traffic.txt"),
+                    "under the 2 GiB cap), averaged over the 270 conv launches (k_conv3lb, k_conv4s2g, k_lin1x1) of "
+                    "two sampler steps, profiles/r06_v_cfg5_pmc_traffic.txt"),
 }
 
 
