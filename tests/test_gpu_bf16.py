@@ -406,11 +406,11 @@ def test_b2_upsample_equals_the_record_upsample(B, H, W, C, tabs):
 
 
 def test_b2_attention_vs_the_record_attention_and_float64():
-    """the b2 attention (config 5; round 6: 4 waves x 64-key tiles, three workgroups per CU) against the 4-byte
-    record form (8 waves x 128-key tiles) and against float64 on the same bf16 operands.  The two tilings apply
-    the online softmax's running-max rescale at different key boundaries (and round P to bf16 under different
-    maxima), so they agree to bf16 rounding of the output, not bit for bit; each is gated against float64 as
-    test_bf16_attention_split_vs_float64 (1e-2 of the scale: P and the output are bf16)"""
+    """the b2 attention (config 5: 2-byte bf16 qkv and output) against the 4-byte record form of the same kernel
+    (8 waves x 128-key tiles, deferred running max) and against float64 on the same bf16 operands.  The b2 output
+    is rounded to bf16, so the two agree to bf16 rounding of the output; each is gated against float64 as
+    test_bf16_attention_split_vs_float64 (1e-2 of the scale: P and the output are bf16).  (A 4-wave x 64-key
+    form measured in round 6 was slower and removed, profiles/r06_h_attn_q4_ab.txt.)"""
     Bt, N, C, heads = 2, 1024, 192, 4
     D = C // heads
     qkv_np = (rng.standard_normal((Bt, N, 3 * C)) * 0.5).astype(np.float32)

@@ -97,7 +97,7 @@ __host__ __device__ constexpr int attn_ksb(int D, bool BF) { return (BF ? D * 2 
 // rows), run on one XCD at about the same time.
 template <int D, int FMT>
 __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict__ qkv, char* __restrict__ out, int N,
-                                                         int C, float scale, int xcd) {
+                                                         int C, float scale, int xcd, float defer2) {
     constexpr bool BF = FMT >= 1, B2 = FMT == 2;
     constexpr int ESZ = B2 ? 2 : 4;  // bytes per element of qkv / out
     static_assert(D % 16 == 0 && D <= 64, "split attention: head dim multiple of 16, <= 64");
@@ -207,7 +207,11 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
 #pragma unroll
         for (int n = 1; n < NST; ++n) mt = fmaxf(mt, mtn[n]);
         mt = fmaxf(mt, __shfl_xor(mt, 32));
-        const float mn = fmaxf(m, mt);
+        // bf16: the running max is deferred (FA4-style) -- the offset m moves only when the tile's max passes it
+        // by more than defer2 in log2 units of p, so p <= 2^(10 + defer2) (2^18: fp32 / bf16 range to spare, the
+        // softmax exact for any offset) and the O rescale below runs on a handful of tiles instead of most of
+        // them; defer2 = 0 is the exact running max
+        const float mn = BF ? ((mt - m) * scale2 > defer2 ? mt : m) : fmaxf(m, mt);
         // exponentials as hardware exp2 of pre-scaled logits (v_exp_f32; the VALU of the
         // softmax, not the MFMA, bounds this loop)
         const float alpha = __builtin_amdgcn_exp2f((m - mn) * scale2);  // 0 on the first tile (m = -inf)
@@ -318,8 +322,12 @@ int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hi
         const char* e = getenv("TCX_ATTN_XCD");
         return (e && e[0] == '0') ? 0 : 1;
     }();
+    static const float defer2 = [] {  // TCX_ATTN_DEFER: deferred-max threshold (log2 units; 0 = exact running max)
+        const char* e = getenv("TCX_ATTN_DEFER");
+        return e ? std::max(0.f, std::min(16.f, (float)atof(e))) : 8.f;
+    }();
     hipLaunchKernelGGL((k_attention_split<D, FMT>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
-                       (char*)out, N, C, scale, xcd);
+                       (char*)out, N, C, scale, xcd, defer2);
     return check_launch("tcx_attention_split");
 }
 
