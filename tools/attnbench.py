@@ -29,5 +29,5 @@ for _ in range(reps):
     e0.record(); run(); e1.record(); e1.synchronize()
     ts.append(e0.elapsed_time(e1) * 1e3)
 o = out.view(torch.bfloat16).float()
-print(f"attn_b2 defer={os.environ.get('TCX_ATTN_DEFER', 'default')} {statistics.median(ts):.1f} us "
+print(f"attn_b2 defer={os.environ.get('TCX_ATTN_DEFER', 'default')} pf2={os.environ.get('TCX_ATTN_PF2', 'default')} {statistics.median(ts):.1f} us "
       f"(min {min(ts):.1f}); out sum {o.sum().item():.6e} absmax {o.abs().max().item():.4f}")

@@ -26,20 +26,21 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
 // tile load (global -> registers) and store (registers -> LDS stage, V transposed) of the kernel below
-#define TCX_ATT_LOAD(k0) \
+#define TCX_ATT_LOAD_R(k0, kreg, vreg) \
     do { \
 _Pragma("unroll") \
         for (int u = 0; u < KI; ++u) {  /* BF: the hi pieces only (global piece 2 pc) */ \
-            const int i = tid + 512 * u; \
+            /* PF2: unconditional (ragged threads reload the last piece): no branch, exact vmcnt counts */ \
+            const int i = PF2 ? min(tid + 512 * u, KT * KPL - 1) : tid + 512 * u; \
             const int j = i / KPL, pc = i - (i / KPL) * KPL; \
-            if (KT * KPL % 512 == 0 || i < KT * KPL) \
+            if (PF2 || KT * KPL % 512 == 0 || i < KT * KPL) \
                 kreg[u] = *reinterpret_cast<const f4*>(base + (size_t)(k0 + j) * rs + (size_t)(C + h * D) * ESZ + \
                                                        (B2 ? pc : BF ? 2 * pc : pc) * 16); \
         } \
 _Pragma("unroll") \
         for (int u = 0; u < VI; ++u) { \
-            const int i = tid + 512 * u; \
-            if (i < (KT / 2) * G) { \
+            const int i = PF2 ? min(tid + 512 * u, (KT / 2) * G - 1) : tid + 512 * u; \
+            if (PF2 || i < (KT / 2) * G) { \
                 const int g = i / (KT / 2), jp = i - g * (KT / 2);  /* key pair (2 jp, 2 jp + 1), dim group g */ \
                 const char* src = base + (size_t)(k0 + 2 * jp) * rs + (size_t)(2 * C + h * D) * ESZ + g * 8 * ESZ; \
                 vreg[u][0] = *reinterpret_cast<const u4*>(src); \
@@ -49,7 +50,7 @@ _Pragma("unroll") \
             } \
         } \
     } while (0)
-#define TCX_ATT_STORE(st) \
+#define TCX_ATT_STORE_R(st, kreg, vreg) \
     do { \
         char* Ks = Kb(st); \
         unsigned* Vh = Vhb(st); \
@@ -83,6 +84,9 @@ _Pragma("unroll") \
         } \
     } while (0)
 
+#define TCX_ATT_LOAD(k0) TCX_ATT_LOAD_R(k0, kreg, vreg)
+#define TCX_ATT_STORE(st) TCX_ATT_STORE_R(st, kreg, vreg)
+
 // staged K row: h2 pieces (D * 4 B), or for BF only the hi pieces (D * 2 B: the lo halves of K and V are
 // never loaded), + 16 B pad (both strides an odd number of 16-B units: conflict-free b128 row reads)
 __host__ __device__ constexpr int attn_ksb(int D, bool BF) { return (BF ? D * 2 : D * 4) + 16; }
@@ -95,10 +99,15 @@ __host__ __device__ constexpr int attn_ksb(int D, bool BF) { return (BF ? D * 2 
 // 1,711 MB read per launch for 302 MB of qkv, profiles/r05_t_cfg5_pmc_traffic.txt).  With xcd_remap the
 // query blocks of an (image, head), and the heads of an image (whose K / V share cache lines of the token
 // rows), run on one XCD at about the same time.
-template <int D, int FMT>
+// PF2 (bf16 forms at N >= 512; TCX_ATTN_PF2=0: off): a second register set, so each key tile's global loads
+// are issued two tiles before its LDS store instead of one.  The loop is unrolled by two so both sets are
+// static registers and its loads / stores unconditional (the last trip reloads the last tile: no compiler
+// vmcnt(0) at control-flow joins), which leaves the previous tile's loads in flight across a whole tile.
+template <int D, int FMT, bool PF2 = false>
 __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict__ qkv, char* __restrict__ out, int N,
                                                          int C, float scale, int xcd, float defer2) {
     constexpr bool BF = FMT >= 1, B2 = FMT == 2;
+    static_assert(!PF2 || BF, "the two-deep prefetch is bf16 only");
     constexpr int ESZ = B2 ? 2 : 4;  // bytes per element of qkv / out
     static_assert(D % 16 == 0 && D <= 64, "split attention: head dim multiple of 16, <= 64");
     constexpr int KT = 128;            // keys per staged tile
@@ -165,13 +174,11 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
     constexpr int VI = ((KT / 2) * G + 511) / 512;   // V (key pair, dim group) items per thread
     f4 kreg[KI];        // native vectors: arrays of HIP's float4/uint4 structs stayed in scratch here
     u4 vreg[VI][4];
-    TCX_ATT_LOAD(0);
-    TCX_ATT_STORE(0);
-    __syncthreads();
+    f4 kreg2[PF2 ? KI : 1];  // PF2: the second set
+    u4 vreg2[PF2 ? VI : 1][4];
     const int ntile = N / KT;
-    for (int tt = 0; tt < ntile; ++tt) {
-        const int cur = tt & 1;
-        if (tt + 1 < ntile) TCX_ATT_LOAD((tt + 1) * KT);  // in flight during this tile's math
+    // one key tile's math from LDS stage cur
+    auto step = [&](const int cur) {
         const char* Ks = Kb(cur);
         const unsigned* Vh = Vhb(cur);
         const unsigned* Vl = Vlb(cur);
@@ -277,8 +284,32 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
             lt += __shfl_xor(lt, 32);
             l += lt;
         }
-        if (tt + 1 < ntile) TCX_ATT_STORE(cur ^ 1);  // that stage was last read in tile tt - 1
+    };
+    TCX_ATT_LOAD(0);
+    TCX_ATT_STORE(0);
+    if constexpr (PF2) {
+        // ntile even (N % 256 == 0), >= 4; set A carries even tiles, set B odd ones
+        TCX_ATT_LOAD_R(KT, kreg2, vreg2);
         __syncthreads();
+        for (int tt = 0; tt < ntile; tt += 2) {
+            TCX_ATT_LOAD_R(min(tt + 2, ntile - 1) * KT, kreg, vreg);  // set A was stored at the end of tile tt - 1
+            step(0);
+            TCX_ATT_STORE_R(1, kreg2, vreg2);  // tile tt + 1 (loaded during tile tt - 1) into the stage tile tt - 1 left
+            __syncthreads();
+            TCX_ATT_LOAD_R(min(tt + 3, ntile - 1) * KT, kreg2, vreg2);
+            step(1);
+            TCX_ATT_STORE_R(0, kreg, vreg);  // tile tt + 2 (the last trip: a reload, never read)
+            __syncthreads();
+        }
+    } else {
+        __syncthreads();
+        for (int tt = 0; tt < ntile; ++tt) {
+            const int cur = tt & 1;
+            if (tt + 1 < ntile) TCX_ATT_LOAD((tt + 1) * KT);  // in flight during this tile's math
+            step(cur);
+            if (tt + 1 < ntile) TCX_ATT_STORE(cur ^ 1);  // that stage was last read in tile tt - 1
+            __syncthreads();
+        }
     }
     if constexpr (ONES) {
         // row D of O^T: tile D / 32, register 4 ((D % 32) / 8) + (D % 4), held by the lanes of half
@@ -304,14 +335,14 @@ __global__ __launch_bounds__(512) void k_attention_split(const char* __restrict_
         }
 }
 
-template <int D, int FMT>
-int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
+template <int D, int FMT, bool PF2>
+int launch_split_v(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
     const float scale = (float)(1.0 / std::sqrt((double)D));
     constexpr int DP = (D + 31) / 32 * 32;
     constexpr size_t shm = 2 * ((size_t)128 * attn_ksb(D, FMT >= 1) + 2 * (size_t)DP * (128 / 2 + 4) * 4);
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D, FMT>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_attention_split<D, FMT, PF2>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) {
             set_error("tcx_attention_split: cannot enable %zu B of dynamic LDS", shm);
             return TCX_EHIP;
@@ -326,13 +357,27 @@ int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hi
         const char* e = getenv("TCX_ATTN_DEFER");
         return e ? std::max(0.f, std::min(16.f, (float)atof(e))) : 8.f;
     }();
-    hipLaunchKernelGGL((k_attention_split<D, FMT>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
+    hipLaunchKernelGGL((k_attention_split<D, FMT, PF2>), dim3(N / 256, heads, Bt), dim3(512), shm, st, (const char*)qkv,
                        (char*)out, N, C, scale, xcd, defer2);
     return check_launch("tcx_attention_split");
 }
 
+template <int D, int FMT>
+int launch_split(const void* qkv, void* out, int Bt, int N, int C, int heads, hipStream_t st) {
+    if constexpr (FMT >= 1) {
+        static const bool pf2 = [] {
+            const char* e = getenv("TCX_ATTN_PF2");
+            return !(e && e[0] == '0');
+        }();
+        if (pf2 && N >= 4 * 128) return launch_split_v<D, FMT, true>(qkv, out, Bt, N, C, heads, st);
+    }
+    return launch_split_v<D, FMT, false>(qkv, out, Bt, N, C, heads, st);
+}
+
 #undef TCX_ATT_LOAD
 #undef TCX_ATT_STORE
+#undef TCX_ATT_LOAD_R
+#undef TCX_ATT_STORE_R
 
 }  // namespace
 }  // namespace tcx
