@@ -521,15 +521,19 @@ __global__ __launch_bounds__(256) void k_sk_reduce_ln(const float* __restrict__ 
     const size_t MN = (size_t)M * N;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     // every operand of the row is requested up front (one memory round trip instead of three)
-    float4 h[V], w4[V], b4[V], g4[V], e4[V];
+    // (round 6: the bias and residual rows too -- they were a third round trip after the partial planes)
+    float4 h[V], w4[V], b4[V], g4[V], e4[V], t4[V], r4[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const int n = 4 * tid + 1024 * v;
-        h[v] = w4[v] = b4[v] = g4[v] = e4[v] = z4;
+        h[v] = w4[v] = b4[v] = g4[v] = e4[v] = t4[v] = r4[v] = z4;
         if (n < N) {
             const size_t i = (size_t)m * N + n;
             float4 a = *reinterpret_cast<const float4*>(part + i);
             h[v] = a;
+            // unconditional loads from a valid row (a branch around a load made the compiler wait on it)
+            t4[v] = *reinterpret_cast<const float4*>((e.b ? e.b : ln.lw) + n);
+            r4[v] = *reinterpret_cast<const float4*>((e.resid ? e.resid : part) + i);
             w4[v] = *reinterpret_cast<const float4*>(ln.lw + n);
             b4[v] = *reinterpret_cast<const float4*>(ln.lb + n);
             if (ln.gy) {
@@ -552,19 +556,19 @@ __global__ __launch_bounds__(256) void k_sk_reduce_ln(const float* __restrict__ 
         if (n < N) {
             const size_t i = (size_t)m * N + n;
             float4 a = h[v];
-#pragma unroll 4
-            for (int p = 1; p < S; ++p) {
-                const float4 u = *reinterpret_cast<const float4*>(part + (size_t)p * MN + i);
-                a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+            // partial planes CH at a time, every load of a chunk issued before its adds (the same order of adds)
+            constexpr int CH = V == 1 ? 8 : 2;
+            for (int p0 = 1; p0 < S; p0 += CH) {
+                float4 u[CH];
+#pragma unroll
+                for (int j = 0; j < CH; ++j)  // (past the last plane: a reload of it, never added)
+                    u[j] = *reinterpret_cast<const float4*>(part + (size_t)min(p0 + j, S - 1) * MN + i);
+#pragma unroll
+                for (int j = 0; j < CH; ++j)
+                    if (p0 + j < S) { a.x += u[j].x; a.y += u[j].y; a.z += u[j].z; a.w += u[j].w; }
             }
-            if (e.b) {
-                const float4 t = *reinterpret_cast<const float4*>(e.b + n);
-                a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w;
-            }
-            if (e.resid) {
-                const float4 r4 = *reinterpret_cast<const float4*>(e.resid + i);
-                a.x += r4.x; a.y += r4.y; a.z += r4.z; a.w += r4.w;
-            }
+            if (e.b) { a.x += t4[v].x; a.y += t4[v].y; a.z += t4[v].z; a.w += t4[v].w; }
+            if (e.resid) { a.x += r4[v].x; a.y += r4[v].y; a.z += r4[v].z; a.w += r4[v].w; }
             *reinterpret_cast<float4*>(e.y + i) = a;
             h[v] = a;
             const double a0 = a.x, a1 = a.y, a2 = a.z, a3 = a.w;
