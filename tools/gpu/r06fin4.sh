@@ -8,5 +8,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/${T}_c5prof -o run -- p
 python3 tools/rocpd_layers.py $(find gpurun_out/${T}_c5prof -name "*.db" | head -1) gpurun_out/${T}_cfg5_layers.txt && \
 rm -rf gpurun_out/${T}_c5prof && \
 STEPS=3 WARM=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_ddim -o run -- python3 tools/train_bench.py ddim > gpurun_out/${T}_ddim.log 2>&1 && \
-cp $(find gpurun_out/${T}_ddim -name "*kernel_stats.csv" | head -1) gpurun_out/${T}_ddim_kernel_stats.csv && \
+python3 tools/rocpd_stats.py $(find gpurun_out/${T}_ddim -name "*.db" | head -1) gpurun_out/${T}_ddim_kernel_stats.csv
 rm -rf gpurun_out/${T}_ddim
